@@ -1,0 +1,126 @@
+/* mysti_verify.h — C ABI of the MI355X StatementBlock verification engine.
+ *
+ * Drop-in boundary for the per-block crypto of hrubaanna/mysticeti
+ * (reference @ 2025-02-04). Each entry point names the reference interface it
+ * replaces (paths relative to the reference repo):
+ *
+ *   mv_blake2b256          BlockHasher = blake2::Blake2b<U32> (mysticeti-core/src/crypto.rs:34),
+ *                          as used by BlockDigest::new (crypto.rs:38-61)
+ *   mv_ed25519_verify      PublicKey::verify_block -> ed25519_consensus::VerificationKey::verify
+ *                          (crypto.rs:174-189; ZIP-215 semantics of ed25519-consensus 2.1.0)
+ *   mv_ed25519_sign        Signer::sign_block -> ed25519_consensus::SigningKey::sign
+ *                          (crypto.rs:199-223; RFC 8032)
+ *   mv_set_committee       Committee::get_public_key / stake (committee.rs:56-87); the
+ *                          VerificationKey decode that happens once per authority
+ *   mv_verify_blocks       the loop `for block in blocks { block.verify(&committee) }` of
+ *                          NetworkSyncer::process_blocks (net_sync.rs:331-375) over
+ *                          StatementBlock::verify (types.rs:315-376), on Data<StatementBlock>
+ *                          bincode bytes (data.rs:43-52)
+ *   mv_dev_*               the same computations on device-resident buffers (HBM in, HBM out)
+ *
+ * Conventions
+ *   - The caller owns every buffer passed in and out; they must stay valid for the call.
+ *     The library copies host inputs into its own pinned staging and device memory.
+ *   - Return value: MV_OK (0) or a negative MV_E_* code; mv_last_error() gives text.
+ *     Per-item verdicts go to caller arrays: a rejected signature is not an error.
+ *   - All calls are synchronous and thread-safe on one context (serialised internally).
+ *   - A context spans the devices in mv_config.device_mask; host-buffer calls shard
+ *     their items across them (no collective: each device returns its slice of verdicts).
+ */
+#ifndef MYSTI_VERIFY_H
+#define MYSTI_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mv_ctx mv_ctx;
+typedef int32_t mv_status;
+
+#define MV_OK 0
+#define MV_E_INVALID_ARG (-1)
+#define MV_E_HIP (-2)
+#define MV_E_NO_DEVICE (-3)
+#define MV_E_NO_COMMITTEE (-4)
+#define MV_E_ALLOC (-5)
+
+/* per-signature verdicts (ed25519_consensus::Error mapping) */
+#define MV_SIG_OK 0
+#define MV_SIG_INVALID 1       /* Error::InvalidSignature */
+#define MV_SIG_MALFORMED_KEY 2 /* Error::MalformedPublicKey (A does not decode) */
+
+/* per-block verdicts, in the error order of StatementBlock::verify (types.rs:315-376) */
+#define MV_BLOCK_OK 0
+#define MV_BLOCK_PARSE_ERROR 1             /* bincode::deserialize failed (data.rs:43-52) */
+#define MV_BLOCK_DIGEST_MISMATCH 2         /* "Digest does not match" types.rs:327-332 */
+#define MV_BLOCK_EPOCH_MISMATCH 3          /* types.rs:333-338 */
+#define MV_BLOCK_UNKNOWN_AUTHOR 4          /* types.rs:339-342 */
+#define MV_BLOCK_GENESIS 5                 /* types.rs:343-345 */
+#define MV_BLOCK_SIG_INVALID 6             /* types.rs:346-348 */
+#define MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY 7 /* types.rs:350-355 */
+#define MV_BLOCK_INCLUDE_ROUND 8           /* types.rs:356-361 */
+#define MV_BLOCK_VOTE_RANGE 9              /* types.rs:363-370, 440-460 */
+#define MV_BLOCK_THRESHOLD_CLOCK 10        /* types.rs:371-374, threshold_clock.rs:12-35 */
+
+typedef struct mv_config {
+  uint32_t device_mask; /* bit i = use HIP device i; 0 = device 0 only */
+  uint32_t max_batch;   /* items per device launch chunk; 0 = default (1<<20) */
+  uint32_t flags;       /* reserved, 0 */
+} mv_config;
+
+mv_status mv_create(const mv_config* cfg, mv_ctx** out);
+void mv_destroy(mv_ctx* ctx);
+const char* mv_last_error(const mv_ctx* ctx);
+/* library version string, e.g. "mysti_verify 0.1 gfx950" */
+const char* mv_version(void);
+
+/* Committee: n authority keys (32-byte encodings) and stakes, committee epoch.
+ * key_ok[i] (optional) receives 1 if key i decodes (VerificationKey::try_from). */
+mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks /* n x 32 */, const uint64_t* stakes, uint32_t n,
+                           uint64_t epoch, uint8_t* key_ok /* n, may be NULL */);
+
+/* Blake2b-256 of n byte strings buf[off[i] .. off[i]+len[i]) -> out[i] (32 B each). */
+mv_status mv_blake2b256(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                        uint8_t* out /* n x 32 */);
+
+/* ZIP-215 ed25519 verification of n signatures over 32-byte messages.
+ * Keys: pk[i] if key_idx == NULL, else committee key key_idx[i] (pk must be NULL). */
+mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg /* n x 32 */, const uint8_t* sig /* n x 64 */,
+                            const uint8_t* pk /* n x 32 or NULL */, const uint32_t* key_idx /* n or NULL */,
+                            uint32_t n, uint8_t* status /* n, MV_SIG_* */);
+
+/* RFC 8032 signing of n 32-byte messages with n 32-byte seeds -> pk (n x 32), sig (n x 64). */
+mv_status mv_ed25519_sign(mv_ctx* ctx, const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk,
+                          uint8_t* sig);
+
+/* StatementBlock::verify on n bincode-serialized blocks buf[off[i] .. off[i]+len[i]).
+ * status[i] = MV_BLOCK_*; msg_digest[i] = Blake2b-256(pre-image) (the signed message),
+ * block_digest[i] = Blake2b-256(pre-image || signature); either digest array may be NULL.
+ * Requires mv_set_committee. */
+mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                           uint8_t* status, uint8_t* msg_digest, uint8_t* block_digest);
+
+/* Host-only helper (no device needed): the signed pre-image of one bincode block
+ * (BlockDigest::digest_without_signature, crypto.rs:85-128). Returns the pre-image
+ * length, or -1 if the bytes do not deserialize. `out` may be NULL to query the length. */
+int64_t mv_block_preimage(const uint8_t* bincode, uint64_t len, uint8_t* out, uint64_t cap);
+
+/* ---- device-resident variants (inputs already in HBM of `device`) ----
+ * Pointers are device pointers, 16-byte aligned; `stream` is a hipStream_t (NULL = the
+ * library's stream for that device). They enqueue work and return without synchronising. */
+mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
+                                const uint8_t* d_pk, uint32_t n, uint8_t* d_status, void* stream);
+mv_status mv_dev_ed25519_sign(mv_ctx* ctx, int device, const uint8_t* d_seed, const uint8_t* d_msg, uint32_t n,
+                              uint8_t* d_pk, uint8_t* d_sig, void* stream);
+
+/* ---- diagnostics (used by the test-suite) ---- */
+/* Runs field/scalar primitive `op` on n lane inputs (16 words each) -> 16 words each (host buffers). */
+mv_status mv_selftest(mv_ctx* ctx, int op, const uint32_t* in, uint32_t n, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MYSTI_VERIFY_H */

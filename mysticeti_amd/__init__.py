@@ -1,0 +1,233 @@
+"""mysticeti_amd — MI355X (gfx950) StatementBlock verification engine.
+
+Python host binding of libmysti_verify.so (C ABI: include/mysti_verify.h). The
+GPU path is the only path: importing works without a GPU, but every compute call
+goes through the HIP library and raises if it (or a device) is missing — there is
+no CPU fallback.
+
+Reference interfaces mirrored (hrubaanna/mysticeti @ 2025-02-04):
+  Engine.verify_blocks     NetworkSyncer::process_blocks' per-block StatementBlock::verify
+                           (net_sync.rs:331-375, types.rs:315-376)
+  Engine.ed25519_verify    PublicKey::verify_block -> VerificationKey::verify (crypto.rs:174-189)
+  Engine.ed25519_sign      Signer::sign_block (crypto.rs:199-223)
+  Engine.blake2b256        BlockHasher (crypto.rs:34)
+  crypto.*                 thin reference-named wrappers (BlockDigest, PublicKey, Signer, ...)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmysti_verify.so")
+
+MV_OK = 0
+SIG_OK, SIG_INVALID, SIG_MALFORMED_KEY = 0, 1, 2
+BLOCK_STATUS = [
+    "OK", "PARSE_ERROR", "DIGEST_MISMATCH", "EPOCH_MISMATCH", "UNKNOWN_AUTHOR", "GENESIS", "SIG_INVALID",
+    "INCLUDE_UNKNOWN_AUTHORITY", "INCLUDE_ROUND", "VOTE_RANGE", "THRESHOLD_CLOCK",
+]
+(BLOCK_OK, BLOCK_PARSE_ERROR, BLOCK_DIGEST_MISMATCH, BLOCK_EPOCH_MISMATCH, BLOCK_UNKNOWN_AUTHOR,
+ BLOCK_GENESIS, BLOCK_SIG_INVALID, BLOCK_INCLUDE_UNKNOWN_AUTHORITY, BLOCK_INCLUDE_ROUND,
+ BLOCK_VOTE_RANGE, BLOCK_THRESHOLD_CLOCK) = range(11)
+
+EXPORTS = [
+    "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",
+    "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
+    "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage",
+]
+
+
+class MvError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device_mask", ctypes.c_uint32), ("max_batch", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libmysti_verify.so (in-tree). Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise MvError(f"{path} missing: build it with `python -m mysticeti_amd.build` (no CPU fallback exists)")
+    lib = ctypes.CDLL(path)
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    lib.mv_create.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(vp)]
+    lib.mv_destroy.argtypes = [vp]
+    lib.mv_destroy.restype = None
+    lib.mv_last_error.argtypes = [vp]
+    lib.mv_last_error.restype = ctypes.c_char_p
+    lib.mv_version.restype = ctypes.c_char_p
+    lib.mv_set_committee.argtypes = [vp, vp, vp, u32, u64, vp]
+    lib.mv_blake2b256.argtypes = [vp, vp, vp, vp, u32, vp]
+    lib.mv_ed25519_verify.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+    lib.mv_ed25519_sign.argtypes = [vp, vp, vp, u32, vp, vp]
+    lib.mv_verify_blocks.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
+    lib.mv_dev_ed25519_verify.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
+    lib.mv_dev_ed25519_sign.argtypes = [vp, ctypes.c_int, vp, vp, u32, vp, vp, vp]
+    lib.mv_selftest.argtypes = [vp, ctypes.c_int, vp, u32, vp]
+    lib.mv_block_preimage.argtypes = [vp, u64, vp, u64]
+    lib.mv_block_preimage.restype = ctypes.c_int64
+    for name in EXPORTS:
+        getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int32
+    _lib = lib
+    return lib
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _u8(a, shape_tail: int) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.uint8))
+    return a.reshape(-1, shape_tail)
+
+
+class Engine:
+    """One mv_ctx: the devices it shards over, their streams and buffers."""
+
+    def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0):
+        self.lib = load_library()
+        mask = 0
+        for d in devices:
+            mask |= 1 << int(d)
+        cfg = _Config(mask, max_batch, 0)
+        h = ctypes.c_void_p()
+        rc = self.lib.mv_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != MV_OK:
+            raise MvError(f"mv_create failed ({rc}): no usable gfx950 device")
+        self.ctx = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.mv_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != MV_OK:
+            raise MvError(f"{what} failed ({rc}): {self.lib.mv_last_error(self.ctx).decode()}")
+
+    # ---- committee ----
+    def set_committee(self, pks, stakes, epoch: int = 0) -> np.ndarray:
+        pks = _u8(pks, 32)
+        stakes = np.ascontiguousarray(np.asarray(stakes, dtype=np.uint64))
+        ok = np.zeros(pks.shape[0], dtype=np.uint8)
+        self._check(self.lib.mv_set_committee(self.ctx, _p(pks), _p(stakes), pks.shape[0], epoch, _p(ok)),
+                    "mv_set_committee")
+        return ok
+
+    # ---- hashes ----
+    def blake2b256(self, items: Sequence[bytes]) -> List[bytes]:
+        n = len(items)
+        lens = np.array([len(x) for x in items], dtype=np.uint64)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            offs[1:] = np.cumsum(lens)[:-1]
+        buf = np.frombuffer(b"".join(items) + b"\0", dtype=np.uint8)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.lib.mv_blake2b256(self.ctx, _p(buf), _p(offs), _p(lens), n, _p(out)), "mv_blake2b256")
+        return [bytes(r) for r in out]
+
+    # ---- signatures ----
+    def ed25519_verify(self, msg, sig, pk=None, key_idx=None) -> np.ndarray:
+        msg, sig = _u8(msg, 32), _u8(sig, 64)
+        n = msg.shape[0]
+        pk_a = _u8(pk, 32) if pk is not None else None
+        ki = np.ascontiguousarray(np.asarray(key_idx, dtype=np.uint32)) if key_idx is not None else None
+        st = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.mv_ed25519_verify(self.ctx, _p(msg), _p(sig), _p(pk_a), _p(ki), n, _p(st)),
+                    "mv_ed25519_verify")
+        return st
+
+    def ed25519_sign(self, seed, msg) -> Tuple[np.ndarray, np.ndarray]:
+        seed, msg = _u8(seed, 32), _u8(msg, 32)
+        n = seed.shape[0]
+        pk = np.zeros((n, 32), dtype=np.uint8)
+        sig = np.zeros((n, 64), dtype=np.uint8)
+        self._check(self.lib.mv_ed25519_sign(self.ctx, _p(seed), _p(msg), n, _p(pk), _p(sig)), "mv_ed25519_sign")
+        return pk, sig
+
+    # ---- blocks ----
+    def verify_blocks(self, blocks: Sequence[bytes]):
+        """StatementBlock::verify for each bincode Data<StatementBlock>: (status, msg_digest, block_digest)."""
+        n = len(blocks)
+        lens = np.array([len(b) for b in blocks], dtype=np.uint64)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            offs[1:] = np.cumsum(lens)[:-1]
+        buf = np.frombuffer(b"".join(blocks) + b"\0", dtype=np.uint8)
+        return self.verify_blocks_packed(buf, offs, lens)
+
+    def verify_blocks_packed(self, buf: np.ndarray, offs: np.ndarray, lens: np.ndarray):
+        n = offs.shape[0]
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        st = np.zeros(n, dtype=np.uint8)
+        md = np.zeros((n, 32), dtype=np.uint8)
+        bd = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.lib.mv_verify_blocks(self.ctx, _p(buf), _p(offs), _p(lens), n, _p(st), _p(md), _p(bd)),
+                    "mv_verify_blocks")
+        return st, md, bd
+
+    # ---- device-resident (torch tensors on the device) ----
+    def dev_verify(self, device: int, d_msg, d_sig, d_pk, d_status, stream_handle: int = 0):
+        n = d_msg.shape[0]
+        self._check(self.lib.mv_dev_ed25519_verify(self.ctx, device, ctypes.c_void_p(d_msg.data_ptr()),
+                                                   ctypes.c_void_p(d_sig.data_ptr()), ctypes.c_void_p(d_pk.data_ptr()),
+                                                   n, ctypes.c_void_p(d_status.data_ptr()),
+                                                   ctypes.c_void_p(stream_handle or None)),
+                    "mv_dev_ed25519_verify")
+
+    def dev_sign(self, device: int, d_seed, d_msg, d_pk, d_sig, stream_handle: int = 0):
+        n = d_seed.shape[0]
+        self._check(self.lib.mv_dev_ed25519_sign(self.ctx, device, ctypes.c_void_p(d_seed.data_ptr()),
+                                                 ctypes.c_void_p(d_msg.data_ptr()), n,
+                                                 ctypes.c_void_p(d_pk.data_ptr()), ctypes.c_void_p(d_sig.data_ptr()),
+                                                 ctypes.c_void_p(stream_handle or None)),
+                    "mv_dev_ed25519_sign")
+
+    # ---- diagnostics ----
+    def selftest(self, op: int, words: np.ndarray) -> np.ndarray:
+        w = np.ascontiguousarray(np.asarray(words, dtype=np.uint32)).reshape(-1, 16)
+        out = np.zeros_like(w)
+        self._check(self.lib.mv_selftest(self.ctx, op, _p(w), w.shape[0], _p(out)), "mv_selftest")
+        return out
+
+
+def block_preimage(bincode: bytes) -> Optional[bytes]:
+    """Host-side pre-image of one bincode StatementBlock (None if it does not deserialize)."""
+    lib = load_library()
+    b = np.frombuffer(bincode + b"\0", dtype=np.uint8)
+    n = lib.mv_block_preimage(_p(b), len(bincode), None, 0)
+    if n < 0:
+        return None
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    lib.mv_block_preimage(_p(b), len(bincode), _p(out), n)
+    return out[:n].tobytes()
+
+
+def version() -> str:
+    return load_library().mv_version().decode()

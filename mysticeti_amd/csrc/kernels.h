@@ -1,0 +1,20 @@
+// Host-side launchers for kernels.hip (internal to libmysti_verify.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mvk {
+size_t verify_scratch_bytes(uint32_t n);
+size_t btable_bytes();
+hipError_t launch_btable_init(void* d_btab, hipStream_t s);
+hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                         uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s);
+hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
+                       uint8_t* sig, hipStream_t s);
+hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+                          hipStream_t s);
+hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                             uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
+hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s);
+}  // namespace mvk

@@ -1,0 +1,525 @@
+// HIP kernels of the StatementBlock verification engine (gfx950 only).
+//
+//   k_btable_init    fixed-base table [j]B, j = 0..128, affine (y+x, y-x, 2dxy)
+//   k_verify         ZIP-215 ed25519 verify, one signature per lane (ed25519-consensus
+//                    VerificationKey::verify, called at mysticeti-core/src/crypto.rs:188)
+//   k_sign           RFC 8032 signing, one per lane (crypto.rs:199-223, corpus generation)
+//   k_blake2b        Blake2b-256 of staged byte strings (crypto.rs:34 BlockHasher)
+//   k_block_hash     signed message Blake2b(P) and block digest Blake2b(P || sig) of
+//                    staged pre-images, sharing the common compressions
+//                    (crypto.rs:38-61 and crypto.rs:174-187)
+//   k_selftest       field / scalar primitives for the parity tests
+//
+// The verify kernel is INT32-VALU bound: HBM traffic is 128 B of
+// input per signature plus the per-lane variable-base table (9 cached points,
+// written once, read 64 times, L2/MALL-resident per wave).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fe25519.h"
+#include "ge25519.h"
+#include "hash_dev.h"
+#include "kernels.h"
+#include "scalar25519.h"
+
+namespace mv {
+
+// ---------------------------------------------------------------- tables
+constexpr int BT_ENTRIES = 129;  // [0..128]B
+constexpr int BT_QUADS = 6;      // 3 fe x 2 uint4
+constexpr int AT_ENTRIES = 9;    // [0..8](-A)
+constexpr int AT_QUADS = 8;      // 4 fe x 2 uint4
+
+MV_DEV uint4 q4(const fe& f, int h) {
+  return make_uint4(f.v[4 * h], f.v[4 * h + 1], f.v[4 * h + 2], f.v[4 * h + 3]);
+}
+MV_DEV void uq4(fe& f, int h, uint4 q) {
+  f.v[4 * h] = q.x;
+  f.v[4 * h + 1] = q.y;
+  f.v[4 * h + 2] = q.z;
+  f.v[4 * h + 3] = q.w;
+}
+
+MV_DEV void lds_btab_load(uint4* sm, const uint4* g) {
+  for (int i = threadIdx.x; i < BT_ENTRIES * BT_QUADS; i += blockDim.x) sm[i] = g[i];
+  __syncthreads();
+}
+// B-table lookup with sign: digit in [-128, 128]
+MV_DEV void btab_get(precomp& p, const uint4* sm, int digit) {
+  int e = digit < 0 ? -digit : digit;
+  const uint4* q = sm + e * BT_QUADS;
+  uq4(p.ypx, 0, q[0]);
+  uq4(p.ypx, 1, q[1]);
+  uq4(p.ymx, 0, q[2]);
+  uq4(p.ymx, 1, q[3]);
+  uq4(p.xy2d, 0, q[4]);
+  uq4(p.xy2d, 1, q[5]);
+  precomp_cneg(p, digit < 0);
+}
+
+// Per-wave A-table scratch: [entry][quad][lane] of uint4, lanes contiguous so the
+// table build writes 1 KiB per wave-instruction and lookups touch <= 9 segments.
+MV_DEV void atab_put(uint4* wave_base, int e, int lane, const cached& c) {
+  uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
+  p[0 * 64] = q4(c.YpX, 0);
+  p[1 * 64] = q4(c.YpX, 1);
+  p[2 * 64] = q4(c.YmX, 0);
+  p[3 * 64] = q4(c.YmX, 1);
+  p[4 * 64] = q4(c.Z, 0);
+  p[5 * 64] = q4(c.Z, 1);
+  p[6 * 64] = q4(c.T2d, 0);
+  p[7 * 64] = q4(c.T2d, 1);
+}
+MV_DEV void atab_get(cached& c, const uint4* wave_base, int lane, int digit) {
+  int e = digit < 0 ? -digit : digit;
+  const uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
+  uq4(c.YpX, 0, p[0 * 64]);
+  uq4(c.YpX, 1, p[1 * 64]);
+  uq4(c.YmX, 0, p[2 * 64]);
+  uq4(c.YmX, 1, p[3 * 64]);
+  uq4(c.Z, 0, p[4 * 64]);
+  uq4(c.Z, 1, p[5 * 64]);
+  uq4(c.T2d, 0, p[6 * 64]);
+  uq4(c.T2d, 1, p[7 * 64]);
+  cached_cneg(c, digit < 0);
+}
+
+MV_DEV void load8(uint32_t w[8], const uint8_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+MV_DEV void store8(uint8_t* p, const uint32_t w[8]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// encode a point: y with the sign of x in bit 255
+MV_DEV void p3_compress(uint32_t out[8], const p3& p) {
+  fe zi, x, y;
+  fe_invert(zi, p.Z);
+  fe_mul(x, p.X, zi);
+  fe_mul(y, p.Y, zi);
+  fe_canon(x, x);
+  fe_canon(y, y);
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = y.v[i];
+  out[7] |= (x.v[0] & 1u) << 31;
+}
+
+// [s]B for s < 2^253 given as signed radix-256 digits (LDS table)
+MV_DEV void basemul(p3& out, const uint32_t sd[8], const uint4* btab) {
+  p2 P;
+  p2_identity(P);
+  p3 P3;
+  p1p1 Q;
+  precomp pre;
+  for (int w = 31; w >= 0; w--) {
+    if (w != 31) {
+      for (int i = 0; i < 7; i++) {
+        p2_dbl(Q, P);
+        p1p1_to_p2(P, Q);
+      }
+      p2_dbl(Q, P);
+      p1p1_to_p3(P3, Q);
+    } else {
+      p3_identity(P3);
+    }
+    btab_get(pre, btab, digit256(sd, w));
+    p3_add_precomp(Q, P3, pre);
+    if (w != 0) p1p1_to_p2(P, Q);
+  }
+  p1p1_to_p3(out, Q);
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= BT_ENTRIES) return;
+  // B = decompress(4/5, sign 0)
+  const uint32_t by[8] = {0x66666658, 0x66666666, 0x66666666, 0x66666666,
+                          0x66666666, 0x66666666, 0x66666666, 0x66666666};
+  p3 B, R;
+  bool okB, okR;
+  decompress_x2(B, okB, by, R, okR, by);
+  p3 acc;
+  p3_identity(acc);
+  cached cb;
+  p3_to_cached(cb, B);
+  for (int i = 0; i < j; i++) {
+    p1p1 t;
+    p3_add_cached(t, acc, cb);
+    p1p1_to_p3(acc, t);
+  }
+  fe zi, x, y, xy, d2;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_const(d2, K_D2);
+  precomp pc;
+  fe_add(pc.ypx, y, x);
+  fe_sub(pc.ymx, y, x);
+  fe_mul(xy, x, y);
+  fe_mul(pc.xy2d, xy, d2);
+  fe_canon(pc.ypx, pc.ypx);
+  fe_canon(pc.ymx, pc.ymx);
+  fe_canon(pc.xy2d, pc.xy2d);
+  uint4* o = out + j * BT_QUADS;
+  o[0] = q4(pc.ypx, 0);
+  o[1] = q4(pc.ypx, 1);
+  o[2] = q4(pc.ymx, 0);
+  o[3] = q4(pc.ymx, 1);
+  o[4] = q4(pc.xy2d, 0);
+  o[5] = q4(pc.xy2d, 1);
+}
+
+// One signature per lane. pk rows are read at key_idx[i] when key_idx != nullptr.
+__global__ void __launch_bounds__(256, 2)
+    k_verify(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
+             const uint32_t* __restrict__ key_idx, uint32_t n, const uint4* __restrict__ btab_g,
+             uint4* __restrict__ scratch, uint8_t* __restrict__ status) {
+  __shared__ uint4 btab[BT_ENTRIES * BT_QUADS];
+  lds_btab_load(btab, btab_g);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t idx = gid < n ? gid : n - 1;
+  const int lane = threadIdx.x & 63;
+  uint4* wave_tab = scratch + (size_t)(gid >> 6) * (AT_ENTRIES * AT_QUADS * 64);
+
+  uint32_t aw[8], rw[8], sw[8], mw[8];
+  load8(aw, pk + 32 * (size_t)(key_idx ? key_idx[idx] : idx));
+  load8(rw, sig + 64 * (size_t)idx);
+  load8(sw, sig + 64 * (size_t)idx + 32);
+  load8(mw, msg + 32 * (size_t)idx);
+
+  const bool s_ok = sc_is_canonical(sw);
+  p3 A, R;
+  bool okA, okR;
+  decompress_x2(A, okA, aw, R, okR, rw);
+
+  // k = SHA-512(R || A || M) mod l over the original encodings
+  uint32_t kin[24], h[16], k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    kin[i] = rw[i];
+    kin[8 + i] = aw[i];
+    kin[16 + i] = mw[i];
+  }
+  sha512_short(h, kin, 96);
+  sc_reduce512(k, h);
+  uint32_t kd[8], sd[8];
+  sc_recode16(kd, k);
+  sc_recode256(sd, sw);
+
+  // variable-base table [j](-A), j = 0..8
+  {
+    p3 nA, cur;
+    p3_neg(nA, A);
+    cached c1, c;
+    cached_identity(c);
+    atab_put(wave_tab, 0, lane, c);
+    p3_to_cached(c1, nA);
+    atab_put(wave_tab, 1, lane, c1);
+    cur = nA;
+    for (int j = 2; j <= 8; j++) {
+      p1p1 t;
+      p3_add_cached(t, cur, c1);
+      p1p1_to_p3(cur, t);
+      p3_to_cached(c, cur);
+      atab_put(wave_tab, j, lane, c);
+    }
+  }
+
+  // Straus: R' = [k](-A) + [s]B, 4-bit windows for k, 8-bit windows for s
+  p2 P;
+  p3 P3;
+  p1p1 Q;
+  cached ca;
+  precomp pb;
+  for (int w = 63; w >= 0; w--) {
+    atab_get(ca, wave_tab, lane, digit16(kd, w));  // issued ahead of the doublings
+    if (w != 63) {
+      for (int i = 0; i < 3; i++) {
+        p2_dbl(Q, P);
+        p1p1_to_p2(P, Q);
+      }
+      p2_dbl(Q, P);
+      p1p1_to_p3(P3, Q);
+    } else {
+      p3_identity(P3);
+    }
+    p3_add_cached(Q, P3, ca);
+    if ((w & 1) == 0) {
+      p1p1_to_p3(P3, Q);
+      btab_get(pb, btab, digit256(sd, w >> 1));
+      p3_add_precomp(Q, P3, pb);
+    }
+    p1p1_to_p2(P, Q);
+  }
+  // cofactored check: [8](R - R') == identity
+  p3 Rp;
+  p1p1_to_p3(Rp, Q);
+  p3 nRp;
+  p3_neg(nRp, Rp);
+  cached cR;
+  p3_to_cached(cR, nRp);
+  p3_add_cached(Q, R, cR);
+  p1p1_to_p2(P, Q);
+  for (int i = 0; i < 3; i++) {
+    p2_dbl(Q, P);
+    p1p1_to_p2(P, Q);
+  }
+  const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
+  if (gid < n) {
+    uint8_t st = !okA ? 2 : ((s_ok && okR && ident) ? 0 : 1);
+    status[gid] = st;
+  }
+}
+
+// RFC 8032: (pk, R || S) from (seed, 32-byte msg)
+__global__ void __launch_bounds__(256, 2)
+    k_sign(const uint8_t* __restrict__ seed, const uint8_t* __restrict__ msg, uint32_t n,
+           const uint4* __restrict__ btab_g, uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sig_out) {
+  __shared__ uint4 btab[BT_ENTRIES * BT_QUADS];
+  lds_btab_load(btab, btab_g);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t idx = gid < n ? gid : n - 1;
+  uint32_t sw[8], mw[8], h[16];
+  load8(sw, seed + 32 * (size_t)idx);
+  load8(mw, msg + 32 * (size_t)idx);
+  sha512_short(h, sw, 32);
+  uint32_t a[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = h[i];
+  a[0] &= 0xfffffff8u;
+  a[7] = (a[7] & 0x7fffffffu) | 0x40000000u;
+#pragma unroll
+  for (int i = 8; i < 16; i++) a[i] = 0;
+  uint32_t ared[8], sd[8];
+  sc_reduce512(ared, a);  // [a]B == [a mod l]B keeps the top digit in range
+  sc_recode256(sd, ared);
+  p3 P;
+  basemul(P, sd, btab);
+  uint32_t pkw[8];
+  p3_compress(pkw, P);
+  // r = SHA-512(prefix || M) mod l
+  uint32_t rin[16], rh[16], r[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    rin[i] = h[8 + i];
+    rin[8 + i] = mw[i];
+  }
+  sha512_short(rh, rin, 64);
+  sc_reduce512(r, rh);
+  sc_recode256(sd, r);
+  basemul(P, sd, btab);
+  uint32_t Rw[8];
+  p3_compress(Rw, P);
+  uint32_t kin[24], kh[16], k[8], S[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    kin[i] = Rw[i];
+    kin[8 + i] = pkw[i];
+    kin[16 + i] = mw[i];
+  }
+  sha512_short(kh, kin, 96);
+  sc_reduce512(k, kh);
+  sc_muladd(S, k, ared, r);
+  if (gid < n) {
+    store8(pk_out + 32 * (size_t)gid, pkw);
+    store8(sig_out + 64 * (size_t)gid, Rw);
+    store8(sig_out + 64 * (size_t)gid + 32, S);
+  }
+}
+
+// Load message words [b*16, b*16+16) of a byte string at 8-aligned `p`, zeroing bytes >= lim.
+MV_DEV void b2_load_block(uint64_t m[16], const uint8_t* p, uint64_t blk, uint64_t lim) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p) + blk * 16;
+  const uint64_t base = blk * 128;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    uint64_t pos = base + 8 * j;
+    uint64_t v = 0;
+    if (pos < lim) {
+      v = q[j];
+      uint64_t rem = lim - pos;
+      if (rem < 8) v &= (1ULL << (8 * rem)) - 1;
+    }
+    m[j] = v;
+  }
+}
+MV_DEV void b2_store256(uint8_t* out, const uint64_t h[8]) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    w[2 * i] = (uint32_t)h[i];
+    w[2 * i + 1] = (uint32_t)(h[i] >> 32);
+  }
+  store8(out, w);
+}
+
+// Blake2b-256 of n staged strings (each 8-aligned, readable up to round-up(len, 8)).
+__global__ void __launch_bounds__(256) k_blake2b(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                                                 const uint64_t* __restrict__ len, uint32_t n,
+                                                 uint8_t* __restrict__ out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  const uint8_t* p = buf + off[gid];
+  const uint64_t L = len[gid];
+  uint64_t h[8], m[16];
+  b2_init256(h);
+  const uint64_t nb = L == 0 ? 1 : (L + 127) / 128;
+  for (uint64_t b = 0; b + 1 < nb; b++) {
+    b2_load_block(m, p, b, L);
+    b2_compress(h, m, 128 * (b + 1), false);
+  }
+  b2_load_block(m, p, nb - 1, L);
+  b2_compress(h, m, L, true);
+  b2_store256(out + 32 * (size_t)gid, h);
+}
+
+// Staged P || sig (8-aligned, len[i] = |P|): msg = B2(P), digest = B2(P || sig).
+__global__ void __launch_bounds__(256) k_block_hash(const uint8_t* __restrict__ buf,
+                                                    const uint64_t* __restrict__ off,
+                                                    const uint64_t* __restrict__ len, uint32_t n,
+                                                    uint8_t* __restrict__ msg_out, uint8_t* __restrict__ dig_out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  const uint8_t* p = buf + off[gid];
+  const uint64_t L = len[gid];
+  uint64_t h[8], m[16];
+  b2_init256(h);
+  const uint64_t common = L == 0 ? 0 : (L - 1) / 128;  // non-final in both hashes
+  for (uint64_t b = 0; b < common; b++) {
+    b2_load_block(m, p, b, L + 64);
+    b2_compress(h, m, 128 * (b + 1), false);
+  }
+  uint64_t hm[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) hm[i] = h[i];
+  b2_load_block(m, p, common, L);
+  b2_compress(hm, m, L, true);
+  b2_store256(msg_out + 32 * (size_t)gid, hm);
+  const uint64_t LD = L + 64;
+  const uint64_t last = (LD - 1) / 128;
+  for (uint64_t b = common; b < last; b++) {
+    b2_load_block(m, p, b, LD);
+    b2_compress(h, m, 128 * (b + 1), false);
+  }
+  b2_load_block(m, p, last, LD);
+  b2_compress(h, m, LD, true);
+  b2_store256(dig_out + 32 * (size_t)gid, h);
+}
+
+// Field / scalar primitives on 16-word lane inputs (parity tests).
+__global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restrict__ in, uint32_t n,
+                                                 const uint4* __restrict__ btab_g, uint32_t* __restrict__ out) {
+  __shared__ uint4 btab[BT_ENTRIES * BT_QUADS];
+  lds_btab_load(btab, btab_g);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  uint32_t x[16], y[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    x[i] = in[16 * (size_t)gid + i];
+    y[i] = 0;
+  }
+  fe a, b, r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.v[i] = x[i];
+    b.v[i] = x[8 + i];
+  }
+  switch (op) {
+    case 0: fe_mul(r, a, b); fe_canon(r, r); break;
+    case 1: fe_sq(r, a); fe_canon(r, r); break;
+    case 2: fe_add(r, a, b); fe_canon(r, r); break;
+    case 3: fe_sub(r, a, b); fe_canon(r, r); break;
+    case 4: fe_invert(r, a); fe_canon(r, r); break;
+    case 5: fe_pow_p58(r, a); fe_canon(r, r); break;
+    case 6: fe_mul_small(r, a, b.v[0]); fe_canon(r, r); break;
+    case 7: {  // ZIP-215 decode of a: x (canonical) and the ok flag in word 8
+      p3 A, B;
+      bool oa, ob;
+      decompress_x2(A, oa, x, B, ob, x);
+      fe_canon(r, A.X);
+      y[8] = oa ? 1u : 0u;
+      break;
+    }
+    case 8: sc_reduce512(r.v, x); break;
+    case 9: {  // sha512 of 64 bytes
+      sha512_short(y, x, 64);
+#pragma unroll
+      for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
+      return;
+    }
+    case 10: fe_set(r, sc_is_canonical(x) ? 1 : 0); break;
+    case 11: {  // [a]B encoding for a scalar a < 2^253
+      uint32_t sd[8];
+      sc_recode256(sd, x);
+      p3 P;
+      basemul(P, sd, btab);
+      p3_compress(r.v, P);
+      break;
+    }
+    case 12: {  // fe_canon of raw 255-bit input
+      fe_from_words(r, x);
+      fe_canon(r, r);
+      break;
+    }
+    default: fe_set(r, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) y[i] = r.v[i];
+#pragma unroll
+  for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
+}
+
+}  // namespace mv
+
+// ---------------------------------------------------------------- launchers
+namespace mvk {
+
+size_t verify_scratch_bytes(uint32_t n) {
+  size_t waves = (size_t)((n + 255) / 256) * 4;  // every wave of the 256-thread grid owns a slot
+  return waves * mv::AT_ENTRIES * mv::AT_QUADS * 64 * sizeof(uint4);
+}
+size_t btable_bytes() { return mv::BT_ENTRIES * mv::BT_QUADS * sizeof(uint4); }
+
+hipError_t launch_btable_init(void* d_btab, hipStream_t s) {
+  hipLaunchKernelGGL(mv::k_btable_init, dim3(1), dim3(256), 0, s, (uint4*)d_btab);
+  return hipGetLastError();
+}
+hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                         uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_verify, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
+                     (const uint4*)btab, (uint4*)scratch, status);
+  return hipGetLastError();
+}
+hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
+                       uint8_t* sig, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_sign, dim3((n + 255) / 256), dim3(256), 0, s, seed, msg, n, (const uint4*)btab, pk, sig);
+  return hipGetLastError();
+}
+hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+                          hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_blake2b, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                             uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_block_hash, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, msg_out, dig_out);
+  return hipGetLastError();
+}
+hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_selftest, dim3((n + 63) / 64), dim3(64), 0, s, op, in, n, (const uint4*)btab, out);
+  return hipGetLastError();
+}
+
+}  // namespace mvk

@@ -1,0 +1,35 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))  # tests use the oracle as the checker
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built HIP library")
+    config.addinivalue_line("markers", "slow: large-batch case")
+
+
+@pytest.fixture(scope="session")
+def engine():
+    import mysticeti_amd as M
+
+    eng = M.Engine(devices=(0,))
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    d = os.path.join(ROOT, "tests", "golden")
+
+    def load(name):
+        with open(os.path.join(d, name)) as f:
+            return json.load(f)
+
+    return load

@@ -1,0 +1,85 @@
+"""GPU: StatementBlock::verify through mv_verify_blocks — statuses in the reference's error
+order (types.rs:315-376) and both Blake2b digests bit-exact vs the fixtures and the oracle."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import blocks as B
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def committee_arrays(c):
+    pks = np.frombuffer(b"".join(bytes.fromhex(x) for x in c["pks"]), dtype=np.uint8).reshape(-1, 32)
+    return pks, np.array(c["stakes"], dtype=np.uint64), c["epoch"]
+
+
+def test_block_edge_cases(engine, golden):
+    e = golden("block_edge.json")
+    pks, stakes, epoch = committee_arrays(e["committee"])
+    ok = engine.set_committee(pks, stakes, epoch)
+    assert ok.all()
+    blocks = [bytes.fromhex(c["bincode"]) for c in e["cases"]]
+    st, md, bd = engine.verify_blocks(blocks)
+    for c, s, b, m, d in zip(e["cases"], st, blocks, md, bd):
+        assert int(s) == c["status"], c["note"]
+        if c["status"] != 1:
+            ost, omd, obd = O.block_verify(b, pks, stakes, epoch)
+            assert m.tobytes() == omd and d.tobytes() == obd, c["note"]
+
+
+def test_config1_4096_blocks(engine, golden):
+    g = golden("blocks_config1.json")
+    pks, stakes, epoch = committee_arrays(g["committee"])
+    engine.set_committee(pks, stakes, epoch)
+    blks = B.gen_config1(O.sign)
+    bins = [b.bincode() for b in blks]
+    assert hashlib.sha256(b"".join(bins)).hexdigest() == g["sha256_bincode_concat"]
+    st, md, bd = engine.verify_blocks(bins)
+    assert (st == 0).all()
+    assert hashlib.sha256(md.tobytes()).hexdigest() == g["sha256_msg_digests"]
+    assert hashlib.sha256(bd.tobytes()).hexdigest() == g["sha256_block_digests"]
+
+
+def test_config4_shape_blocks(engine, golden):
+    g = golden("blocks_config4_sample.json")
+    pks, stakes, epoch = committee_arrays(g["committee"])
+    engine.set_committee(pks, stakes, epoch)
+    blks = B.gen_config4(O.sign, rounds=2)
+    bins = [b.bincode() for b in blks]
+    st, md, bd = engine.verify_blocks(bins)
+    assert (st == 0).all()
+    assert hashlib.sha256(md.tobytes()).hexdigest() == g["sha256_msg_digests"]
+    assert hashlib.sha256(bd.tobytes()).hexdigest() == g["sha256_block_digests"]
+
+
+def test_mixed_lengths_and_failures(engine):
+    """Ragged pre-image lengths in one wave (41 B .. ~9 KB) with failures mixed in."""
+    seeds = [B.authority_seed(a) for a in range(7)]
+    pks = np.frombuffer(b"".join(O.public_key(s) for s in seeds), dtype=np.uint8).reshape(-1, 32)
+    stakes = np.array([3, 1, 1, 2, 1, 1, 1], dtype=np.uint64)
+    engine.set_committee(pks, stakes, 0)
+    prev = [B.genesis(a) for a in range(7)]
+    blocks = []
+    rng = np.random.default_rng(5)
+    for r in range(1, 40):
+        for a in range(7):
+            k = int(rng.integers(1, 8))
+            inc = [prev[a].reference()] + [prev[x].reference() for x in range(7) if x != a][: k - 1]
+            sts = [("share", bytes(int(rng.integers(0, 700))))] * int(rng.integers(0, 3))
+            sts += [("range", prev[(a + 1) % 7].reference(), 0, int(rng.integers(0, 5)))] * int(rng.integers(0, 20))
+            blocks.append(B.new_with_signer(a, r, inc, sts, r, False, 0, seeds[a], O.sign))
+        prev = blocks[-7:]
+    bins = [b.bincode() for b in blocks]
+    # corrupt a few
+    bins[3] = bins[3][:-5] + bytes([bins[3][-5] ^ 1]) + bins[3][-4:]
+    bins[10] = bins[10][:60]
+    st, md, bd = engine.verify_blocks(bins)
+    for i, b in enumerate(bins):
+        ost, omd, obd = O.block_verify(b, pks, stakes, 0)
+        assert int(st[i]) == ost, i
+        if ost != 1:
+            assert md[i].tobytes() == omd and bd[i].tobytes() == obd, i
+    assert len({int(s) for s in st}) >= 3

@@ -1,0 +1,127 @@
+"""GPU: field / scalar / hash primitives of the HIP kernels vs Python big integers
+and hashlib (bit-exact). Edge values: 0, 1, p-1, p, p+1, 2^255-1, 2^256-1, y+p."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import zip215 as Z
+
+pytestmark = pytest.mark.gpu
+P = Z.P
+EDGE = [0, 1, 2, 19, P - 1, P, P + 1, P + 18, 2**255 - 1, 2**255, 2**256 - 1, 2**256 - 38, 2**32 - 1, 2**224,
+        Z.D, Z.SQRT_M1]
+
+
+def words(x: int, n=8):
+    return [(x >> (32 * i)) & 0xFFFFFFFF for i in range(n)]
+
+
+def val(ws):
+    return sum(int(w) << (32 * i) for i, w in enumerate(ws))
+
+
+def pairs(r, count=300):
+    out = [(a, b) for a in EDGE for b in EDGE[:6]]
+    for _ in range(count):
+        out.append((r.randrange(2**256), r.randrange(2**256)))
+    return out
+
+
+def run(engine, op, items):
+    w = np.array([words(a) + words(b) for a, b in items], dtype=np.uint32)
+    return engine.selftest(op, w)
+
+
+def test_fe_mul_sq_add_sub(engine):
+    r = random.Random(1)
+    items = pairs(r)
+    for op, f in [(0, lambda a, b: a * b), (1, lambda a, b: a * a), (2, lambda a, b: a + b),
+                  (6, lambda a, b: a * (b & 0x3FFFFFF))]:
+        it = items if op != 6 else [(a, b & 0x3FFFFFF) for a, b in items]
+        out = run(engine, op, it)
+        for (a, b), o in zip(it, out):
+            assert val(o[:8]) == f(a, b) % P, (op, a, b)
+
+
+def test_fe_sub_tight_inputs(engine):
+    # fe_sub's contract: tight inputs (< 2^255 + 2^14) -- which every fe op returns
+    r = random.Random(2)
+    items = [(a % (2**255 + 2**13), b % (2**255 + 2**13)) for a, b in pairs(r)]
+    out = run(engine, 3, items)
+    for (a, b), o in zip(items, out):
+        assert val(o[:8]) == (a - b) % P, (a, b)
+
+
+def test_fe_invert_pow(engine):
+    r = random.Random(3)
+    items = [(a, 0) for a in EDGE] + [(r.randrange(2**256), 0) for _ in range(100)]
+    out = run(engine, 4, items)
+    for (a, _), o in zip(items, out):
+        assert val(o[:8]) == pow(a % P, P - 2, P)
+    out = run(engine, 5, items)
+    for (a, _), o in zip(items, out):
+        assert val(o[:8]) == pow(a % P, (P - 5) // 8, P)
+
+
+def test_fe_canon_of_255_bit_inputs(engine):
+    items = [(y, 0) for y in [0, 1, P - 1, P, P + 1, P + 18, 2**255 - 1]]
+    out = run(engine, 12, items)
+    for (a, _), o in zip(items, out):
+        assert val(o[:8]) == (a & (2**255 - 1)) % P
+
+
+def test_decompress_zip215(engine):
+    r = random.Random(4)
+    encs = [e for e, _ in Z.small_order_encodings()]
+    encs += [r.randrange(2**256).to_bytes(32, "little") for _ in range(200)]
+    encs += [(y | s << 255).to_bytes(32, "little") for y in range(P, 2**255) for s in (0, 1)]
+    w = np.array([list(np.frombuffer(e, dtype=np.uint32)) + [0] * 8 for e in encs], dtype=np.uint32)
+    out = engine.selftest(7, w)
+    for e, o in zip(encs, out):
+        pt = Z.decompress(e)
+        assert bool(o[8]) == (pt is not None), e.hex()
+        if pt is not None:
+            assert val(o[:8]) == pt[0] % P, e.hex()
+
+
+def test_scalar_reduce_and_canonical(engine):
+    r = random.Random(5)
+    xs = [0, 1, Z.L - 1, Z.L, Z.L + 1, 2 * Z.L, 2**512 - 1, 2**256, Z.L * Z.L] + [r.randrange(2**512) for _ in range(300)]
+    w = np.array([words(x, 16) for x in xs], dtype=np.uint32)
+    out = engine.selftest(8, w)
+    for x, o in zip(xs, out):
+        assert val(o[:8]) == x % Z.L
+    ss = [0, 1, Z.L - 1, Z.L, Z.L + 1, 2**255 - 1, 2**253, 2**252] + [r.randrange(2**256) for _ in range(100)]
+    w = np.array([words(s) + [0] * 8 for s in ss], dtype=np.uint32)
+    out = engine.selftest(10, w)
+    for s, o in zip(ss, out):
+        assert o[0] == (1 if s < Z.L else 0), s
+
+
+def test_sha512_64(engine):
+    r = random.Random(6)
+    msgs = [bytes(r.randrange(256) for _ in range(64)) for _ in range(100)]
+    w = np.array([list(np.frombuffer(m, dtype=np.uint32)) for m in msgs], dtype=np.uint32)
+    out = engine.selftest(9, w)
+    for m, o in zip(msgs, out):
+        assert o.astype("<u4").tobytes() == hashlib.sha512(m).digest()
+
+
+def test_basepoint_mul(engine):
+    r = random.Random(8)
+    ks = [0, 1, 2, 3, 127, 128, 129, 255, 256, Z.L - 1] + [r.randrange(Z.L) for _ in range(60)]
+    w = np.array([words(k) + [0] * 8 for k in ks], dtype=np.uint32)
+    out = engine.selftest(11, w)
+    for k, o in zip(ks, out):
+        assert o[:8].astype("<u4").tobytes() == Z.compress(Z.scalarmult(Z.B_POINT, k)), k
+
+
+def test_blake2b_kats(engine, golden):
+    g = golden("hash_kat.json")
+    lens = [int(n) for n in g["blake2b256"]]
+    items = [bytes((i * 31 + 7) % 251 for i in range(n)) for n in lens]
+    out = engine.blake2b256(items)
+    for n, o in zip(lens, out):
+        assert o.hex() == g["blake2b256"][str(n)], n
