@@ -1,0 +1,232 @@
+"""Benchmark: verified StatementBlock signatures / s on 1..8 MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "config 2"): per GPU, a batch of 1,048,576
+independent Ed25519 signatures over 32-byte block digests (seed_i =
+SHA-512("mysti-seed"||i)[:32], msg_i = Blake2b-256("mysti-msg"||i), RFC 8032
+signatures made on the GPU by the library's own signer), verified with ZIP-215
+semantics. One step = one verify pass over the whole batch, inputs and the accept
+vector resident in HBM (no PCIe in the timed region; the PCIe-inclusive rate is
+reported separately as `end_to_end`).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; each rank verifies its
+own shard (weak scaling, no data-path collective); barrier + synchronize around the
+timed region, max time over ranks (gloo), value = all ranks' signatures / that time.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import struct
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "verified StatementBlock sigs/sec (1/2/4/8 MI355X) vs host-core ed25519-consensus"
+# Algorithmic work per signature: 3,200 field multiplications x 64
+# 32x32->64 multiply-accumulates, plus one SHA-512 compression (~6,000 32-bit ops).
+W_VERIFY_MACS = 3200 * 64
+W_SHA512_OPS = 6000
+# Peaks: full-rate 32-bit VALU = 256 CU x 128 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md:
+# FP32 vector 157.3 TFLOPS = 2 x 78.6 T lane-ops/s); v_mad_u64_u32 issues at half that
+# rate on gfx950 (tools/microbench_valu.hip, profiles/r01_microbench_valu*.jsonl), so one
+# MAC costs 2 full-rate issue slots.
+PEAK_VALU_OPS = 256 * 128 * 2.4e9
+MAC_SLOTS = 2
+
+
+def corpus_host(lo: int, n: int):
+    seed = np.frombuffer(b"".join(hashlib.sha512(b"mysti-seed" + struct.pack("<Q", i)).digest()[:32]
+                                  for i in range(lo, lo + n)), dtype=np.uint8).reshape(n, 32)
+    msg = np.frombuffer(b"".join(hashlib.blake2b(b"mysti-msg" + struct.pack("<Q", i), digest_size=32).digest()
+                                 for i in range(lo, lo + n)), dtype=np.uint8).reshape(n, 32)
+    return seed, msg
+
+
+def cpu_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, sample: int):
+    """The oracle's C restatement (-O3 -march=native, built on this host) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-s", "native"], check=True)
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libmv_oracle_native.so"))
+    vp = ctypes.c_void_p
+    lib.orc_ed25519_verify_batch.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+    threads = min(16, os.cpu_count() or 1)  # the box's CPU share is 16 cores
+    res = {}
+    # ~8 s single-threaded, then `passes` sweeps of the sample on all threads (~10 s)
+    for t, n, passes in ((1, min(sample, 250_000), 1), (threads, sample, 4)):
+        p = np.ascontiguousarray(pk[:n]); s = np.ascontiguousarray(sig[:n]); m = np.ascontiguousarray(msg[:n])
+        st = np.zeros(n, dtype=np.uint8)
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            lib.orc_ed25519_verify_batch(vp(p.ctypes.data), vp(s.ctypes.data), vp(m.ctypes.data), n,
+                                         vp(st.ctypes.data), t)
+        dt = time.perf_counter() - t0
+        assert (st == 0).all(), "oracle rejected a valid corpus signature"
+        res[t] = (n * passes / dt, n * passes, dt)
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(res[threads][0], 1), "unit": "sigs/s", "cores": threads, "kind": "port",
+        "sample": f"{res[threads][1]} verifies of config-2 signatures on {threads} threads ({res[threads][2]:.1f} s); "
+                  f"single core: {res[1][1]} verifies ({res[1][2]:.1f} s)",
+        "single_core_value": round(res[1][0], 1), "host_cpu": model, "nproc": os.cpu_count(),
+        "impl": "oracle/ed25519.c: dalek u64-backend structure (5x51 limbs, Straus wNAF-5/8), gcc -O3 -march=native",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20, help="0 disables the CPU baseline")
+    ap.add_argument("--no-e2e", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    import mysticeti_amd as M
+
+    eng = M.Engine(devices=(local_rank,))
+    n = args.batch
+
+    # ---- corpus: host hashes, GPU signing (library signer), all resident in HBM ----
+    seed_h, msg_h = corpus_host(rank * n, n)
+    d_seed = torch.from_numpy(seed_h.copy()).to(dev)
+    d_msg = torch.from_numpy(msg_h.copy()).to(dev)
+    d_pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    d_status = torch.full((n,), 255, dtype=torch.uint8, device=dev)
+    # a dedicated non-default stream: the library launches on it and the HIP events
+    # below are recorded on it, so kernel_ms times exactly the verify launches
+    stream = torch.cuda.Stream(dev)
+    assert stream.cuda_stream != 0
+    torch.cuda.synchronize(dev)  # the H2D copies above ran on the default stream
+    eng.dev_sign(local_rank, d_seed, d_msg, d_pk, d_sig, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        eng.dev_verify(local_rank, d_msg, d_sig, d_pk, d_status, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step, on this stream
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    status = d_status.cpu().numpy()
+    accepted = int((status == 0).sum())
+    ok = accepted == n
+    parity = None
+    if rank == 0 and n == (1 << 20):
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_config2.json")))
+        parity = hashlib.sha256(status.tobytes()).hexdigest() == gold["sha256_status"] and \
+            hashlib.sha256(d_sig.cpu().numpy().tobytes()).hexdigest() == gold["sha256_sig"]
+    if dist:
+        tk = torch.tensor([0 if ok else 1], dtype=torch.int64)
+        dist.all_reduce(tk, op=dist.ReduceOp.SUM)
+        ok = int(tk.item()) == 0
+
+    total = n * world * args.steps
+    value = total / elapsed
+    rate_kernel = n / (kernel_ms * 1e-3)
+    ops_per_sig = MAC_SLOTS * W_VERIFY_MACS + W_SHA512_OPS
+    achieved = rate_kernel * ops_per_sig
+
+    out = None
+    if rank == 0:
+        e2e = None
+        if not args.no_e2e:
+            # PCIe-inclusive: host buffers in, accept vector out, through the C ABI
+            pk_h, sig_h = d_pk.cpu().numpy(), d_sig.cpu().numpy()
+            eng.ed25519_verify(msg_h, sig_h, pk_h)
+            t2 = time.perf_counter()
+            st_h = eng.ed25519_verify(msg_h, sig_h, pk_h)
+            t3 = time.perf_counter()
+            e2e = {"value": round(n / (t3 - t2), 1), "unit": "sigs/s", "note": "host arrays in, statuses out (H2D 128 B/sig)",
+                   "accepted": int((st_h == 0).sum())}
+        cpu = None
+        if args.cpu_sample > 0:
+            cpu = cpu_baseline(d_pk.cpu().numpy(), d_sig.cpu().numpy(), msg_h, min(args.cpu_sample, n))
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "sigs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (config-2 corpus regenerated from its seed rule; signed on-GPU, pinned by "
+                    "tests/golden/batch_config2.json)",
+            "config": {"workload": "config2: 1,048,576 independent Ed25519 (ZIP-215) signatures over 32-byte "
+                                   "block digests per GPU", "batch_per_gpu": n, "global_batch": n * world,
+                       "parallelism": f"shard-per-gpu x{world}, no collective"},
+            "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2),
+                         "unit": "TOP/s", "frac": round(achieved / PEAK_VALU_OPS, 4), "traffic": None,
+                         "kernel": "k_verify", "kernel_ms": round(kernel_ms, 4),
+                         "work_per_sig": f"{W_VERIFY_MACS} MACs x {MAC_SLOTS} slots + {W_SHA512_OPS} SHA-512 ops"},
+            "cpu_baseline": cpu,
+            "end_to_end": e2e,
+            "correct": bool(ok),
+            "parity_sha256": parity,
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = {"all_cores": round(value / world / cpu["value"], 1),
+                                     "single_core": round(value / world / cpu["single_core_value"], 1)}
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
