@@ -46,37 +46,28 @@ MV_DEV void cached_identity(cached& c) {
 }
 
 MV_DEV void p1p1_to_p2(p2& r, const p1p1& c) {
-  fe_mul(r.X, c.X, c.T);
-  fe_mul(r.Y, c.Y, c.Z);
-  fe_mul(r.Z, c.Z, c.T);
+  fe_mul3(r.X, c.X, c.T, r.Y, c.Y, c.Z, r.Z, c.Z, c.T);
 }
 MV_DEV void p1p1_to_p3(p3& r, const p1p1& c) {
-  fe_mul(r.X, c.X, c.T);
-  fe_mul(r.Y, c.Y, c.Z);
-  fe_mul(r.Z, c.Z, c.T);
-  fe_mul(r.T, c.X, c.Y);
+  fe_mul4(r.X, c.X, c.T, r.Y, c.Y, c.Z, r.Z, c.Z, c.T, r.T, c.X, c.Y);
 }
 MV_DEV void p3_to_cached(cached& r, const p3& p) {
   fe d2;
   fe_const(d2, K_D2);
-  fe_add(r.YpX, p.Y, p.X);
-  fe_sub(r.YmX, p.Y, p.X);
+  fe_addsub2<2u>(r.YpX, p.Y, p.X, r.YmX, p.Y, p.X);
   r.Z = p.Z;
   fe_mul(r.T2d, p.T, d2);
 }
-// 2P from projective: 4 squarings (dbl-2008-hwcd, a = -1)
+// 2P from projective: 4 squarings (dbl-2008-hwcd, a = -1), grouped 4-way
 MV_DEV void p2_dbl(p1p1& r, const p2& p) {
-  fe XX, YY, ZZ2, S;
-  fe_sq(XX, p.X);
-  fe_sq(YY, p.Y);
-  fe_sq(ZZ2, p.Z);
-  fe_add(ZZ2, ZZ2, ZZ2);
+  fe XX, YY, ZZ, S, S2;
   fe_add(S, p.X, p.Y);
-  fe_sq(S, S);
-  fe_add(r.Y, YY, XX);
-  fe_sub(r.Z, YY, XX);
-  fe_sub(r.X, S, r.Y);
-  fe_sub(r.T, ZZ2, r.Z);
+  fe_sq4(XX, p.X, YY, p.Y, ZZ, p.Z, S2, S);
+  fe ZZ2;
+  // Y' = YY + XX, Z' = YY - XX, ZZ2 = 2 ZZ
+  fe_addsub3<2u>(r.Y, YY, XX, r.Z, YY, XX, ZZ2, ZZ, ZZ);
+  // X' = (X+Y)^2 - Y', T' = 2ZZ - Z'
+  fe_addsub2<3u>(r.X, S2, r.Y, r.T, ZZ2, r.Z);
 }
 MV_DEV void p3_dbl(p1p1& r, const p3& p) {
   p2 q;
@@ -85,32 +76,18 @@ MV_DEV void p3_dbl(p1p1& r, const p3& p) {
 }
 // P + Q (Q cached): 4 multiplications
 MV_DEV void p3_add_cached(p1p1& r, const p3& p, const cached& q) {
-  fe PP, MM, TT, ZZ;
-  fe_add(PP, p.Y, p.X);
-  fe_sub(MM, p.Y, p.X);
-  fe_mul(PP, PP, q.YpX);
-  fe_mul(MM, MM, q.YmX);
-  fe_mul(TT, p.T, q.T2d);
-  fe_mul(ZZ, p.Z, q.Z);
+  fe PP, MM, TT, ZZ, ypx, ymx;
+  fe_addsub2<2u>(ypx, p.Y, p.X, ymx, p.Y, p.X);
+  fe_mul4(PP, ypx, q.YpX, MM, ymx, q.YmX, TT, p.T, q.T2d, ZZ, p.Z, q.Z);
   fe_add(ZZ, ZZ, ZZ);
-  fe_sub(r.X, PP, MM);
-  fe_add(r.Y, PP, MM);
-  fe_add(r.Z, ZZ, TT);
-  fe_sub(r.T, ZZ, TT);
+  fe_addsub4<9u>(r.X, PP, MM, r.Y, PP, MM, r.Z, ZZ, TT, r.T, ZZ, TT);
 }
 // P + Q (Q precomp, Z = 1): 3 multiplications
 MV_DEV void p3_add_precomp(p1p1& r, const p3& p, const precomp& q) {
-  fe PP, MM, TT, Z2;
-  fe_add(PP, p.Y, p.X);
-  fe_sub(MM, p.Y, p.X);
-  fe_mul(PP, PP, q.ypx);
-  fe_mul(MM, MM, q.ymx);
-  fe_mul(TT, p.T, q.xy2d);
-  fe_add(Z2, p.Z, p.Z);
-  fe_sub(r.X, PP, MM);
-  fe_add(r.Y, PP, MM);
-  fe_add(r.Z, Z2, TT);
-  fe_sub(r.T, Z2, TT);
+  fe PP, MM, TT, Z2, ypx, ymx;
+  fe_addsub3<2u>(ypx, p.Y, p.X, ymx, p.Y, p.X, Z2, p.Z, p.Z);
+  fe_mul3(PP, ypx, q.ypx, MM, ymx, q.ymx, TT, p.T, q.xy2d);
+  fe_addsub4<9u>(r.X, PP, MM, r.Y, PP, MM, r.Z, Z2, TT, r.T, Z2, TT);
 }
 // conditional negation of table entries: -(x, y) = (-x, y) swaps y+x / y-x and negates xy
 MV_DEV void cached_cneg(cached& c, bool neg) {

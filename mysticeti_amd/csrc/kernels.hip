@@ -15,6 +15,7 @@
 // written once, read 64 times, L2/MALL-resident per wave).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fe25519.h"
 #include "ge25519.h"
@@ -70,7 +71,9 @@ MV_DEV void atab_put(uint4* wave_base, int e, int lane, const cached& c) {
   p[6 * 64] = q4(c.T2d, 0);
   p[7 * 64] = q4(c.T2d, 1);
 }
-MV_DEV void atab_get(cached& c, const uint4* wave_base, int lane, int digit) {
+// raw entry load; the sign is applied at use time (cached_cneg) so the gather's
+// latency hides behind the window's doublings
+MV_DEV void atab_load(cached& c, const uint4* wave_base, int lane, int digit) {
   int e = digit < 0 ? -digit : digit;
   const uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
   uq4(c.YpX, 0, p[0 * 64]);
@@ -81,7 +84,6 @@ MV_DEV void atab_get(cached& c, const uint4* wave_base, int lane, int digit) {
   uq4(c.Z, 1, p[5 * 64]);
   uq4(c.T2d, 0, p[6 * 64]);
   uq4(c.T2d, 1, p[7 * 64]);
-  cached_cneg(c, digit < 0);
 }
 
 MV_DEV void load8(uint32_t w[8], const uint8_t* p) {
@@ -175,8 +177,26 @@ __global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
   o[5] = q4(pc.xy2d, 1);
 }
 
+// Per-wave scratch layout (uint4 units, each [..][lane]): the variable-base table,
+// then R (X, Y, T; Z = 1) and the recoded scalars, which are parked in HBM during
+// the ladder instead of holding 48 VGPRs.
+constexpr int SCR_R = AT_ENTRIES * AT_QUADS;  // 72
+constexpr int SCR_DIG = SCR_R + 6;            // 78: 8 x uint2 per lane = 4 quads
+constexpr int WAVE_QUADS = SCR_DIG + 4;       // 82
+
+MV_DEV void scr_put_fe(uint4* wave_base, int q, int lane, const fe& f) {
+  wave_base[q * 64 + lane] = q4(f, 0);
+  wave_base[(q + 1) * 64 + lane] = q4(f, 1);
+}
+MV_DEV void scr_get_fe(fe& f, const uint4* wave_base, int q, int lane) {
+  uq4(f, 0, wave_base[q * 64 + lane]);
+  uq4(f, 1, wave_base[(q + 1) * 64 + lane]);
+}
+
 // One signature per lane. pk rows are read at key_idx[i] when key_idx != nullptr.
-__global__ void __launch_bounds__(256, 2)
+// MINW = minimum waves per SIMD (2 -> <= 256 VGPRs, 1 -> <= 512).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW)
     k_verify(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
              const uint32_t* __restrict__ key_idx, uint32_t n, const uint4* __restrict__ btab_g,
              uint4* __restrict__ scratch, uint8_t* __restrict__ status) {
@@ -185,35 +205,41 @@ __global__ void __launch_bounds__(256, 2)
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t idx = gid < n ? gid : n - 1;
   const int lane = threadIdx.x & 63;
-  uint4* wave_tab = scratch + (size_t)(gid >> 6) * (AT_ENTRIES * AT_QUADS * 64);
+  uint4* wave_tab = scratch + (size_t)(gid >> 6) * (WAVE_QUADS * 64);
+  uint2* wave_dig = reinterpret_cast<uint2*>(wave_tab + SCR_DIG * 64);
 
-  uint32_t aw[8], rw[8], sw[8], mw[8];
-  load8(aw, pk + 32 * (size_t)(key_idx ? key_idx[idx] : idx));
-  load8(rw, sig + 64 * (size_t)idx);
-  load8(sw, sig + 64 * (size_t)idx + 32);
-  load8(mw, msg + 32 * (size_t)idx);
-
-  const bool s_ok = sc_is_canonical(sw);
-  p3 A, R;
-  bool okA, okR;
-  decompress_x2(A, okA, aw, R, okR, rw);
-
-  // k = SHA-512(R || A || M) mod l over the original encodings
-  uint32_t kin[24], h[16], k[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    kin[i] = rw[i];
-    kin[8 + i] = aw[i];
-    kin[16 + i] = mw[i];
-  }
-  sha512_short(h, kin, 96);
-  sc_reduce512(k, h);
-  uint32_t kd[8], sd[8];
-  sc_recode16(kd, k);
-  sc_recode256(sd, sw);
-
-  // variable-base table [j](-A), j = 0..8
+  bool okA, okR, s_ok;
   {
+    uint32_t aw[8], rw[8], sw[8], mw[8];
+    load8(aw, pk + 32 * (size_t)(key_idx ? key_idx[idx] : idx));
+    load8(rw, sig + 64 * (size_t)idx);
+    load8(sw, sig + 64 * (size_t)idx + 32);
+    load8(mw, msg + 32 * (size_t)idx);
+
+    s_ok = sc_is_canonical(sw);
+    p3 A, R;
+    decompress_x2(A, okA, aw, R, okR, rw);
+    scr_put_fe(wave_tab, SCR_R + 0, lane, R.X);
+    scr_put_fe(wave_tab, SCR_R + 2, lane, R.Y);
+    scr_put_fe(wave_tab, SCR_R + 4, lane, R.T);
+
+    // k = SHA-512(R || A || M) mod l over the original encodings
+    uint32_t kin[24], h[16], k[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      kin[i] = rw[i];
+      kin[8 + i] = aw[i];
+      kin[16 + i] = mw[i];
+    }
+    sha512_short(h, kin, 96);
+    sc_reduce512(k, h);
+    uint32_t kd[8], sd[8];
+    sc_recode16(kd, k);
+    sc_recode256(sd, sw);
+#pragma unroll
+    for (int j = 0; j < 8; j++) wave_dig[j * 64 + lane] = make_uint2(kd[j], sd[j]);
+
+    // variable-base table [j](-A), j = 0..8
     p3 nA, cur;
     p3_neg(nA, A);
     cached c1, c;
@@ -237,35 +263,52 @@ __global__ void __launch_bounds__(256, 2)
   p1p1 Q;
   cached ca;
   precomp pb;
-  for (int w = 63; w >= 0; w--) {
-    atab_get(ca, wave_tab, lane, digit16(kd, w));  // issued ahead of the doublings
-    if (w != 63) {
-      for (int i = 0; i < 3; i++) {
+  // 8 groups of 8 windows; a group's digit word (k nibbles, s bytes) is loaded one
+  // group ahead, so no window waits on memory except for its table gather, which
+  // is issued before the doublings and consumed after them.
+  uint2 dw_next = wave_dig[7 * 64 + lane];
+  for (int g = 7; g >= 0; g--) {
+    const uint2 dw = dw_next;
+    if (g > 0) dw_next = wave_dig[(g - 1) * 64 + lane];
+    for (int j = 7; j >= 0; j--) {
+      const int w = 8 * g + j;
+      const int dk = ((int)(dw.x << (28 - 4 * j))) >> 28;
+      atab_load(ca, wave_tab, lane, dk);
+      if (w != 63) {
+        for (int i = 0; i < 3; i++) {
+          p2_dbl(Q, P);
+          p1p1_to_p2(P, Q);
+        }
         p2_dbl(Q, P);
-        p1p1_to_p2(P, Q);
+        p1p1_to_p3(P3, Q);
+      } else {
+        p3_identity(P3);
       }
-      p2_dbl(Q, P);
-      p1p1_to_p3(P3, Q);
-    } else {
-      p3_identity(P3);
+      cached_cneg(ca, dk < 0);
+      p3_add_cached(Q, P3, ca);
+      if ((j & 1) == 0) {
+        p1p1_to_p3(P3, Q);
+        const int ds = ((int)(dw.y << (24 - 8 * (j >> 1)))) >> 24;
+        btab_get(pb, btab, ds);
+        p3_add_precomp(Q, P3, pb);
+      }
+      p1p1_to_p2(P, Q);
     }
-    p3_add_cached(Q, P3, ca);
-    if ((w & 1) == 0) {
-      p1p1_to_p3(P3, Q);
-      btab_get(pb, btab, digit256(sd, w >> 1));
-      p3_add_precomp(Q, P3, pb);
-    }
-    p1p1_to_p2(P, Q);
   }
   // cofactored check: [8](R - R') == identity
-  p3 Rp;
+  p3 R, Rp;
   p1p1_to_p3(Rp, Q);
+  scr_get_fe(R.X, wave_tab, SCR_R + 0, lane);
+  scr_get_fe(R.Y, wave_tab, SCR_R + 2, lane);
+  scr_get_fe(R.T, wave_tab, SCR_R + 4, lane);
+  fe_set(R.Z, 1);
   p3 nRp;
   p3_neg(nRp, Rp);
   cached cR;
   p3_to_cached(cR, nRp);
   p3_add_cached(Q, R, cR);
   p1p1_to_p2(P, Q);
+#pragma unroll 1
   for (int i = 0; i < 3; i++) {
     p2_dbl(Q, P);
     p1p1_to_p2(P, Q);
@@ -483,7 +526,14 @@ namespace mvk {
 
 size_t verify_scratch_bytes(uint32_t n) {
   size_t waves = (size_t)((n + 255) / 256) * 4;  // every wave of the 256-thread grid owns a slot
-  return waves * mv::AT_ENTRIES * mv::AT_QUADS * 64 * sizeof(uint4);
+  return waves * mv::WAVE_QUADS * 64 * sizeof(uint4);
+}
+static int verify_variant() {
+  static int v = [] {
+    const char* e = getenv("MV_VERIFY_OCC");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
 }
 size_t btable_bytes() { return mv::BT_ENTRIES * mv::BT_QUADS * sizeof(uint4); }
 
@@ -494,8 +544,12 @@ hipError_t launch_btable_init(void* d_btab, hipStream_t s) {
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mv::k_verify, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                     (const uint4*)btab, (uint4*)scratch, status);
+  if (verify_variant() == 1)
+    hipLaunchKernelGGL(mv::k_verify<1>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
+                       (const uint4*)btab, (uint4*)scratch, status);
+  else
+    hipLaunchKernelGGL(mv::k_verify<2>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
+                       (const uint4*)btab, (uint4*)scratch, status);
   return hipGetLastError();
 }
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
