@@ -1,23 +1,20 @@
 // GF(2^255-19) arithmetic for gfx950, one field element per lane.
 //
-// Representation: 8 x 32-bit limbs (radix 2^32, little-endian), value held
-// loosely in [0, 2^256); every operation returns a "tight" value
-// < 2^255 + 2^14, which every operation accepts as input. Canonical form is
-// produced only for comparisons and encoding.
+// Representation: 9 unsaturated limbs of 29 bits (radix 2^29, 261 bits), so a
+// whole column of a schoolbook product fits in 64 bits and needs no carry
+// flags. Why not 8 x 32-bit limbs: on gfx950 every carry-consuming instruction
+// (v_addc_co_u32 with an SGPR carry) issues at half rate, like v_mad_u64_u32
+// itself, so a saturated MAC costs two half-rate slots; here a MAC is ONE
+// v_mad_u64_u32 (tools/microbench_mac.hip, profiles/r01/). Additions become
+// full-rate limb-wise v_add_u32 with no carry chain.
 //
-// Multiplication is product-scanning (column-wise) on v_mad_u64_u32 with its
-// carry-out into a third accumulator word (v_addc_co_u32): 3 issue slots per
-// 32x32 MAC on CDNA4, where v_mad_u64_u32 issues at half the full VALU rate
-// (tools/microbench_valu.hip). The 512-bit product is folded with
-// 2^256 = 38 (mod p) and then 2^255 = 19.
-//
-// ILP / hazard structure: on gfx950 a VALU that reads an SGPR carry written by a
-// VALU needs 2 wait states, and each product is one serial MAC chain. So every
-// operation comes in an N-way form (fe_mul_n, fe_sq_n, fe_addsub_n) that runs N
-// independent field operations in lock-step, instruction by instruction (volatile
-// asm keeps the order): with N >= 3 every carry consumer sits >= 3 instructions
-// after its producer (no s_nop) and N MAC chains overlap their latency. The
-// curve formulas (ge25519.h) group their independent operations into these calls.
+// Limb bounds (all arithmetic relies on them):
+//   N  "normalised": every limb < 2^29 + 2^23. Output of mul, sq, sub, normalize.
+//   A  lazy sum of two N values: every limb < 2^30 + 2^24. Output of fe_add.
+// fe_mul / fe_sq accept N or A inputs: 9 * (2^30 + 2^24)^2 < 2^63.3, so the
+// 64-bit column sums cannot overflow. fe_sub accepts N or A for both operands
+// (its bias constant has every limb >= 1.5 * 2^30). fe_add needs N inputs;
+// fe_addn (add + normalise) returns N. Reduction uses 2^261 = 1216 (mod p).
 //
 // Replaces (semantics only) curve25519-dalek-ng 4.1.1 FieldElement51, the
 // field under ed25519-consensus (mysticeti-core/src/crypto.rs:25,188).
@@ -27,400 +24,182 @@
 
 #define MV_DEV __device__ __forceinline__
 
+#include "carry32.h"
+
 namespace mv {
 
+constexpr uint32_t M29 = (1u << 29) - 1;
+constexpr uint32_t R261 = 1216;  // 2^261 mod p
+
 struct fe {
-  uint32_t v[8];
+  uint32_t v[9];
 };
 
-// ---- carry-flag primitives (wave64 carry masks live in SGPR pairs) ----
-// Volatile: their relative order is the interleaving schedule.
-MV_DEV void a_mad(uint64_t& acc, uint64_t& cm, uint32_t a, uint32_t b) {
-  asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cm) : "v"(a), "v"(b));
-}
-MV_DEV void a_cnt(uint32_t& c2, uint64_t& cm) {  // c2 += carry
-  asm volatile("v_addc_co_u32 %0, %1, %0, 0, %1" : "+v"(c2), "+s"(cm));
-}
-MV_DEV uint32_t add_co(uint32_t a, uint32_t b, uint64_t& cm) {
-  uint32_t r;
-  asm volatile("v_add_co_u32 %0, %1, %2, %3" : "=v"(r), "=s"(cm) : "v"(a), "v"(b));
-  return r;
-}
-MV_DEV uint32_t addc_co(uint32_t a, uint32_t b, uint64_t& cm) {
-  uint32_t r;
-  asm volatile("v_addc_co_u32 %0, %1, %2, %3, %1" : "=v"(r), "+s"(cm) : "v"(a), "v"(b));
-  return r;
-}
-MV_DEV uint32_t addc0(uint32_t a, uint64_t& cm) {  // a + carry, carry out
-  uint32_t r;
-  asm volatile("v_addc_co_u32 %0, %1, %2, 0, %1" : "=v"(r), "+s"(cm) : "v"(a));
-  return r;
-}
-MV_DEV uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& bm) {
-  uint32_t r;
-  asm volatile("v_sub_co_u32 %0, %1, %2, %3" : "=v"(r), "=s"(bm) : "v"(a), "v"(b));
-  return r;
-}
-MV_DEV uint32_t subb_co(uint32_t a, uint32_t b, uint64_t& bm) {
-  uint32_t r;
-  asm volatile("v_subb_co_u32 %0, %1, %2, %3, %1" : "=v"(r), "+s"(bm) : "v"(a), "v"(b));
-  return r;
-}
-MV_DEV uint32_t subb0(uint32_t a, uint64_t& bm) {  // a - borrow, borrow out
-  uint32_t r;
-  asm volatile("v_subb_co_u32 %0, %1, %2, 0, %1" : "=v"(r), "+s"(bm) : "v"(a));
-  return r;
-}
-// carry/borrow bit of the lane as 0/1
-MV_DEV uint32_t carry_bit(uint64_t& cm) {
-  uint32_t r;
-  asm volatile("v_cndmask_b32 %0, 0, 1, %1" : "=v"(r) : "s"(cm));
-  return r;
-}
-// plain 32x32+64 -> 64 (no carry-out consumer)
-MV_DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
-  uint64_t r, cm;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cm) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-// one serial MAC into a 96-bit (acc, c2) accumulator (scalar arithmetic, not hot)
-MV_DEV void mac(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
-  uint64_t cm;
-  a_mad(acc, cm, a, b);
-  a_cnt(c2, cm);
-}
-// ---------------------------------------------------------------- N-way core
-
-// r[c] (8 limbs) + 19*h[c], h[c] = 2*top[c] + bit255(r[c]); r7 keeps 31 bits.
-template <int N>
-MV_DEV void fold_n(fe (&r)[N], const uint32_t (&top)[N]) {
-  uint32_t m[N];
+// ---- normalisation: carry pass, limbs < 2^32 in -> N out ----
+MV_DEV void fe_normalize(fe& r) {
+  uint32_t c;
 #pragma unroll
-  for (int c = 0; c < N; c++) {
-    uint32_t h = (top[c] << 1) | (r[c].v[7] >> 31);
-    r[c].v[7] &= 0x7fffffffu;
-    m[c] = h * 19u;
+  for (int i = 0; i < 8; i++) {
+    c = r.v[i] >> 29;
+    r.v[i] &= M29;
+    r.v[i + 1] += c;
   }
-  uint64_t cm[N];
-#pragma unroll
-  for (int c = 0; c < N; c++) r[c].v[0] = add_co(r[c].v[0], m[c], cm[c]);
-#pragma unroll
-  for (int i = 1; i < 8; i++)
-#pragma unroll
-    for (int c = 0; c < N; c++) r[c].v[i] = addc0(r[c].v[i], cm[c]);
+  c = r.v[8] >> 29;  // weight 2^261
+  r.v[8] &= M29;
+  r.v[0] += __umul24(c, R261);  // < 2^29 + 2^14
 }
 
-// Incremental 2^256-reduction: consumes the product limbs w_0..w_15 in column
-// order, so only 8 limbs + one pending high word per element stay live.
-//   k < 8 : lo[k] = w_k
-//   k >= 8: u = w_k * 38 + lo[k-8]; r_{k-8} = lo(u) + hi(u_{k-9}) + carry
-// then the 2^255 fold of the top word.
-template <int N>
-struct Reducer {
-  fe r[N];
-  uint32_t hprev[N];
-  uint64_t cm[N];
-  MV_DEV void step(int k, const uint32_t (&w)[N]) {
-    if (k < 8) {
-#pragma unroll
-      for (int c = 0; c < N; c++) r[c].v[k] = w[c];
-      return;
-    }
-    const int i = k - 8;
-    uint32_t hi[N];
-#pragma unroll
-    for (int c = 0; c < N; c++) {
-      uint64_t u = mad64(w[c], 38u, (uint64_t)r[c].v[i]);  // < 2^38 + 2^32
-      r[c].v[i] = (uint32_t)u;
-      hi[c] = (uint32_t)(u >> 32);
-    }
-    if (i == 1) {
-#pragma unroll
-      for (int c = 0; c < N; c++) r[c].v[1] = add_co(r[c].v[1], hprev[c], cm[c]);
-    } else if (i > 1) {
-#pragma unroll
-      for (int c = 0; c < N; c++) r[c].v[i] = addc_co(r[c].v[i], hprev[c], cm[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < N; c++) hprev[c] = hi[c];
-  }
-  MV_DEV void finish(fe (&out)[N]);
-};
-
-template <int N>
-MV_DEV void Reducer<N>::finish(fe (&out)[N]) {
-  uint32_t top[N];
-#pragma unroll
-  for (int c = 0; c < N; c++) top[c] = addc0(hprev[c], cm[c]);  // < 2^7
-  fold_n<N>(r, top);
-#pragma unroll
-  for (int c = 0; c < N; c++) out[c] = r[c];
-}
-
-template <int N>
-MV_DEV void fe_mul_n(fe (&r)[N], const fe (&a)[N], const fe (&b)[N]) {
-  Reducer<N> red;
-  uint64_t acc[N];
-  uint32_t c2[N];
-#pragma unroll
-  for (int c = 0; c < N; c++) {
-    acc[c] = 0;
-    c2[c] = 0;
-  }
-#pragma unroll
-  for (int k = 0; k < 15; k++) {
-#pragma unroll
-    for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) {
-      uint64_t cm[N];
-#pragma unroll
-      for (int c = 0; c < N; c++) a_mad(acc[c], cm[c], a[c].v[i], b[c].v[k - i]);
-#pragma unroll
-      for (int c = 0; c < N; c++) a_cnt(c2[c], cm[c]);
-    }
-    uint32_t w[N];
-#pragma unroll
-    for (int c = 0; c < N; c++) {
-      w[c] = (uint32_t)acc[c];
-      acc[c] = (acc[c] >> 32) | ((uint64_t)c2[c] << 32);
-      c2[c] = 0;
-    }
-    red.step(k, w);
-  }
-  uint32_t w[N];
-#pragma unroll
-  for (int c = 0; c < N; c++) w[c] = (uint32_t)acc[c];
-  red.step(15, w);
-  red.finish(r);
-}
-
-// squaring: cross-product columns t_k, then u_k = 2 t_k + diag_k with a carry
-// chain along the columns, fed straight into the reducer.
-template <int N>
-MV_DEV void fe_sq_n(fe (&r)[N], const fe (&a)[N]) {
-  Reducer<N> red;
-  uint64_t acc[N], cd[N];
-  uint32_t c2[N], tprev[N], dhi[N];
-#pragma unroll
-  for (int c = 0; c < N; c++) {
-    acc[c] = 0;
-    c2[c] = 0;
-    tprev[c] = 0;
-  }
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    if (k >= 1 && k < 14) {
-#pragma unroll
-      for (int i = (k > 7 ? k - 7 : 0); i < k - i; i++) {
-        uint64_t cm[N];
-#pragma unroll
-        for (int c = 0; c < N; c++) a_mad(acc[c], cm[c], a[c].v[i], a[c].v[k - i]);
-#pragma unroll
-        for (int c = 0; c < N; c++) a_cnt(c2[c], cm[c]);
-      }
-    }
-    uint32_t t[N], d[N], w[N];
-#pragma unroll
-    for (int c = 0; c < N; c++) {
-      t[c] = (uint32_t)acc[c];  // cross column k (0 for k = 0)
-      acc[c] = (acc[c] >> 32) | ((uint64_t)c2[c] << 32);
-      c2[c] = 0;
-      if ((k & 1) == 0) {
-        uint64_t sq = mad64(a[c].v[k >> 1], a[c].v[k >> 1], 0);
-        d[c] = (uint32_t)sq;
-        dhi[c] = (uint32_t)(sq >> 32);
-      } else {
-        d[c] = dhi[c];
-      }
-    }
-    if (k == 0) {
-#pragma unroll
-      for (int c = 0; c < N; c++) w[c] = d[c];  // t_0 == 0
-    } else if (k == 1) {
-#pragma unroll
-      for (int c = 0; c < N; c++) w[c] = add_co(__builtin_amdgcn_alignbit(t[c], tprev[c], 31), d[c], cd[c]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < N; c++) w[c] = addc_co(__builtin_amdgcn_alignbit(t[c], tprev[c], 31), d[c], cd[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < N; c++) tprev[c] = t[c];
-    red.step(k, w);
-  }
-  red.finish(r);
-}
-
-// r[c] = a[c] + b[c] or, for bit c of SUB, a[c] - b[c] (computed as a + (2p - b)).
-// Tight inputs; tight outputs.
-template <int N, unsigned SUB>
-MV_DEV void fe_addsub_n(fe (&r)[N], const fe (&a)[N], const fe (&b)[N]) {
-  fe bb[N];
-  uint64_t cm[N];
-  // 2p - b for the subtractions (2p = 2^256 - 38 > tight b: no borrow out)
-#pragma unroll
-  for (int c = 0; c < N; c++) {
-    if (SUB & (1u << c)) {
-      bb[c].v[0] = sub_co(0xffffffdau, b[c].v[0], cm[c]);
-    } else {
-      bb[c] = b[c];
-    }
-  }
-#pragma unroll
-  for (int i = 1; i < 8; i++)
-#pragma unroll
-    for (int c = 0; c < N; c++)
-      if (SUB & (1u << c)) bb[c].v[i] = subb_co(0xffffffffu, b[c].v[i], cm[c]);
-#pragma unroll
-  for (int c = 0; c < N; c++) r[c].v[0] = add_co(a[c].v[0], bb[c].v[0], cm[c]);
-#pragma unroll
-  for (int i = 1; i < 8; i++)
-#pragma unroll
-    for (int c = 0; c < N; c++) r[c].v[i] = addc_co(a[c].v[i], bb[c].v[i], cm[c]);
-  uint32_t top[N];
-#pragma unroll
-  for (int c = 0; c < N; c++) top[c] = carry_bit(cm[c]);
-  fold_n<N>(r, top);
-}
-
-// ---------------------------------------------------------------- scalar wrappers
-MV_DEV void fe_set(fe& r, uint32_t x) {
+// ---- basic ops ----
+MV_DEV void fe_set(fe& r, uint32_t x) {  // x < 2^29
   r.v[0] = x;
 #pragma unroll
-  for (int i = 1; i < 8; i++) r.v[i] = 0;
+  for (int i = 1; i < 9; i++) r.v[i] = 0;
 }
-MV_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
-  fe ra[1], aa[1] = {a}, bb[1] = {b};
-  fe_mul_n<1>(ra, aa, bb);
-  r = ra[0];
-}
-MV_DEV void fe_sq(fe& r, const fe& a) {
-  fe ra[1], aa[1] = {a};
-  fe_sq_n<1>(ra, aa);
-  r = ra[0];
-}
+// lazy: N + N -> A (a multiplication input only)
 MV_DEV void fe_add(fe& r, const fe& a, const fe& b) {
-  fe ra[1], aa[1] = {a}, bb[1] = {b};
-  fe_addsub_n<1, 0u>(ra, aa, bb);
-  r = ra[0];
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + b.v[i];
 }
+MV_DEV void fe_addn(fe& r, const fe& a, const fe& b) {  // (N|A) + (N|A) -> N
+  fe_add(r, a, b);
+  fe_normalize(r);
+}
+// a - b + C, C = 0 mod p with limbs in (2^31 - 2^29, 2^31]: never negative -> N
 MV_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
-  fe ra[1], aa[1] = {a}, bb[1] = {b};
-  fe_addsub_n<1, 1u>(ra, aa, bb);
-  r = ra[0];
+  r.v[0] = a.v[0] + (0x7fffed00u - b.v[0]);
+#pragma unroll
+  for (int i = 1; i < 9; i++) r.v[i] = a.v[i] + (0x7ffffffcu - b.v[i]);
+  fe_normalize(r);
 }
 MV_DEV void fe_neg(fe& r, const fe& a) {
   fe z;
   fe_set(z, 0);
   fe_sub(r, z, a);
 }
-// two independent products / squares / adds
-MV_DEV void fe_mul2(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1) {
-  fe r[2], a[2] = {a0, a1}, b[2] = {b0, b1};
-  fe_mul_n<2>(r, a, b);
-  r0 = r[0];
-  r1 = r[1];
-}
-MV_DEV void fe_sq2(fe& r0, const fe& a0, fe& r1, const fe& a1) {
-  fe r[2], a[2] = {a0, a1};
-  fe_sq_n<2>(r, a);
-  r0 = r[0];
-  r1 = r[1];
-}
-MV_DEV void fe_mul3(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2,
-                    const fe& b2) {
-  fe r[3], a[3] = {a0, a1, a2}, b[3] = {b0, b1, b2};
-  fe_mul_n<3>(r, a, b);
-  r0 = r[0];
-  r1 = r[1];
-  r2 = r[2];
-}
-MV_DEV void fe_mul4(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2,
-                    const fe& b2, fe& r3, const fe& a3, const fe& b3) {
-  fe r[4], a[4] = {a0, a1, a2, a3}, b[4] = {b0, b1, b2, b3};
-  fe_mul_n<4>(r, a, b);
-  r0 = r[0];
-  r1 = r[1];
-  r2 = r[2];
-  r3 = r[3];
-}
-MV_DEV void fe_sq4(fe& r0, const fe& a0, fe& r1, const fe& a1, fe& r2, const fe& a2, fe& r3, const fe& a3) {
-  fe r[4], a[4] = {a0, a1, a2, a3};
-  fe_sq_n<4>(r, a);
-  r0 = r[0];
-  r1 = r[1];
-  r2 = r[2];
-  r3 = r[3];
-}
-template <unsigned SUB>
-MV_DEV void fe_addsub2(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1) {
-  fe r[2], a[2] = {a0, a1}, b[2] = {b0, b1};
-  fe_addsub_n<2, SUB>(r, a, b);
-  r0 = r[0];
-  r1 = r[1];
-}
-template <unsigned SUB>
-MV_DEV void fe_addsub3(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1, fe& r2,
-                       const fe& a2, const fe& b2) {
-  fe r[3], a[3] = {a0, a1, a2}, b[3] = {b0, b1, b2};
-  fe_addsub_n<3, SUB>(r, a, b);
-  r0 = r[0];
-  r1 = r[1];
-  r2 = r[2];
-}
-template <unsigned SUB>
-MV_DEV void fe_addsub4(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1, fe& r2,
-                       const fe& a2, const fe& b2, fe& r3, const fe& a3, const fe& b3) {
-  fe r[4], a[4] = {a0, a1, a2, a3}, b[4] = {b0, b1, b2, b3};
-  fe_addsub_n<4, SUB>(r, a, b);
-  r0 = r[0];
-  r1 = r[1];
-  r2 = r[2];
-  r3 = r[3];
+
+// 17 column sums (each < 2^63.3 + 2^47) -> N
+MV_DEV void fe_reduce_cols(fe& r, uint64_t (&c)[17]) {
+  // 1. normalise the high columns 9..16 into 29-bit limbs h9..h16 plus h17 (< 2^32)
+  uint32_t h[9];
+#pragma unroll
+  for (int k = 9; k < 16; k++) {
+    h[k - 9] = (uint32_t)c[k] & M29;
+    c[k + 1] += c[k] >> 29;
+  }
+  h[7] = (uint32_t)c[16] & M29;
+  h[8] = (uint32_t)(c[16] >> 29);
+  // 2. fold: 2^(29k) = 1216 * 2^(29(k-9)) for k >= 9
+#pragma unroll
+  for (int k = 0; k < 9; k++) c[k] += (uint64_t)h[k] * R261;
+  // 3. normalise the low columns; the carry out of limb 8 has weight 2^261
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    r.v[k] = (uint32_t)c[k] & M29;
+    c[k + 1] += c[k] >> 29;
+  }
+  r.v[8] = (uint32_t)c[8] & M29;
+  uint64_t top = c[8] >> 29;  // < 2^35
+  uint64_t t0 = (uint64_t)r.v[0] + top * R261;  // < 2^46
+  r.v[0] = (uint32_t)t0 & M29;
+  r.v[1] += (uint32_t)(t0 >> 29);  // < 2^29 + 2^17
 }
 
+MV_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
+  uint64_t c[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+#pragma unroll
+    for (int j = 0; j < 9; j++) c[i + j] += (uint64_t)a.v[i] * b.v[j];
+  fe_reduce_cols(r, c);
+}
+MV_DEV void fe_sq(fe& r, const fe& a) {
+  uint32_t a2[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a2[i] = a.v[i] << 1;  // < 2^31.01
+  uint64_t c[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    c[2 * i] += (uint64_t)a.v[i] * a.v[i];
+#pragma unroll
+    for (int j = i + 1; j < 9; j++) c[i + j] += (uint64_t)a2[i] * a.v[j];
+  }
+  fe_reduce_cols(r, c);
+}
 MV_DEV void fe_sqn(fe& r, const fe& a, int n) {
   fe_sq(r, a);
 #pragma unroll 1
   for (int i = 1; i < n; i++) fe_sq(r, r);
 }
-// multiply by a small constant (< 2^26)
+// multiply by a small constant c < 2^26 (N|A input)
 MV_DEV void fe_mul_small(fe& r, const fe& a, uint32_t c) {
-  uint32_t lo[8], hi[8];
+  uint64_t t[9];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t u = mad64(a.v[i], c, 0);
-    lo[i] = (uint32_t)u;
-    hi[i] = (uint32_t)(u >> 32);
+  for (int i = 0; i < 9; i++) t[i] = (uint64_t)a.v[i] * c;  // < 2^56.1
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    r.v[k] = (uint32_t)t[k] & M29;
+    t[k + 1] += t[k] >> 29;
   }
-  uint64_t cm;
-  fe rr[1];
-  rr[0].v[0] = lo[0];
-  rr[0].v[1] = add_co(lo[1], hi[0], cm);
-#pragma unroll
-  for (int i = 2; i < 8; i++) rr[0].v[i] = addc_co(lo[i], hi[i - 1], cm);
-  uint32_t top[1] = {addc0(hi[7], cm)};
-  fold_n<1>(rr, top);  // top < 2^26: h*19 < 2^32
-  r = rr[0];
+  r.v[8] = (uint32_t)t[8] & M29;
+  uint64_t t0 = (uint64_t)r.v[0] + (t[8] >> 29) * R261;
+  r.v[0] = (uint32_t)t0 & M29;
+  r.v[1] += (uint32_t)(t0 >> 29);
+}
+
+// grouped forms kept for the curve formulas' readability (no carries: the
+// compiler interleaves independent operations by itself)
+MV_DEV void fe_mul2(fe& r0, const fe& a0, const fe& b0, fe& r1, const fe& a1, const fe& b1) {
+  fe_mul(r0, a0, b0);
+  fe_mul(r1, a1, b1);
+}
+MV_DEV void fe_sq2(fe& r0, const fe& a0, fe& r1, const fe& a1) {
+  fe_sq(r0, a0);
+  fe_sq(r1, a1);
 }
 
 // ---- canonical form / predicates ----
+// fully reduced value in [0, p)
 MV_DEV void fe_canon(fe& r, const fe& a) {
-  // a tight (< 2p): subtract p iff a + 19 >= 2^255
-  fe t;
-  uint64_t cm;
-  t.v[0] = add_co(a.v[0], 19u, cm);
+  fe t = a;
+  fe_normalize(t);  // limbs < 2^29 + 2^14, value < 2^261 + small
+  // fold bits >= 255 (limb 8 holds bits 232..260) with 2^255 = 19, twice
 #pragma unroll
-  for (int i = 1; i < 8; i++) t.v[i] = addc0(a.v[i], cm);
-  bool ge = (t.v[7] >> 31) != 0;
-  t.v[7] &= 0x7fffffffu;
+  for (int it = 0; it < 2; it++) {
+    uint32_t q = t.v[8] >> 23;
+    t.v[8] &= (1u << 23) - 1;
+    t.v[0] += q * 19u;
+    uint32_t c;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = ge ? t.v[i] : a.v[i];
+    for (int i = 0; i < 8; i++) {
+      c = t.v[i] >> 29;
+      t.v[i] &= M29;
+      t.v[i + 1] += c;
+    }
+  }
+  // now t < 2^255 + tiny: subtract p iff t + 19 >= 2^255
+  uint32_t u[9];
+  uint32_t c = 19;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    uint32_t s = t.v[i] + c;
+    c = s >> 29;
+    u[i] = s & M29;
+  }
+  const bool ge = (u[8] >> 23) != 0;  // t + 19 >= 2^255
+  u[8] &= (1u << 23) - 1;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = ge ? u[i] : t.v[i];
 }
 MV_DEV bool fe_is_zero(const fe& a) {
   fe c;
   fe_canon(c, a);
   uint32_t o = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) o |= c.v[i];
+  for (int i = 0; i < 9; i++) o |= c.v[i];
   return o == 0;
 }
 MV_DEV bool fe_eq(const fe& a, const fe& b) {
@@ -435,13 +214,35 @@ MV_DEV bool fe_is_negative(const fe& a) {
 }
 MV_DEV void fe_cmov(fe& r, const fe& a, bool c) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = c ? a.v[i] : r.v[i];
+  for (int i = 0; i < 9; i++) r.v[i] = c ? a.v[i] : r.v[i];
 }
-// decode 32 LE bytes given as 8 words; bit 255 dropped, value NOT range-checked (ZIP-215)
-MV_DEV void fe_from_words(fe& r, const uint32_t w[8]) {
+// 8 words (< 2^256) -> fe, all 256 bits kept (the top limb takes bits 232..255)
+MV_DEV void fe_from_words_full(fe& r, const uint32_t w[8]) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = w[i];
-  r.v[7] &= 0x7fffffffu;
+  for (int i = 0; i < 9; i++) {
+    const int b = 29 * i, wi = b >> 5, s = b & 31;
+    uint32_t lo = w[wi];
+    uint32_t hi = (wi + 1 < 8) ? w[wi + 1] : 0u;
+    r.v[i] = __builtin_amdgcn_alignbit(hi, lo, s) & M29;
+  }
+}
+// 32 LE bytes as 8 words -> fe; bit 255 dropped, value NOT range-checked (ZIP-215)
+MV_DEV void fe_from_words(fe& r, const uint32_t w[8]) {
+  fe_from_words_full(r, w);
+  r.v[8] &= (1u << 23) - 1;  // bits 232..254
+}
+// canonical fe -> 8 LE words
+MV_DEV void fe_to_words(uint32_t w[8], const fe& a) {
+  fe c;
+  fe_canon(c, a);
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int b = 32 * j, li = b / 29, s = b % 29;
+    uint32_t x = c.v[li] >> s;
+    if (li + 1 < 9) x |= c.v[li + 1] << (29 - s);
+    if (s > 26 && li + 2 < 9) x |= c.v[li + 2] << (58 - s);
+    w[j] = x;
+  }
 }
 
 // ---- exponentiation chains ----

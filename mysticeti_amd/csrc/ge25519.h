@@ -31,8 +31,10 @@ __constant__ const uint32_t K_SQRTM1[8] = {0x4a0ea0b0, 0xc4ee1b27, 0xad2fe478, 0
                                            0x3dfbd7a7, 0x2b4d0099, 0x4fc1df0b, 0x2b832480};
 
 MV_DEV void fe_const(fe& r, const uint32_t* c) {
+  uint32_t w[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = c[i];
+  for (int i = 0; i < 8; i++) w[i] = c[i];
+  fe_from_words_full(r, w);
 }
 
 MV_DEV void p3_identity(p3& p) {
@@ -45,29 +47,40 @@ MV_DEV void cached_identity(cached& c) {
   fe_set(c.YpX, 1); fe_set(c.YmX, 1); fe_set(c.Z, 1); fe_set(c.T2d, 0);
 }
 
+// Bounds (fe25519.h): p3 / p2 coordinates are N; p1p1 coordinates are N or A
+// (all multiplication inputs); cached entries: YpX A, the rest N.
 MV_DEV void p1p1_to_p2(p2& r, const p1p1& c) {
-  fe_mul3(r.X, c.X, c.T, r.Y, c.Y, c.Z, r.Z, c.Z, c.T);
+  fe_mul(r.X, c.X, c.T);
+  fe_mul(r.Y, c.Y, c.Z);
+  fe_mul(r.Z, c.Z, c.T);
 }
 MV_DEV void p1p1_to_p3(p3& r, const p1p1& c) {
-  fe_mul4(r.X, c.X, c.T, r.Y, c.Y, c.Z, r.Z, c.Z, c.T, r.T, c.X, c.Y);
+  fe_mul(r.X, c.X, c.T);
+  fe_mul(r.Y, c.Y, c.Z);
+  fe_mul(r.Z, c.Z, c.T);
+  fe_mul(r.T, c.X, c.Y);
 }
 MV_DEV void p3_to_cached(cached& r, const p3& p) {
   fe d2;
   fe_const(d2, K_D2);
-  fe_addsub2<2u>(r.YpX, p.Y, p.X, r.YmX, p.Y, p.X);
+  fe_add(r.YpX, p.Y, p.X);
+  fe_sub(r.YmX, p.Y, p.X);
   r.Z = p.Z;
   fe_mul(r.T2d, p.T, d2);
 }
-// 2P from projective: 4 squarings (dbl-2008-hwcd, a = -1), grouped 4-way
+// 2P from projective: 4 squarings (dbl-2008-hwcd, a = -1)
 MV_DEV void p2_dbl(p1p1& r, const p2& p) {
-  fe XX, YY, ZZ, S, S2;
+  fe XX, YY, ZZ, S, S2, ZZ2;
   fe_add(S, p.X, p.Y);
-  fe_sq4(XX, p.X, YY, p.Y, ZZ, p.Z, S2, S);
-  fe ZZ2;
-  // Y' = YY + XX, Z' = YY - XX, ZZ2 = 2 ZZ
-  fe_addsub3<2u>(r.Y, YY, XX, r.Z, YY, XX, ZZ2, ZZ, ZZ);
-  // X' = (X+Y)^2 - Y', T' = 2ZZ - Z'
-  fe_addsub2<3u>(r.X, S2, r.Y, r.T, ZZ2, r.Z);
+  fe_sq(XX, p.X);
+  fe_sq(YY, p.Y);
+  fe_sq(ZZ, p.Z);
+  fe_sq(S2, S);
+  fe_add(r.Y, YY, XX);   // A
+  fe_sub(r.Z, YY, XX);   // N
+  fe_add(ZZ2, ZZ, ZZ);   // A
+  fe_sub(r.X, S2, r.Y);  // N
+  fe_sub(r.T, ZZ2, r.Z); // N
 }
 MV_DEV void p3_dbl(p1p1& r, const p3& p) {
   p2 q;
@@ -76,23 +89,37 @@ MV_DEV void p3_dbl(p1p1& r, const p3& p) {
 }
 // P + Q (Q cached): 4 multiplications
 MV_DEV void p3_add_cached(p1p1& r, const p3& p, const cached& q) {
-  fe PP, MM, TT, ZZ, ypx, ymx;
-  fe_addsub2<2u>(ypx, p.Y, p.X, ymx, p.Y, p.X);
-  fe_mul4(PP, ypx, q.YpX, MM, ymx, q.YmX, TT, p.T, q.T2d, ZZ, p.Z, q.Z);
-  fe_add(ZZ, ZZ, ZZ);
-  fe_addsub4<9u>(r.X, PP, MM, r.Y, PP, MM, r.Z, ZZ, TT, r.T, ZZ, TT);
+  fe PP, MM, TT, ZZ, ZZ2, ypx, ymx;
+  fe_add(ypx, p.Y, p.X);
+  fe_sub(ymx, p.Y, p.X);
+  fe_mul(PP, ypx, q.YpX);
+  fe_mul(MM, ymx, q.YmX);
+  fe_mul(TT, p.T, q.T2d);
+  fe_mul(ZZ, p.Z, q.Z);
+  fe_add(ZZ2, ZZ, ZZ);      // A
+  fe_sub(r.X, PP, MM);      // N
+  fe_add(r.Y, PP, MM);      // A
+  fe_addn(r.Z, ZZ2, TT);    // A + N: normalised
+  fe_sub(r.T, ZZ2, TT);     // N
 }
 // P + Q (Q precomp, Z = 1): 3 multiplications
 MV_DEV void p3_add_precomp(p1p1& r, const p3& p, const precomp& q) {
   fe PP, MM, TT, Z2, ypx, ymx;
-  fe_addsub3<2u>(ypx, p.Y, p.X, ymx, p.Y, p.X, Z2, p.Z, p.Z);
-  fe_mul3(PP, ypx, q.ypx, MM, ymx, q.ymx, TT, p.T, q.xy2d);
-  fe_addsub4<9u>(r.X, PP, MM, r.Y, PP, MM, r.Z, Z2, TT, r.T, Z2, TT);
+  fe_add(ypx, p.Y, p.X);
+  fe_sub(ymx, p.Y, p.X);
+  fe_mul(PP, ypx, q.ypx);
+  fe_mul(MM, ymx, q.ymx);
+  fe_mul(TT, p.T, q.xy2d);
+  fe_add(Z2, p.Z, p.Z);
+  fe_sub(r.X, PP, MM);
+  fe_add(r.Y, PP, MM);
+  fe_addn(r.Z, Z2, TT);
+  fe_sub(r.T, Z2, TT);
 }
 // conditional negation of table entries: -(x, y) = (-x, y) swaps y+x / y-x and negates xy
 MV_DEV void cached_cneg(cached& c, bool neg) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < 9; i++) {
     uint32_t a = c.YpX.v[i], b = c.YmX.v[i];
     c.YpX.v[i] = neg ? b : a;
     c.YmX.v[i] = neg ? a : b;
@@ -103,7 +130,7 @@ MV_DEV void cached_cneg(cached& c, bool neg) {
 }
 MV_DEV void precomp_cneg(precomp& c, bool neg) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < 9; i++) {
     uint32_t a = c.ypx.v[i], b = c.ymx.v[i];
     c.ypx.v[i] = neg ? b : a;
     c.ymx.v[i] = neg ? a : b;

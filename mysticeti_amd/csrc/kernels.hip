@@ -26,19 +26,62 @@
 namespace mv {
 
 // ---------------------------------------------------------------- tables
+// Table entries are stored in the field's limb form (9 x 29-bit words per element):
+// B entries (precomp, 27 words + 1 pad = 7 uint4) in LDS, the per-lane variable-base
+// entries (cached, 36 words = 9 uint4) in the per-wave HBM scratch.
 constexpr int BT_ENTRIES = 129;  // [0..128]B
-constexpr int BT_QUADS = 6;      // 3 fe x 2 uint4
+constexpr int BT_QUADS = 7;
 constexpr int AT_ENTRIES = 9;    // [0..8](-A)
-constexpr int AT_QUADS = 8;      // 4 fe x 2 uint4
+constexpr int AT_QUADS = 9;
 
-MV_DEV uint4 q4(const fe& f, int h) {
-  return make_uint4(f.v[4 * h], f.v[4 * h + 1], f.v[4 * h + 2], f.v[4 * h + 3]);
+template <int NW>
+MV_DEV void words_to_quads(uint4 (&q)[(NW + 3) / 4], const uint32_t (&w)[NW]) {
+#pragma unroll
+  for (int i = 0; i < (NW + 3) / 4; i++)
+    q[i] = make_uint4(w[4 * i], 4 * i + 1 < NW ? w[4 * i + 1] : 0u, 4 * i + 2 < NW ? w[4 * i + 2] : 0u,
+                      4 * i + 3 < NW ? w[4 * i + 3] : 0u);
 }
-MV_DEV void uq4(fe& f, int h, uint4 q) {
-  f.v[4 * h] = q.x;
-  f.v[4 * h + 1] = q.y;
-  f.v[4 * h + 2] = q.z;
-  f.v[4 * h + 3] = q.w;
+template <int NW>
+MV_DEV void quads_to_words(uint32_t (&w)[NW], const uint4 (&q)[(NW + 3) / 4]) {
+#pragma unroll
+  for (int i = 0; i < (NW + 3) / 4; i++) {
+    w[4 * i] = q[i].x;
+    if (4 * i + 1 < NW) w[4 * i + 1] = q[i].y;
+    if (4 * i + 2 < NW) w[4 * i + 2] = q[i].z;
+    if (4 * i + 3 < NW) w[4 * i + 3] = q[i].w;
+  }
+}
+MV_DEV void cached_to_quads(uint4 (&q)[9], const cached& c) {
+  uint32_t w[36];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    w[i] = c.YpX.v[i];
+    w[9 + i] = c.YmX.v[i];
+    w[18 + i] = c.Z.v[i];
+    w[27 + i] = c.T2d.v[i];
+  }
+  words_to_quads<36>(q, w);
+}
+MV_DEV void quads_to_cached(cached& c, const uint4 (&q)[9]) {
+  uint32_t w[36];
+  quads_to_words<36>(w, q);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    c.YpX.v[i] = w[i];
+    c.YmX.v[i] = w[9 + i];
+    c.Z.v[i] = w[18 + i];
+    c.T2d.v[i] = w[27 + i];
+  }
+}
+MV_DEV void precomp_to_quads(uint4 (&q)[7], const precomp& c) {
+  uint32_t w[27];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    w[i] = c.ypx.v[i];
+    w[9 + i] = c.ymx.v[i];
+    w[18 + i] = c.xy2d.v[i];
+  }
+  words_to_quads<27>(q, w);
 }
 
 MV_DEV void lds_btab_load(uint4* sm, const uint4* g) {
@@ -48,13 +91,18 @@ MV_DEV void lds_btab_load(uint4* sm, const uint4* g) {
 // B-table lookup with sign: digit in [-128, 128]
 MV_DEV void btab_get(precomp& p, const uint4* sm, int digit) {
   int e = digit < 0 ? -digit : digit;
-  const uint4* q = sm + e * BT_QUADS;
-  uq4(p.ypx, 0, q[0]);
-  uq4(p.ypx, 1, q[1]);
-  uq4(p.ymx, 0, q[2]);
-  uq4(p.ymx, 1, q[3]);
-  uq4(p.xy2d, 0, q[4]);
-  uq4(p.xy2d, 1, q[5]);
+  const uint4* qp = sm + e * BT_QUADS;
+  uint4 q[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) q[i] = qp[i];
+  uint32_t w[27];
+  quads_to_words<27>(w, q);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    p.ypx.v[i] = w[i];
+    p.ymx.v[i] = w[9 + i];
+    p.xy2d.v[i] = w[18 + i];
+  }
   precomp_cneg(p, digit < 0);
 }
 
@@ -62,28 +110,20 @@ MV_DEV void btab_get(precomp& p, const uint4* sm, int digit) {
 // table build writes 1 KiB per wave-instruction and lookups touch <= 9 segments.
 MV_DEV void atab_put(uint4* wave_base, int e, int lane, const cached& c) {
   uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
-  p[0 * 64] = q4(c.YpX, 0);
-  p[1 * 64] = q4(c.YpX, 1);
-  p[2 * 64] = q4(c.YmX, 0);
-  p[3 * 64] = q4(c.YmX, 1);
-  p[4 * 64] = q4(c.Z, 0);
-  p[5 * 64] = q4(c.Z, 1);
-  p[6 * 64] = q4(c.T2d, 0);
-  p[7 * 64] = q4(c.T2d, 1);
+  uint4 q[9];
+  cached_to_quads(q, c);
+#pragma unroll
+  for (int i = 0; i < 9; i++) p[i * 64] = q[i];
 }
 // raw entry load; the sign is applied at use time (cached_cneg) so the gather's
 // latency hides behind the window's doublings
 MV_DEV void atab_load(cached& c, const uint4* wave_base, int lane, int digit) {
   int e = digit < 0 ? -digit : digit;
   const uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
-  uq4(c.YpX, 0, p[0 * 64]);
-  uq4(c.YpX, 1, p[1 * 64]);
-  uq4(c.YmX, 0, p[2 * 64]);
-  uq4(c.YmX, 1, p[3 * 64]);
-  uq4(c.Z, 0, p[4 * 64]);
-  uq4(c.Z, 1, p[5 * 64]);
-  uq4(c.T2d, 0, p[6 * 64]);
-  uq4(c.T2d, 1, p[7 * 64]);
+  uint4 q[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) q[i] = p[i * 64];
+  quads_to_cached(c, q);
 }
 
 MV_DEV void load8(uint32_t w[8], const uint8_t* p) {
@@ -104,11 +144,10 @@ MV_DEV void p3_compress(uint32_t out[8], const p3& p) {
   fe_invert(zi, p.Z);
   fe_mul(x, p.X, zi);
   fe_mul(y, p.Y, zi);
-  fe_canon(x, x);
-  fe_canon(y, y);
-#pragma unroll
-  for (int i = 0; i < 8; i++) out[i] = y.v[i];
-  out[7] |= (x.v[0] & 1u) << 31;
+  uint32_t xw[8];
+  fe_to_words(xw, x);
+  fe_to_words(out, y);
+  out[7] |= (xw[0] & 1u) << 31;
 }
 
 // [s]B for s < 2^253 given as signed radix-256 digits (LDS table)
@@ -168,29 +207,46 @@ __global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
   fe_canon(pc.ypx, pc.ypx);
   fe_canon(pc.ymx, pc.ymx);
   fe_canon(pc.xy2d, pc.xy2d);
+  uint4 q[7];
+  precomp_to_quads(q, pc);
   uint4* o = out + j * BT_QUADS;
-  o[0] = q4(pc.ypx, 0);
-  o[1] = q4(pc.ypx, 1);
-  o[2] = q4(pc.ymx, 0);
-  o[3] = q4(pc.ymx, 1);
-  o[4] = q4(pc.xy2d, 0);
-  o[5] = q4(pc.xy2d, 1);
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = q[i];
 }
 
 // Per-wave scratch layout (uint4 units, each [..][lane]): the variable-base table,
 // then R (X, Y, T; Z = 1) and the recoded scalars, which are parked in HBM during
 // the ladder instead of holding 48 VGPRs.
-constexpr int SCR_R = AT_ENTRIES * AT_QUADS;  // 72
-constexpr int SCR_DIG = SCR_R + 6;            // 78: 8 x uint2 per lane = 4 quads
-constexpr int WAVE_QUADS = SCR_DIG + 4;       // 82
+constexpr int SCR_R = AT_ENTRIES * AT_QUADS;  // 81: R's X, Y, T (27 words -> 7 quads)
+constexpr int SCR_DIG = SCR_R + 7;            // 88: 8 x uint2 per lane = 4 quads
+constexpr int WAVE_QUADS = SCR_DIG + 4;       // 92
 
-MV_DEV void scr_put_fe(uint4* wave_base, int q, int lane, const fe& f) {
-  wave_base[q * 64 + lane] = q4(f, 0);
-  wave_base[(q + 1) * 64 + lane] = q4(f, 1);
+MV_DEV void scr_put_xyt(uint4* wave_base, int q0, int lane, const p3& P) {
+  uint32_t w[27];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    w[i] = P.X.v[i];
+    w[9 + i] = P.Y.v[i];
+    w[18 + i] = P.T.v[i];
+  }
+  uint4 q[7];
+  words_to_quads<27>(q, w);
+#pragma unroll
+  for (int i = 0; i < 7; i++) wave_base[(q0 + i) * 64 + lane] = q[i];
 }
-MV_DEV void scr_get_fe(fe& f, const uint4* wave_base, int q, int lane) {
-  uq4(f, 0, wave_base[q * 64 + lane]);
-  uq4(f, 1, wave_base[(q + 1) * 64 + lane]);
+MV_DEV void scr_get_xyt(p3& P, const uint4* wave_base, int q0, int lane) {
+  uint4 q[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) q[i] = wave_base[(q0 + i) * 64 + lane];
+  uint32_t w[27];
+  quads_to_words<27>(w, q);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    P.X.v[i] = w[i];
+    P.Y.v[i] = w[9 + i];
+    P.T.v[i] = w[18 + i];
+  }
+  fe_set(P.Z, 1);
 }
 
 // One signature per lane. pk rows are read at key_idx[i] when key_idx != nullptr.
@@ -219,9 +275,7 @@ __global__ void __launch_bounds__(256, MINW)
     s_ok = sc_is_canonical(sw);
     p3 A, R;
     decompress_x2(A, okA, aw, R, okR, rw);
-    scr_put_fe(wave_tab, SCR_R + 0, lane, R.X);
-    scr_put_fe(wave_tab, SCR_R + 2, lane, R.Y);
-    scr_put_fe(wave_tab, SCR_R + 4, lane, R.T);
+    scr_put_xyt(wave_tab, SCR_R, lane, R);
 
     // k = SHA-512(R || A || M) mod l over the original encodings
     uint32_t kin[24], h[16], k[8];
@@ -298,10 +352,7 @@ __global__ void __launch_bounds__(256, MINW)
   // cofactored check: [8](R - R') == identity
   p3 R, Rp;
   p1p1_to_p3(Rp, Q);
-  scr_get_fe(R.X, wave_tab, SCR_R + 0, lane);
-  scr_get_fe(R.Y, wave_tab, SCR_R + 2, lane);
-  scr_get_fe(R.T, wave_tab, SCR_R + 4, lane);
-  fe_set(R.Z, 1);
+  scr_get_xyt(R, wave_tab, SCR_R, lane);
   p3 nRp;
   p3_neg(nRp, Rp);
   cached cR;
@@ -469,11 +520,8 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
     y[i] = 0;
   }
   fe a, b, r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    a.v[i] = x[i];
-    b.v[i] = x[8 + i];
-  }
+  fe_from_words_full(a, x);
+  fe_from_words_full(b, x + 8);
   switch (op) {
     case 0: fe_mul(r, a, b); fe_canon(r, r); break;
     case 1: fe_sq(r, a); fe_canon(r, r); break;
@@ -481,7 +529,7 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
     case 3: fe_sub(r, a, b); fe_canon(r, r); break;
     case 4: fe_invert(r, a); fe_canon(r, r); break;
     case 5: fe_pow_p58(r, a); fe_canon(r, r); break;
-    case 6: fe_mul_small(r, a, b.v[0]); fe_canon(r, r); break;
+    case 6: fe_mul_small(r, a, x[8]); fe_canon(r, r); break;
     case 7: {  // ZIP-215 decode of a: x (canonical) and the ok flag in word 8
       p3 A, B;
       bool oa, ob;
@@ -490,7 +538,15 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
       y[8] = oa ? 1u : 0u;
       break;
     }
-    case 8: sc_reduce512(r.v, x); break;
+    case 8: {
+      uint32_t k[8];
+      sc_reduce512(k, x);
+#pragma unroll
+      for (int i = 0; i < 8; i++) out[16 * (size_t)gid + i] = k[i];
+#pragma unroll
+      for (int i = 8; i < 16; i++) out[16 * (size_t)gid + i] = 0;
+      return;
+    }
     case 9: {  // sha512 of 64 bytes
       sha512_short(y, x, 64);
 #pragma unroll
@@ -503,8 +559,13 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
       sc_recode256(sd, x);
       p3 P;
       basemul(P, sd, btab);
-      p3_compress(r.v, P);
-      break;
+      uint32_t enc[8];
+      p3_compress(enc, P);
+#pragma unroll
+      for (int i = 0; i < 8; i++) out[16 * (size_t)gid + i] = enc[i];
+#pragma unroll
+      for (int i = 8; i < 16; i++) out[16 * (size_t)gid + i] = 0;
+      return;
     }
     case 12: {  // fe_canon of raw 255-bit input
       fe_from_words(r, x);
@@ -513,8 +574,12 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
     }
     default: fe_set(r, 0);
   }
+  {
+    uint32_t rw[8];
+    fe_to_words(rw, r);
 #pragma unroll
-  for (int i = 0; i < 8; i++) y[i] = r.v[i];
+    for (int i = 0; i < 8; i++) y[i] = rw[i];
+  }
 #pragma unroll
   for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
 }

@@ -14,7 +14,7 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
 
-constexpr int ITERS = 2048;
+constexpr int ITERS = 65536;
 constexpr int ACC = 8;
 
 // One op per macro invocation on accumulator i.
@@ -31,6 +31,9 @@ constexpr int ACC = 8;
 #define OP_LSHR64(i)  asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(q[i]))
 #define OP_FMA64(i)   asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(d[i]) : "v"(dx), "v"(dy))
 #define OP_CNDMASK(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r[i]) : "v"(b))
+#define OP_MOV(i)     asm volatile("v_mov_b32 %0, %1" : "=v"(r[i]) : "v"(r[(i + 1) % ACC]))
+#define OP_LSHLADD64(i) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(q[i]) : "v"(q[(i + 1) % ACC]))
+#define OP_MAC(i)     asm volatile("v_mad_u64_u32 %0, s[40:41], %2, %3, %0\n\tv_addc_co_u32 %1, s[40:41], %1, 0, s[40:41]" : "+v"(q[i]), "+v"(r[i]) : "v"(a), "v"(b) : "s40", "s41")
 
 #define KERNEL(NAME, OPM, OPS_PER)                                                     \
   __global__ void __launch_bounds__(256) k_##NAME(uint32_t* out, uint32_t a, uint32_t b, int iters) { \
@@ -69,6 +72,8 @@ KERNEL(add3_u32, OP_ADD3, 1)
 KERNEL(lshrrev_b64, OP_LSHR64, 1)
 KERNEL(fma_f64, OP_FMA64, 1)
 KERNEL(cndmask_b32, OP_CNDMASK, 1)
+KERNEL(mov_b32, OP_MOV, 1)
+KERNEL(lshl_add_u64, OP_LSHLADD64, 1)
 
 typedef void (*kfn)(uint32_t*, uint32_t, uint32_t, int);
 
@@ -86,11 +91,11 @@ static int run(const char* name, kfn k, kfn k1, int instrs_per_op, uint32_t* dou
   double instr_rate = ops * instrs_per_op / (ms * 1e-3);
   // latency: single wave, single chain
   CHECK(hipEventRecord(e0));
-  hipLaunchKernelGGL(k1, dim3(1), dim3(64), 0, 0, dout, 3u, 5u, ITERS);
+  hipLaunchKernelGGL(k1, dim3(1), dim3(64), 0, 0, dout, 3u, 5u, ITERS / 16);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms1; CHECK(hipEventElapsedTime(&ms1, e0, e1));
-  double lat_ns = ms1 * 1e6 / (ITERS * 4.0);
+  double lat_ns = ms1 * 1e6 / (ITERS / 16 * 4.0);
   printf("{\"instr\": \"%s\", \"lane_ops_per_s\": %.4e, \"instr_lane_rate\": %.4e, \"dep_latency_ns_per_op\": %.3f, \"ms\": %.3f}\n",
          name, ops / (ms * 1e-3), instr_rate, lat_ns, ms);
   return 0;
@@ -116,5 +121,7 @@ int main() {
   RUN(lshrrev_b64, 1)
   RUN(fma_f64, 1)
   RUN(cndmask_b32, 1)
+  RUN(mov_b32, 1)
+  RUN(lshl_add_u64, 1)
   return 0;
 }
