@@ -113,12 +113,14 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     import mysticeti_amd as M
+    from mysticeti_amd.dist import all_ranks_ok, shard_range, timed_region
 
     eng = M.Engine(devices=(local_rank,))
     n = args.batch
 
     # ---- corpus: host hashes, GPU signing (library signer), all resident in HBM ----
-    seed_h, msg_h = corpus_host(rank * n, n)
+    lo, _ = shard_range(rank, world, n)
+    seed_h, msg_h = corpus_host(lo, n)
     d_seed = torch.from_numpy(seed_h.copy()).to(dev)
     d_msg = torch.from_numpy(msg_h.copy()).to(dev)
     d_pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
@@ -137,26 +139,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    state = {"first": True}
+
+    def timed_step():
+        if state["first"]:
+            ev0.record(stream)  # HIP events on the launch stream bracket the K launches
+            state["first"] = False
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+
+    def sync():
+        torch.cuda.synchronize(dev)
+
+    elapsed = timed_region(timed_step, args.steps, lambda: (ev1.record(stream) if not state["first"] else None,
+                                                            sync()), dist)
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step, on this stream
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     status = d_status.cpu().numpy()
     accepted = int((status == 0).sum())
@@ -166,10 +163,7 @@ def main():
         gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_config2.json")))
         parity = hashlib.sha256(status.tobytes()).hexdigest() == gold["sha256_status"] and \
             hashlib.sha256(d_sig.cpu().numpy().tobytes()).hexdigest() == gold["sha256_sig"]
-    if dist:
-        tk = torch.tensor([0 if ok else 1], dtype=torch.int64)
-        dist.all_reduce(tk, op=dist.ReduceOp.SUM)
-        ok = int(tk.item()) == 0
+    ok = all_ranks_ok(ok, dist)
 
     total = n * world * args.steps
     value = total / elapsed

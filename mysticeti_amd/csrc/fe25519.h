@@ -77,57 +77,52 @@ MV_DEV void fe_neg(fe& r, const fe& a) {
   fe_sub(r, z, a);
 }
 
-// 17 column sums (each < 2^63.3 + 2^47) -> N
-MV_DEV void fe_reduce_cols(fe& r, uint64_t (&c)[17]) {
-  // 1. normalise the high columns 9..16 into 29-bit limbs h9..h16 plus h17 (< 2^32)
-  uint32_t h[9];
+// Column-scanning reduction, shared by mul and sq. col(k) returns the 64-bit sum
+// of column k (< 2^63.3). High columns 9..16 are normalised as they are produced
+// (carry chain h) and folded at once with 2^261 = 1216, so only the 9 low
+// column sums are live at a time.
+template <class Col>
+MV_DEV void fe_reduce_scan(fe& r, Col col) {
+  uint64_t lo[9];
 #pragma unroll
-  for (int k = 9; k < 16; k++) {
-    h[k - 9] = (uint32_t)c[k] & M29;
-    c[k + 1] += c[k] >> 29;
+  for (int k = 0; k < 9; k++) lo[k] = col(k);
+  uint64_t h = 0;
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+    h += col(k);  // < 2^63.3 + 2^35
+    lo[k - 9] += (uint64_t)((uint32_t)h & M29) * R261;
+    h >>= 29;
   }
-  h[7] = (uint32_t)c[16] & M29;
-  h[8] = (uint32_t)(c[16] >> 29);
-  // 2. fold: 2^(29k) = 1216 * 2^(29(k-9)) for k >= 9
-#pragma unroll
-  for (int k = 0; k < 9; k++) c[k] += (uint64_t)h[k] * R261;
-  // 3. normalise the low columns; the carry out of limb 8 has weight 2^261
+  lo[8] += (uint64_t)(uint32_t)h * R261;  // h < 2^32: carry out of column 16
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    r.v[k] = (uint32_t)c[k] & M29;
-    c[k + 1] += c[k] >> 29;
+    r.v[k] = (uint32_t)lo[k] & M29;
+    lo[k + 1] += lo[k] >> 29;
   }
-  r.v[8] = (uint32_t)c[8] & M29;
-  uint64_t top = c[8] >> 29;  // < 2^35
-  uint64_t t0 = (uint64_t)r.v[0] + top * R261;  // < 2^46
+  r.v[8] = (uint32_t)lo[8] & M29;
+  uint64_t t0 = (uint64_t)r.v[0] + (lo[8] >> 29) * R261;  // top < 2^35
   r.v[0] = (uint32_t)t0 & M29;
   r.v[1] += (uint32_t)(t0 >> 29);  // < 2^29 + 2^17
 }
 
 MV_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
-  uint64_t c[17];
+  fe_reduce_scan(r, [&](int k) {
+    uint64_t c = 0;
 #pragma unroll
-  for (int k = 0; k < 17; k++) c[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 9; i++)
-#pragma unroll
-    for (int j = 0; j < 9; j++) c[i + j] += (uint64_t)a.v[i] * b.v[j];
-  fe_reduce_cols(r, c);
+    for (int i = (k > 8 ? k - 8 : 0); i <= (k < 8 ? k : 8); i++) c += (uint64_t)a.v[i] * b.v[k - i];
+    return c;
+  });
 }
 MV_DEV void fe_sq(fe& r, const fe& a) {
   uint32_t a2[9];
 #pragma unroll
   for (int i = 0; i < 9; i++) a2[i] = a.v[i] << 1;  // < 2^31.01
-  uint64_t c[17];
+  fe_reduce_scan(r, [&](int k) {
+    uint64_t c = (k & 1) ? 0 : (uint64_t)a.v[k >> 1] * a.v[k >> 1];
 #pragma unroll
-  for (int k = 0; k < 17; k++) c[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    c[2 * i] += (uint64_t)a.v[i] * a.v[i];
-#pragma unroll
-    for (int j = i + 1; j < 9; j++) c[i + j] += (uint64_t)a2[i] * a.v[j];
-  }
-  fe_reduce_cols(r, c);
+    for (int i = (k > 8 ? k - 8 : 0); i < k - i; i++) c += (uint64_t)a2[i] * a.v[k - i];
+    return c;
+  });
 }
 MV_DEV void fe_sqn(fe& r, const fe& a, int n) {
   fe_sq(r, a);

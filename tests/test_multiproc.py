@@ -1,0 +1,57 @@
+"""CPU: the N>1 bench path (one process per GPU, gloo host collectives only) with
+world_size 2 on the CPU: disjoint weak-scaling shards, max-over-ranks timing, and
+per-rank verification of its own corpus slice (checked by the oracle)."""
+import hashlib
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from mysticeti_amd.dist import all_ranks_ok, shard_range, timed_region
+
+
+def _worker(rank, world, port, out):
+    import time
+
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as O
+
+    lo, hi = shard_range(rank, world, 64)
+    seed = np.frombuffer(b"".join(hashlib.sha512(b"mysti-seed" + struct.pack("<Q", i)).digest()[:32]
+                                  for i in range(lo, hi)), dtype=np.uint8).reshape(-1, 32)
+    msg = np.frombuffer(b"".join(hashlib.blake2b(b"mysti-msg" + struct.pack("<Q", i), digest_size=32).digest()
+                                 for i in range(lo, hi)), dtype=np.uint8).reshape(-1, 32)
+    pk, sig = O.sign_batch(seed, msg, 1)
+    ok = bool((O.verify_batch(pk, sig, msg, 1) == 0).all())
+    # rank 1 is deliberately slower: the reported time must be the max over ranks
+    el = timed_region(lambda: time.sleep(0.05 * (rank + 1)), 2, lambda: None, dist)
+    out[rank] = (lo, hi, el, all_ranks_ok(ok, dist), all_ranks_ok(rank == 0, dist))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo():
+    world = 2
+    port = 29500 + os.getpid() % 1000
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+    r0, r1 = out[0], out[1]
+    assert (r0[0], r0[1]) == (0, 64) and (r1[0], r1[1]) == (64, 128)
+    assert r0[2] == r1[2] and r0[2] >= 0.2  # both report the slower rank's time
+    assert r0[3] and r1[3]  # every shard verified
+    assert not r0[4] and not r1[4]  # one failing rank fails the job
+
+
+def test_shard_ranges_cover_without_overlap():
+    for world in (1, 2, 4, 8):
+        seen = []
+        for r in range(world):
+            lo, hi = shard_range(r, world, 1000)
+            seen.extend(range(lo, hi))
+        assert seen == list(range(world * 1000))
