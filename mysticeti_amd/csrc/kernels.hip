@@ -1,8 +1,10 @@
 // HIP kernels of the StatementBlock verification engine (gfx950 only).
 //
-//   k_btable_init    fixed-base table [j]B, j = 0..128, affine (y+x, y-x, 2dxy)
+//   k_btable_init    fixed-base tables [j]B and [j](2^124 B), j = 0..128, affine
+//                    (y+x, y-x, 2dxy)
 //   k_verify         ZIP-215 ed25519 verify, one signature per lane (ed25519-consensus
-//                    VerificationKey::verify, called at mysticeti-core/src/crypto.rs:188)
+//                    VerificationKey::verify, called at mysticeti-core/src/crypto.rs:188),
+//                    on half-size scalars (scalar25519.h sc_halfsize)
 //   k_sign           RFC 8032 signing, one per lane (crypto.rs:199-223, corpus generation)
 //   k_blake2b        Blake2b-256 of staged byte strings (crypto.rs:34 BlockHasher)
 //   k_block_hash     signed message Blake2b(P) and block digest Blake2b(P || sig) of
@@ -11,8 +13,8 @@
 //   k_selftest       field / scalar primitives for the parity tests
 //
 // The verify kernel is INT32-VALU bound: HBM traffic is 128 B of
-// input per signature plus the per-lane variable-base table (9 cached points,
-// written once, read 64 times, L2/MALL-resident per wave).
+// input per signature plus the per-lane variable-base tables (2 x 9 cached points,
+// written once, read 32 times each, L2/MALL-resident per wave).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -29,10 +31,12 @@ namespace mv {
 // Table entries are stored in the field's limb form (9 x 29-bit words per element):
 // B entries (precomp, 27 words + 1 pad = 7 uint4) in LDS, the per-lane variable-base
 // entries (cached, 36 words = 9 uint4) in the per-wave HBM scratch.
-constexpr int BT_ENTRIES = 129;  // [0..128]B
+constexpr int BT_ENTRIES = 129;  // [0..128]B, then [0..128](2^124 B)
 constexpr int BT_QUADS = 7;
-constexpr int AT_ENTRIES = 9;    // [0..8](-A)
+constexpr int BT_TABLE = BT_ENTRIES * BT_QUADS;  // uint4 per fixed-base table
+constexpr int AT_ENTRIES = 9;    // [0..8](-A), [0..8](-R)
 constexpr int AT_QUADS = 9;
+constexpr int AT_TABLE = AT_ENTRIES * AT_QUADS;  // uint4 per lane per variable-base table
 
 template <int NW>
 MV_DEV void words_to_quads(uint4 (&q)[(NW + 3) / 4], const uint32_t (&w)[NW]) {
@@ -84,8 +88,8 @@ MV_DEV void precomp_to_quads(uint4 (&q)[7], const precomp& c) {
   words_to_quads<27>(q, w);
 }
 
-MV_DEV void lds_btab_load(uint4* sm, const uint4* g) {
-  for (int i = threadIdx.x; i < BT_ENTRIES * BT_QUADS; i += blockDim.x) sm[i] = g[i];
+MV_DEV void lds_btab_load(uint4* sm, const uint4* g, int quads) {
+  for (int i = threadIdx.x; i < quads; i += blockDim.x) sm[i] = g[i];
   __syncthreads();
 }
 // B-table lookup with sign: digit in [-128, 128]
@@ -106,8 +110,9 @@ MV_DEV void btab_get(precomp& p, const uint4* sm, int digit) {
   precomp_cneg(p, digit < 0);
 }
 
-// Per-wave A-table scratch: [entry][quad][lane] of uint4, lanes contiguous so the
-// table build writes 1 KiB per wave-instruction and lookups touch <= 9 segments.
+// Per-wave variable-base table scratch (wave_base = the table's first uint4):
+// [entry][quad][lane] of uint4, lanes contiguous so the table build writes 1 KiB per
+// wave-instruction and lookups touch <= 9 segments.
 MV_DEV void atab_put(uint4* wave_base, int e, int lane, const cached& c) {
   uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
   uint4 q[9];
@@ -177,7 +182,8 @@ MV_DEV void basemul(p3& out, const uint32_t sd[8], const uint4* btab) {
 
 // ---------------------------------------------------------------- kernels
 __global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = threadIdx.x;
+  const int t = blockIdx.x;  // 0: B, 1: 2^124 B
   if (j >= BT_ENTRIES) return;
   // B = decompress(4/5, sign 0)
   const uint32_t by[8] = {0x66666658, 0x66666666, 0x66666666, 0x66666666,
@@ -185,14 +191,27 @@ __global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
   p3 B, R;
   bool okB, okR;
   decompress_x2(B, okB, by, R, okR, by);
+  if (t == 1) {
+    p2 P;
+    p1p1 Q;
+    P.X = B.X;
+    P.Y = B.Y;
+    P.Z = B.Z;
+    for (int i = 0; i < 123; i++) {
+      p2_dbl(Q, P);
+      p1p1_to_p2(P, Q);
+    }
+    p2_dbl(Q, P);
+    p1p1_to_p3(B, Q);
+  }
   p3 acc;
   p3_identity(acc);
   cached cb;
   p3_to_cached(cb, B);
   for (int i = 0; i < j; i++) {
-    p1p1 t;
-    p3_add_cached(t, acc, cb);
-    p1p1_to_p3(acc, t);
+    p1p1 q;
+    p3_add_cached(q, acc, cb);
+    p1p1_to_p3(acc, q);
   }
   fe zi, x, y, xy, d2;
   fe_invert(zi, acc.Z);
@@ -209,60 +228,56 @@ __global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
   fe_canon(pc.xy2d, pc.xy2d);
   uint4 q[7];
   precomp_to_quads(q, pc);
-  uint4* o = out + j * BT_QUADS;
+  uint4* o = out + t * BT_TABLE + j * BT_QUADS;
 #pragma unroll
   for (int i = 0; i < 7; i++) o[i] = q[i];
 }
 
-// Per-wave scratch layout (uint4 units, each [..][lane]): the variable-base table,
-// then R (X, Y, T; Z = 1) and the recoded scalars, which are parked in HBM during
-// the ladder instead of holding 48 VGPRs.
-constexpr int SCR_R = AT_ENTRIES * AT_QUADS;  // 81: R's X, Y, T (27 words -> 7 quads)
-constexpr int SCR_DIG = SCR_R + 7;            // 88: 8 x uint2 per lane = 4 quads
-constexpr int WAVE_QUADS = SCR_DIG + 4;       // 92
+// Per-wave scratch layout (uint4 units, each [..][lane]): the two variable-base
+// tables, then the recoded scalars, parked in HBM during the ladder instead of
+// holding 16 VGPRs.
+constexpr int SCR_AT = 0;                  // [0..8](-A) or [0..8](A), by the sign of c
+constexpr int SCR_RT = AT_TABLE;           // [0..8](-R)
+constexpr int SCR_DIG = 2 * AT_TABLE;      // 4 groups x uint4 (c, d, e lo, e hi)
+constexpr int WAVE_QUADS = SCR_DIG + 4;    // 166
 
-MV_DEV void scr_put_xyt(uint4* wave_base, int q0, int lane, const p3& P) {
-  uint32_t w[27];
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    w[i] = P.X.v[i];
-    w[9 + i] = P.Y.v[i];
-    w[18 + i] = P.T.v[i];
+// [0..8]P as cached points into a per-wave table
+MV_DEV void vtab_build(uint4* tab, int lane, const p3& P) {
+  cached c1, c;
+  cached_identity(c);
+  atab_put(tab, 0, lane, c);
+  p3_to_cached(c1, P);
+  atab_put(tab, 1, lane, c1);
+  p3 cur = P;
+  for (int j = 2; j <= 8; j++) {
+    p1p1 t;
+    p3_add_cached(t, cur, c1);
+    p1p1_to_p3(cur, t);
+    p3_to_cached(c, cur);
+    atab_put(tab, j, lane, c);
   }
-  uint4 q[7];
-  words_to_quads<27>(q, w);
-#pragma unroll
-  for (int i = 0; i < 7; i++) wave_base[(q0 + i) * 64 + lane] = q[i];
-}
-MV_DEV void scr_get_xyt(p3& P, const uint4* wave_base, int q0, int lane) {
-  uint4 q[7];
-#pragma unroll
-  for (int i = 0; i < 7; i++) q[i] = wave_base[(q0 + i) * 64 + lane];
-  uint32_t w[27];
-  quads_to_words<27>(w, q);
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    P.X.v[i] = w[i];
-    P.Y.v[i] = w[9 + i];
-    P.T.v[i] = w[18 + i];
-  }
-  fe_set(P.Z, 1);
 }
 
 // One signature per lane. pk rows are read at key_idx[i] when key_idx != nullptr.
 // MINW = minimum waves per SIMD (2 -> <= 256 VGPRs, 1 -> <= 512).
+//
+// Checks [8]([e]B - [c]A - [d]R) == O with e = d*s mod l, (c, d) = sc_halfsize(k),
+// which holds iff the ZIP-215 equation [8]([s]B - [k]A - R) == O does (see
+// sc_halfsize). e's signed radix-256 digits 0..15 go against [j]B at the even 4-bit
+// windows, digits 16..31 against [j](2^124 B) at the odd ones, so every one of the
+// 32 windows does 4 doublings and three additions (A, R, B or 2^124 B).
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW)
     k_verify(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
              const uint32_t* __restrict__ key_idx, uint32_t n, const uint4* __restrict__ btab_g,
              uint4* __restrict__ scratch, uint8_t* __restrict__ status) {
-  __shared__ uint4 btab[BT_ENTRIES * BT_QUADS];
-  lds_btab_load(btab, btab_g);
+  __shared__ uint4 btab[2 * BT_TABLE];
+  lds_btab_load(btab, btab_g, 2 * BT_TABLE);
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t idx = gid < n ? gid : n - 1;
   const int lane = threadIdx.x & 63;
   uint4* wave_tab = scratch + (size_t)(gid >> 6) * (WAVE_QUADS * 64);
-  uint2* wave_dig = reinterpret_cast<uint2*>(wave_tab + SCR_DIG * 64);
+  uint4* wave_dig = wave_tab + SCR_DIG * 64;
 
   bool okA, okR, s_ok;
   {
@@ -273,10 +288,6 @@ __global__ void __launch_bounds__(256, MINW)
     load8(mw, msg + 32 * (size_t)idx);
 
     s_ok = sc_is_canonical(sw);
-    p3 A, R;
-    decompress_x2(A, okA, aw, R, okR, rw);
-    scr_put_xyt(wave_tab, SCR_R, lane, R);
-
     // k = SHA-512(R || A || M) mod l over the original encodings
     uint32_t kin[24], h[16], k[8];
 #pragma unroll
@@ -287,48 +298,50 @@ __global__ void __launch_bounds__(256, MINW)
     }
     sha512_short(h, kin, 96);
     sc_reduce512(k, h);
-    uint32_t kd[8], sd[8];
-    sc_recode16(kd, k);
-    sc_recode256(sd, sw);
+    uint32_t c[4], d[8], e[8], zero[8];
+    bool c_neg;
+    sc_halfsize(c, c_neg, d, k);
 #pragma unroll
-    for (int j = 0; j < 8; j++) wave_dig[j * 64 + lane] = make_uint2(kd[j], sd[j]);
+    for (int i = 0; i < 8; i++) zero[i] = 0;
+#pragma unroll
+    for (int i = 4; i < 8; i++) d[i] = 0;
+    sc_muladd(e, d, sw, zero);
+    uint32_t cd[4], dd[4], ed[8];
+    sc_recode16_128(cd, c);
+    sc_recode16_128(dd, d);
+    sc_recode256(ed, e);
+#pragma unroll
+    for (int g = 0; g < 4; g++) wave_dig[g * 64 + lane] = make_uint4(cd[g], dd[g], ed[g], ed[4 + g]);
 
-    // variable-base table [j](-A), j = 0..8
-    p3 nA, cur;
-    p3_neg(nA, A);
-    cached c1, c;
-    cached_identity(c);
-    atab_put(wave_tab, 0, lane, c);
-    p3_to_cached(c1, nA);
-    atab_put(wave_tab, 1, lane, c1);
-    cur = nA;
-    for (int j = 2; j <= 8; j++) {
-      p1p1 t;
-      p3_add_cached(t, cur, c1);
-      p1p1_to_p3(cur, t);
-      p3_to_cached(c, cur);
-      atab_put(wave_tab, j, lane, c);
-    }
+    p3 A, R, nR;
+    decompress_x2(A, okA, aw, R, okR, rw);
+    // -[c]A = [|c|](-A) for c >= 0, [|c|]A for c < 0
+    if (!c_neg) p3_neg(A, A);
+    vtab_build(wave_tab + SCR_AT * 64, lane, A);
+    p3_neg(nR, R);
+    vtab_build(wave_tab + SCR_RT * 64, lane, nR);
   }
 
-  // Straus: R' = [k](-A) + [s]B, 4-bit windows for k, 8-bit windows for s
+  const uint4* tabA = wave_tab + SCR_AT * 64;
+  const uint4* tabR = wave_tab + SCR_RT * 64;
   p2 P;
   p3 P3;
   p1p1 Q;
-  cached ca;
+  cached ca, cr;
   precomp pb;
-  // 8 groups of 8 windows; a group's digit word (k nibbles, s bytes) is loaded one
-  // group ahead, so no window waits on memory except for its table gather, which
-  // is issued before the doublings and consumed after them.
-  uint2 dw_next = wave_dig[7 * 64 + lane];
-  for (int g = 7; g >= 0; g--) {
-    const uint2 dw = dw_next;
+  // 4 groups of 8 windows; a group's digit quad is loaded one group ahead, each
+  // window's two table gathers are issued before its doublings and consumed after.
+  uint4 dw_next = wave_dig[3 * 64 + lane];
+  for (int g = 3; g >= 0; g--) {
+    const uint4 dw = dw_next;
     if (g > 0) dw_next = wave_dig[(g - 1) * 64 + lane];
     for (int j = 7; j >= 0; j--) {
       const int w = 8 * g + j;
-      const int dk = ((int)(dw.x << (28 - 4 * j))) >> 28;
-      atab_load(ca, wave_tab, lane, dk);
-      if (w != 63) {
+      const int dc = ((int)(dw.x << (28 - 4 * j))) >> 28;
+      const int dd = ((int)(dw.y << (28 - 4 * j))) >> 28;
+      atab_load(ca, tabA, lane, dc);
+      atab_load(cr, tabR, lane, dd);
+      if (w != 31) {
         for (int i = 0; i < 3; i++) {
           p2_dbl(Q, P);
           p1p1_to_p2(P, Q);
@@ -338,27 +351,21 @@ __global__ void __launch_bounds__(256, MINW)
       } else {
         p3_identity(P3);
       }
-      cached_cneg(ca, dk < 0);
+      cached_cneg(ca, dc < 0);
       p3_add_cached(Q, P3, ca);
-      if ((j & 1) == 0) {
-        p1p1_to_p3(P3, Q);
-        const int ds = ((int)(dw.y << (24 - 8 * (j >> 1)))) >> 24;
-        btab_get(pb, btab, ds);
-        p3_add_precomp(Q, P3, pb);
-      }
+      p1p1_to_p3(P3, Q);
+      cached_cneg(cr, dd < 0);
+      p3_add_cached(Q, P3, cr);
+      p1p1_to_p3(P3, Q);
+      // even window 2i: digit i of e (B); odd window 2i+1: digit 16+i (2^124 B)
+      const uint32_t ew = (j & 1) ? dw.w : dw.z;
+      const int de = ((int)(ew << (24 - 8 * (j >> 1)))) >> 24;
+      btab_get(pb, btab + (j & 1) * BT_TABLE, de);
+      p3_add_precomp(Q, P3, pb);
       p1p1_to_p2(P, Q);
     }
   }
-  // cofactored check: [8](R - R') == identity
-  p3 R, Rp;
-  p1p1_to_p3(Rp, Q);
-  scr_get_xyt(R, wave_tab, SCR_R, lane);
-  p3 nRp;
-  p3_neg(nRp, Rp);
-  cached cR;
-  p3_to_cached(cR, nRp);
-  p3_add_cached(Q, R, cR);
-  p1p1_to_p2(P, Q);
+  // cofactored check: [8]([e]B - [c]A - [d]R) == identity
 #pragma unroll 1
   for (int i = 0; i < 3; i++) {
     p2_dbl(Q, P);
@@ -375,8 +382,8 @@ __global__ void __launch_bounds__(256, MINW)
 __global__ void __launch_bounds__(256, 2)
     k_sign(const uint8_t* __restrict__ seed, const uint8_t* __restrict__ msg, uint32_t n,
            const uint4* __restrict__ btab_g, uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sig_out) {
-  __shared__ uint4 btab[BT_ENTRIES * BT_QUADS];
-  lds_btab_load(btab, btab_g);
+  __shared__ uint4 btab[BT_TABLE];
+  lds_btab_load(btab, btab_g, BT_TABLE);
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t idx = gid < n ? gid : n - 1;
   uint32_t sw[8], mw[8], h[16];
@@ -509,8 +516,8 @@ __global__ void __launch_bounds__(256) k_block_hash(const uint8_t* __restrict__ 
 // Field / scalar primitives on 16-word lane inputs (parity tests).
 __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restrict__ in, uint32_t n,
                                                  const uint4* __restrict__ btab_g, uint32_t* __restrict__ out) {
-  __shared__ uint4 btab[BT_ENTRIES * BT_QUADS];
-  lds_btab_load(btab, btab_g);
+  __shared__ uint4 btab[2 * BT_TABLE];
+  lds_btab_load(btab, btab_g, 2 * BT_TABLE);
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n) return;
   uint32_t x[16], y[16];
@@ -567,6 +574,35 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
       for (int i = 8; i < 16; i++) out[16 * (size_t)gid + i] = 0;
       return;
     }
+    case 13: {  // sc_halfsize of k < l: c words 0..3, c_neg word 4, d words 8..11
+      uint32_t c[4], d[4];
+      bool neg;
+      sc_halfsize(c, neg, d, x);
+#pragma unroll
+      for (int i = 0; i < 16; i++) y[i] = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        y[i] = c[i];
+        y[8 + i] = d[i];
+      }
+      y[4] = neg;
+#pragma unroll
+      for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
+      return;
+    }
+    case 14: {  // [a](2^124 B) encoding via the second fixed-base table
+      uint32_t sd[8];
+      sc_recode256(sd, x);
+      p3 P;
+      basemul(P, sd, btab + BT_TABLE);
+      uint32_t enc[8];
+      p3_compress(enc, P);
+#pragma unroll
+      for (int i = 0; i < 8; i++) out[16 * (size_t)gid + i] = enc[i];
+#pragma unroll
+      for (int i = 8; i < 16; i++) out[16 * (size_t)gid + i] = 0;
+      return;
+    }
     case 12: {  // fe_canon of raw 255-bit input
       fe_from_words(r, x);
       fe_canon(r, r);
@@ -600,10 +636,10 @@ static int verify_variant() {
   }();
   return v;
 }
-size_t btable_bytes() { return mv::BT_ENTRIES * mv::BT_QUADS * sizeof(uint4); }
+size_t btable_bytes() { return 2 * mv::BT_TABLE * sizeof(uint4); }
 
 hipError_t launch_btable_init(void* d_btab, hipStream_t s) {
-  hipLaunchKernelGGL(mv::k_btable_init, dim3(1), dim3(256), 0, s, (uint4*)d_btab);
+  hipLaunchKernelGGL(mv::k_btable_init, dim3(2), dim3(256), 0, s, (uint4*)d_btab);
   return hipGetLastError();
 }
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,

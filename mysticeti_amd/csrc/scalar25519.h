@@ -138,6 +138,149 @@ MV_DEV void sc_recode256(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-16 recoding of a value < 2^127 (4 words): 32 digits in [-8, 7]. The
+// top nibble is at most 7 and absorbs the last carry (d + carry <= 7 needs x < 2^127
+// with top nibble <= 6, which the half-size scalars below satisfy).
+MV_DEV void sc_recode16_128(uint32_t out[4], const uint32_t x[4]) {
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint32_t d = ((x[w] >> (4 * j)) & 15u) + carry;
+      carry = (d + 8) >> 4;
+      d = (d - (carry << 4)) & 15u;
+      o |= d << (4 * j);
+    }
+    out[w] = o;
+  }
+}
+
+// bit length of an 8-word value (0 for 0)
+MV_DEV int len256(const uint32_t x[8]) {
+  int L = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) L = x[i] ? 32 * i + 32 - (int)__clz(x[i]) : L;
+  return L;
+}
+// r = x << s mod 2^(32 NW), 0 <= s < 256 (per-lane s: funnel shifts, then a
+// 3-stage word-select network instead of dynamic register indexing)
+template <int NW>
+MV_DEV void shl_var(uint32_t (&r)[NW], const uint32_t (&x)[NW], int s) {
+  const int bsh = s & 31, ws = s >> 5;
+#pragma unroll
+  for (int i = NW - 1; i >= 0; i--) {
+    const uint64_t pair = ((uint64_t)x[i] << 32) | (i ? x[i - 1] : 0u);
+    r[i] = (uint32_t)(pair >> (32 - bsh));
+  }
+#pragma unroll
+  for (int k = 1; k <= 4; k <<= 1) {
+    const bool on = (ws & k) != 0;
+#pragma unroll
+    for (int i = NW - 1; i >= 0; i--) r[i] = on ? (i >= k ? r[i - k] : 0u) : r[i];
+  }
+}
+
+// Half-size scalars for verification (T. Pornin, "Optimized lattice basis reduction
+// in dimension 2, and fast Schnorr and EdDSA signature verification", 2020): find
+// c, d with c = d*k (mod l), |c| < 2^126, 0 < d < 2^127, so that
+//   [8]([s]B - [k]A - R) = O  <=>  [8]([d*s mod l]B - [c]A - [d]R) = O
+// (d is invertible mod l; c - d*k is a multiple of l, which [8] kills on A's
+// torsion part). The reduction is the extended-Euclid remainder sequence of (l, k),
+// quotients applied as shift-subtract steps, stopped at the first remainder below
+// 2^126 (Thue): its cofactor t satisfies |t| <= l / 2^126 < 2^127. t is tracked mod
+// 2^128 (every intermediate cofactor is below 2^127 in magnitude). Each step drops
+// len(a) + len(b) by at least one, so the loop ends within ~380 steps; for random k it
+// takes ~110 (64-lane max ~125).
+// Output: c as magnitude (4 words) + sign, d (4 words).
+MV_DEV void sc_halfsize(uint32_t c[4], bool& c_neg, uint32_t d[4], const uint32_t k[8]) {
+  uint32_t a[8], b[8], ta[4], tb[4];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a[i] = SC_L[i];
+    b[i] = k[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    ta[i] = 0;
+    tb[i] = i == 0;
+  }
+  int la = 253, lb = len256(b);
+  bool done = lb <= 126;
+  if (done) {  // k itself is short: (c, d) = (k, 1)
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = b[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) ta[i] = tb[i];
+  }
+  while (!done) {
+    const int s = la - lb;
+    uint32_t bs[8], x[8];
+    shl_var<8>(bs, b, s);
+    uint64_t bm;
+    x[0] = sub_co(a[0], bs[0], bm);
+#pragma unroll
+    for (int i = 1; i < 8; i++) x[i] = subb_co(a[i], bs[i], bm);
+    const uint32_t over = carry_bit(bm);  // b << s > a: use b << (s - 1), s >= 1
+    if (over) {
+      uint64_t cm;
+      uint32_t h[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) h[i] = (bs[i] >> 1) | (i < 7 ? bs[i + 1] << 31 : 0u);
+      x[0] = add_co(x[0], h[0], cm);
+#pragma unroll
+      for (int i = 1; i < 8; i++) x[i] = addc_co(x[i], h[i], cm);
+    }
+    uint32_t ts[4];
+    shl_var<4>(ts, tb, s - (int)over);
+    uint64_t tm;
+    ta[0] = sub_co(ta[0], ts[0], tm);
+#pragma unroll
+    for (int i = 1; i < 4; i++) ta[i] = subb_co(ta[i], ts[i], tm);
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = x[i];
+    la = len256(a);
+    if (la <= 126) {
+      done = true;
+    } else {
+      uint64_t cm;
+      (void)sub_co(a[0], b[0], cm);
+#pragma unroll
+      for (int i = 1; i < 8; i++) (void)subb_co(a[i], b[i], cm);
+      if (carry_bit(cm)) {  // a < b: swap roles
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const uint32_t t = a[i];
+          a[i] = b[i];
+          b[i] = t;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t t = ta[i];
+          ta[i] = tb[i];
+          tb[i] = t;
+        }
+        const int t = la;
+        la = lb;
+        lb = t;
+      }
+    }
+  }
+  // d = ta (signed); make d positive, moving the sign to c = a
+  c_neg = (int32_t)ta[3] < 0;
+  uint64_t nm;
+  uint32_t nd[4];
+  nd[0] = sub_co(0u, ta[0], nm);
+#pragma unroll
+  for (int i = 1; i < 4; i++) nd[i] = subb_co(0u, ta[i], nm);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    d[i] = c_neg ? nd[i] : ta[i];
+    c[i] = a[i];
+  }
+}
+
 // uniform-index word pick without dynamic register indexing
 MV_DEV uint32_t pick8(const uint32_t a[8], int idx) {
   uint32_t r = a[0];

@@ -125,3 +125,49 @@ def test_blake2b_kats(engine, golden):
     out = engine.blake2b256(items)
     for n, o in zip(lens, out):
         assert o.hex() == g["blake2b256"][str(n)], n
+
+
+def _halfsize_model(k):
+    """Extended-Euclid remainder sequence of (l, k) stopped below 2^126, quotients as
+    shift-subtract steps (the algorithm of scalar25519.h sc_halfsize)."""
+    a, ta, b, tb = Z.L, 0, k, 1
+    if b < 2**126:
+        return b, 1
+    while True:
+        s = a.bit_length() - b.bit_length()
+        if (b << s) > a:
+            s -= 1
+        a -= b << s
+        ta -= tb << s
+        if a < 2**126:
+            return a, ta
+        if a < b:
+            a, ta, b, tb = b, tb, a, ta
+
+
+def test_halfsize_scalars(engine):
+    r = random.Random(9)
+    T = 2**126
+    ks = [0, 1, 2, T - 1, T, T + 1, 2**200 + 5, 2**252, Z.L - 1, Z.L - 2, (Z.L - 1) // 2, (Z.L + 1) // 2,
+          2**252 - 1, 3 * T, Z.L // 3, Z.L // 5 + 7] + [r.randrange(Z.L) for _ in range(3000)]
+    w = np.array([words(k) + [0] * 8 for k in ks], dtype=np.uint32)
+    out = engine.selftest(13, w)
+    for k, o in zip(ks, out):
+        c, neg, d = val(o[:4]), int(o[4]), val(o[8:12])
+        mc, md = _halfsize_model(k)
+        if md < 0:
+            mc, md = -mc, -md
+        assert (-c if neg else c) == mc and d == md, k
+        # the property the verify equation relies on
+        assert ((-c if neg else c) - d * k) % Z.L == 0 and c < T and 0 < d < 2**127, k
+        assert (d >> 124) <= 6  # the radix-16 recoding's top digit stays in [-8, 7]
+
+
+def test_second_fixed_base_table(engine):
+    # [a](2^124 B) from the second LDS table == [a * 2^124 mod l]B
+    r = random.Random(10)
+    ks = [0, 1, 2, 128, 129, Z.L - 1] + [r.randrange(Z.L) for _ in range(60)]
+    w = np.array([words(k) + [0] * 8 for k in ks], dtype=np.uint32)
+    out = engine.selftest(14, w)
+    for k, o in zip(ks, out):
+        assert o[:8].astype("<u4").tobytes() == Z.compress(Z.scalarmult(Z.B_POINT, k * 2**124 % Z.L)), k
