@@ -27,6 +27,21 @@
 
 namespace mv {
 
+// Phase clocks for tools/phase_clock.hip (compiled only there): lane 0 of every wave
+// records clock64() deltas at the verify kernel's phase boundaries.
+#ifdef MV_PHASE_CLOCKS
+__device__ unsigned long long* g_phase_buf;
+#define MV_PHASE(i)                                                                   \
+  do {                                                                                \
+    if ((threadIdx.x & 63) == 0 && g_phase_buf)                                       \
+      g_phase_buf[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (i)] = clock64(); \
+  } while (0)
+#else
+#define MV_PHASE(i) \
+  do {              \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- tables
 // Table entries are stored in the field's limb form (9 x 29-bit words per element):
 // B entries (precomp, 27 words + 1 pad = 7 uint4) in LDS, the per-lane variable-base
@@ -273,10 +288,15 @@ __global__ void __launch_bounds__(256, MINW)
              uint4* __restrict__ scratch, uint8_t* __restrict__ status) {
   __shared__ uint4 btab[2 * BT_TABLE];
   lds_btab_load(btab, btab_g, 2 * BT_TABLE);
+  MV_PHASE(0);
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t idx = gid < n ? gid : n - 1;
   const int lane = threadIdx.x & 63;
+#ifdef MV_EXP_SHARED_TAB  // timing experiment only (tools/phase_clock.hip): one table region for all waves
+  uint4* wave_tab = scratch + (size_t)((gid >> 6) & 7) * (WAVE_QUADS * 64);
+#else
   uint4* wave_tab = scratch + (size_t)(gid >> 6) * (WAVE_QUADS * 64);
+#endif
   uint4* wave_dig = wave_tab + SCR_DIG * 64;
 
   bool okA, okR, s_ok;
@@ -298,9 +318,16 @@ __global__ void __launch_bounds__(256, MINW)
     }
     sha512_short(h, kin, 96);
     sc_reduce512(k, h);
+    MV_PHASE(1);
     uint32_t c[4], d[8], e[8], zero[8];
     bool c_neg;
+#ifdef MV_EXP_NO_HALFSIZE  // timing experiment only: wrong (c, d), same instruction stream after
+    for (int i = 0; i < 4; i++) { c[i] = k[i] >> 2; d[i] = k[4 + i] >> 2; }
+    c_neg = k[0] & 1;
+#else
     sc_halfsize(c, c_neg, d, k);
+#endif
+    MV_PHASE(2);
 #pragma unroll
     for (int i = 0; i < 8; i++) zero[i] = 0;
 #pragma unroll
@@ -312,15 +339,18 @@ __global__ void __launch_bounds__(256, MINW)
     sc_recode256(ed, e);
 #pragma unroll
     for (int g = 0; g < 4; g++) wave_dig[g * 64 + lane] = make_uint4(cd[g], dd[g], ed[g], ed[4 + g]);
+    MV_PHASE(3);
 
     p3 A, R, nR;
     decompress_x2(A, okA, aw, R, okR, rw);
+    MV_PHASE(4);
     // -[c]A = [|c|](-A) for c >= 0, [|c|]A for c < 0
     if (!c_neg) p3_neg(A, A);
     vtab_build(wave_tab + SCR_AT * 64, lane, A);
     p3_neg(nR, R);
     vtab_build(wave_tab + SCR_RT * 64, lane, nR);
   }
+  MV_PHASE(5);
 
   const uint4* tabA = wave_tab + SCR_AT * 64;
   const uint4* tabR = wave_tab + SCR_RT * 64;
@@ -365,6 +395,7 @@ __global__ void __launch_bounds__(256, MINW)
       p1p1_to_p2(P, Q);
     }
   }
+  MV_PHASE(6);
   // cofactored check: [8]([e]B - [c]A - [d]R) == identity
 #pragma unroll 1
   for (int i = 0; i < 3; i++) {
@@ -376,6 +407,7 @@ __global__ void __launch_bounds__(256, MINW)
     uint8_t st = !okA ? 2 : ((s_ok && okR && ident) ? 0 : 1);
     status[gid] = st;
   }
+  MV_PHASE(7);
 }
 
 // RFC 8032: (pk, R || S) from (seed, 32-byte msg)
@@ -632,7 +664,7 @@ size_t verify_scratch_bytes(uint32_t n) {
 static int verify_variant() {
   static int v = [] {
     const char* e = getenv("MV_VERIFY_OCC");
-    return (e && e[0] == '1') ? 1 : 2;
+    return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
   }();
   return v;
 }
@@ -647,6 +679,9 @@ hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* 
   if (n == 0) return hipSuccess;
   if (verify_variant() == 1)
     hipLaunchKernelGGL(mv::k_verify<1>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
+                       (const uint4*)btab, (uint4*)scratch, status);
+  else if (verify_variant() == 3)
+    hipLaunchKernelGGL(mv::k_verify<3>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)btab, (uint4*)scratch, status);
   else
     hipLaunchKernelGGL(mv::k_verify<2>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
