@@ -22,7 +22,8 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmysti_verify.so")
+# MV_LIB selects an experiment build (python -m mysticeti_amd.build --variant NAME -D...)
+LIB_PATH = os.environ.get("MV_LIB") or os.path.join(_HERE, "libmysti_verify.so")
 
 MV_OK = 0
 SIG_OK, SIG_INVALID, SIG_MALFORMED_KEY = 0, 1, 2

@@ -31,32 +31,39 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src: str, force: bool) -> str:
+def _compile(src: str, force: bool, obj_dir: str = OBJ, defines=()) -> str:
     s = os.path.join(CSRC, src)
-    o = os.path.join(OBJ, src + ".o")
+    o = os.path.join(obj_dir, src + ".o")
     deps = [s] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "mysti_verify.h")]
     if force or _newer(o, deps):
         lang = [] if src.endswith(".hip") else ["-x", "hip"]
-        cmd = [HIPCC] + COMMON + lang + ["-c", s, "-o", o]
+        cmd = [HIPCC] + COMMON + [f"-D{d}" for d in defines] + lang + ["-c", s, "-o", o]
         subprocess.run(cmd, check=True)
     return o
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(force: bool = False, verbose: bool = True, variant: str = "", defines=()) -> str:
+    """Builds the product library, or with `variant` an experiment build
+    (mysticeti_amd/_build/<variant>/libmysti_verify.so, compiled with -D`defines`; load it
+    with MV_LIB=<path>)."""
+    obj_dir = os.path.join(OBJ, variant) if variant else OBJ
+    lib = os.path.join(obj_dir, "libmysti_verify.so") if variant else LIB
+    os.makedirs(obj_dir, exist_ok=True)
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
-    if force or _newer(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+        objs = list(ex.map(lambda s: _compile(s, force, obj_dir, defines), SOURCES))
+    if force or _newer(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"]
         subprocess.run(cmd, check=True)
         if verbose:
-            print("built", LIB)
-    return LIB
+            print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
     a = ap.parse_args()
-    build(force=a.force)
+    build(force=a.force, variant=a.variant, defines=a.defines)
     sys.exit(0)

@@ -125,24 +125,33 @@ MV_DEV void btab_get(precomp& p, const uint4* sm, int digit) {
   precomp_cneg(p, digit < 0);
 }
 
-// Per-wave variable-base table scratch (wave_base = the table's first uint4):
-// [entry][quad][lane] of uint4, lanes contiguous so the table build writes 1 KiB per
-// wave-instruction and lookups touch <= 9 segments.
-MV_DEV void atab_put(uint4* wave_base, int e, int lane, const cached& c) {
-  uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
+// Per-wave variable-base table scratch. Lane-major: each lane owns 2 x 81 contiguous
+// uint4 ([table][entry][quad]), so one entry gather reads 144 contiguous bytes per lane
+// (2 cache lines) and the whole line is used; the wave-major alternative
+// ([table][entry][quad][lane], MV_TAB_WAVE_MAJOR) coalesces the build's stores but a
+// random-digit gather then touches ~5 partly used lines per 8 lanes per quad.
+#ifdef MV_TAB_WAVE_MAJOR
+constexpr int TAB_LANE_STRIDE = 1, TAB_QUAD_STRIDE = 64;
+#else
+constexpr int TAB_LANE_STRIDE = 2 * AT_TABLE, TAB_QUAD_STRIDE = 1;
+#endif
+constexpr int TAB_ENTRY_STRIDE = AT_QUADS * TAB_QUAD_STRIDE;
+constexpr int TAB_TABLE_STRIDE = AT_ENTRIES * TAB_ENTRY_STRIDE;  // A table -> R table
+MV_DEV void atab_put(uint4* tab, int e, const cached& c) {
+  uint4* p = tab + e * TAB_ENTRY_STRIDE;
   uint4 q[9];
   cached_to_quads(q, c);
 #pragma unroll
-  for (int i = 0; i < 9; i++) p[i * 64] = q[i];
+  for (int i = 0; i < 9; i++) p[i * TAB_QUAD_STRIDE] = q[i];
 }
 // raw entry load; the sign is applied at use time (cached_cneg) so the gather's
 // latency hides behind the window's doublings
-MV_DEV void atab_load(cached& c, const uint4* wave_base, int lane, int digit) {
+MV_DEV void atab_load(cached& c, const uint4* tab, int digit) {
   int e = digit < 0 ? -digit : digit;
-  const uint4* p = wave_base + (e * AT_QUADS) * 64 + lane;
+  const uint4* p = tab + e * TAB_ENTRY_STRIDE;
   uint4 q[9];
 #pragma unroll
-  for (int i = 0; i < 9; i++) q[i] = p[i * 64];
+  for (int i = 0; i < 9; i++) q[i] = p[i * TAB_QUAD_STRIDE];
   quads_to_cached(c, q);
 }
 
@@ -248,28 +257,26 @@ __global__ void __launch_bounds__(256) k_btable_init(uint4* out) {
   for (int i = 0; i < 7; i++) o[i] = q[i];
 }
 
-// Per-wave scratch layout (uint4 units, each [..][lane]): the two variable-base
-// tables, then the recoded scalars, parked in HBM during the ladder instead of
-// holding 16 VGPRs.
-constexpr int SCR_AT = 0;                  // [0..8](-A) or [0..8](A), by the sign of c
-constexpr int SCR_RT = AT_TABLE;           // [0..8](-R)
-constexpr int SCR_DIG = 2 * AT_TABLE;      // 4 groups x uint4 (c, d, e lo, e hi)
-constexpr int WAVE_QUADS = SCR_DIG + 4;    // 166
+// Per-wave scratch layout (uint4 units): the two variable-base tables of the 64 lanes
+// ([0..8](-A) or [0..8](A) by the sign of c, then [0..8](-R)), then the recoded
+// scalars [group][lane], parked in HBM during the ladder instead of holding 16 VGPRs.
+constexpr int SCR_DIG = 2 * AT_TABLE * 64;  // 4 groups x uint4 (c, d, e lo, e hi)
+constexpr int WAVE_QUADS = 2 * AT_TABLE + 4;  // 166 per lane
 
 // [0..8]P as cached points into a per-wave table
-MV_DEV void vtab_build(uint4* tab, int lane, const p3& P) {
+MV_DEV void vtab_build(uint4* tab, const p3& P) {
   cached c1, c;
   cached_identity(c);
-  atab_put(tab, 0, lane, c);
+  atab_put(tab, 0, c);
   p3_to_cached(c1, P);
-  atab_put(tab, 1, lane, c1);
+  atab_put(tab, 1, c1);
   p3 cur = P;
   for (int j = 2; j <= 8; j++) {
     p1p1 t;
     p3_add_cached(t, cur, c1);
     p1p1_to_p3(cur, t);
     p3_to_cached(c, cur);
-    atab_put(tab, j, lane, c);
+    atab_put(tab, j, c);
   }
 }
 
@@ -297,7 +304,9 @@ __global__ void __launch_bounds__(256, MINW)
 #else
   uint4* wave_tab = scratch + (size_t)(gid >> 6) * (WAVE_QUADS * 64);
 #endif
-  uint4* wave_dig = wave_tab + SCR_DIG * 64;
+  uint4* wave_dig = wave_tab + SCR_DIG;
+  uint4* tabA = wave_tab + lane * TAB_LANE_STRIDE;
+  uint4* tabR = tabA + TAB_TABLE_STRIDE;
 
   bool okA, okR, s_ok;
   {
@@ -346,14 +355,12 @@ __global__ void __launch_bounds__(256, MINW)
     MV_PHASE(4);
     // -[c]A = [|c|](-A) for c >= 0, [|c|]A for c < 0
     if (!c_neg) p3_neg(A, A);
-    vtab_build(wave_tab + SCR_AT * 64, lane, A);
+    vtab_build(tabA, A);
     p3_neg(nR, R);
-    vtab_build(wave_tab + SCR_RT * 64, lane, nR);
+    vtab_build(tabR, nR);
   }
   MV_PHASE(5);
 
-  const uint4* tabA = wave_tab + SCR_AT * 64;
-  const uint4* tabR = wave_tab + SCR_RT * 64;
   p2 P;
   p3 P3;
   p1p1 Q;
@@ -369,8 +376,8 @@ __global__ void __launch_bounds__(256, MINW)
       const int w = 8 * g + j;
       const int dc = ((int)(dw.x << (28 - 4 * j))) >> 28;
       const int dd = ((int)(dw.y << (28 - 4 * j))) >> 28;
-      atab_load(ca, tabA, lane, dc);
-      atab_load(cr, tabR, lane, dd);
+      atab_load(ca, tabA, dc);
+      atab_load(cr, tabR, dd);
       if (w != 31) {
         for (int i = 0; i < 3; i++) {
           p2_dbl(Q, P);
