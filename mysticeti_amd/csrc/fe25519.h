@@ -78,22 +78,22 @@ MV_DEV void fe_neg(fe& r, const fe& a) {
 }
 
 // Column-scanning reduction, shared by mul and sq. col(k) returns the 64-bit sum
-// of column k (< 2^63.3). High columns 9..16 are normalised as they are produced
-// (carry chain h) and folded at once with 2^261 = 1216, so only the 9 low
-// column sums are live at a time.
+// of column k (< 2^63.3). A high column k = 9..16 is folded as it is produced,
+// without a carry chain: its 32-bit halves L, H go to the low columns with
+// 2^261 = 1216 and 2^(261+32) = 2^(29*10) * 8 = 1216 * 8 (mod p) as one
+// v_mad_u64_u32 each (L * 1216 -> column k-9, H * 9728 -> column k-8; the low
+// sums stay < 2^63.3 + 2^42.3 + 2^44.6). Only the 9 low sums are live at a time.
 template <class Col>
 MV_DEV void fe_reduce_scan(fe& r, Col col) {
   uint64_t lo[9];
 #pragma unroll
   for (int k = 0; k < 9; k++) lo[k] = col(k);
-  uint64_t h = 0;
 #pragma unroll
   for (int k = 9; k < 17; k++) {
-    h += col(k);  // < 2^63.3 + 2^35
-    lo[k - 9] += (uint64_t)((uint32_t)h & M29) * R261;
-    h >>= 29;
+    const uint64_t c = col(k);
+    lo[k - 9] += (uint64_t)(uint32_t)c * R261;
+    lo[k - 8] += (uint64_t)(uint32_t)(c >> 32) * (8 * R261);
   }
-  lo[8] += (uint64_t)(uint32_t)h * R261;  // h < 2^32: carry out of column 16
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     r.v[k] = (uint32_t)lo[k] & M29;
