@@ -16,6 +16,10 @@
  *                          NetworkSyncer::process_blocks (net_sync.rs:331-375) over
  *                          StatementBlock::verify (types.rs:315-376), on Data<StatementBlock>
  *                          bincode bytes (data.rs:43-52)
+ *   mv_dev_ed25519_verify_batch
+ *                          ed25519_consensus::batch::Verifier (the ZIP-215 batch rule, which agrees
+ *                          with VerificationKey::verify) over a whole batch, with an exact
+ *                          per-signature fallback: per-item verdicts equal mv_ed25519_verify's
  *   mv_dev_*               the same computations on device-resident buffers (HBM in, HBM out)
  *
  * Conventions
@@ -65,10 +69,17 @@ typedef int32_t mv_status;
 #define MV_BLOCK_VOTE_RANGE 9              /* types.rs:363-370, 440-460 */
 #define MV_BLOCK_THRESHOLD_CLOCK 10        /* types.rs:371-374, threshold_clock.rs:12-35 */
 
+/* mv_config.flags */
+#define MV_FLAG_NO_BATCH 1u /* host-buffer verify: never use the batch (random linear combination) path */
+
+/* Host-buffer verify calls of at least this many signatures per device take the batch path
+ * (one combined equation + exact fallback); smaller ones verify every signature alone. */
+#define MV_BATCH_MIN 4096u
+
 typedef struct mv_config {
   uint32_t device_mask; /* bit i = use HIP device i; 0 = device 0 only */
   uint32_t max_batch;   /* items per device launch chunk; 0 = default (1<<20) */
-  uint32_t flags;       /* reserved, 0 */
+  uint32_t flags;       /* MV_FLAG_* */
 } mv_config;
 
 mv_status mv_create(const mv_config* cfg, mv_ctx** out);
@@ -113,10 +124,23 @@ int64_t mv_block_preimage(const uint8_t* bincode, uint64_t len, uint8_t* out, ui
  * library's stream for that device). They enqueue work and return without synchronising. */
 mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
                                 const uint8_t* d_pk, uint32_t n, uint8_t* d_status, void* stream);
+/* Batch path on device buffers: verdicts identical to mv_dev_ed25519_verify. The combined
+ * equation [8](-[sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i) == O with secret random
+ * 128-bit z_i (BLAKE2b PRF keyed per context and call) is checked first; if it fails, every
+ * signature is re-verified individually on the same stream, so each verdict is exact (an
+ * invalid signature survives a passing combination with probability <= 2^-128).
+ * `d_pk` rows are indexed by item, or by `d_key_idx` (device array) when it is non-NULL.
+ * Enqueues only; `d_batch_ok` (optional, device, 4 bytes) receives 1 if the combination held. */
+mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
+                                      const uint8_t* d_pk, const uint32_t* d_key_idx, uint32_t n,
+                                      uint8_t* d_status, uint32_t* d_batch_ok, void* stream);
 mv_status mv_dev_ed25519_sign(mv_ctx* ctx, int device, const uint8_t* d_seed, const uint8_t* d_msg, uint32_t n,
                               uint8_t* d_pk, uint8_t* d_sig, void* stream);
 
 /* ---- diagnostics (used by the test-suite) ---- */
+/* Host-buffer batch-path counters since mv_create: batches tried, batches whose combined
+ * equation failed (and were re-verified signature by signature). */
+mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks);
 /* Runs field/scalar primitive `op` on n lane inputs (16 words each) -> 16 words each (host buffers). */
 mv_status mv_selftest(mv_ctx* ctx, int op, const uint32_t* in, uint32_t n, uint32_t* out);
 

@@ -38,8 +38,10 @@ BLOCK_STATUS = [
 EXPORTS = [
     "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
-    "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage",
+    "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
 ]
+FLAG_NO_BATCH = 1
+BATCH_MIN = 4096
 
 
 class MvError(RuntimeError):
@@ -74,6 +76,8 @@ def load_library(path: str = LIB_PATH):
     lib.mv_ed25519_sign.argtypes = [vp, vp, vp, u32, vp, vp]
     lib.mv_verify_blocks.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
     lib.mv_dev_ed25519_verify.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
+    lib.mv_dev_ed25519_verify_batch.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, u32, vp, vp, vp]
+    lib.mv_batch_stats.argtypes = [vp, vp, vp]
     lib.mv_dev_ed25519_sign.argtypes = [vp, ctypes.c_int, vp, vp, u32, vp, vp, vp]
     lib.mv_selftest.argtypes = [vp, ctypes.c_int, vp, u32, vp]
     lib.mv_block_preimage.argtypes = [vp, u64, vp, u64]
@@ -96,12 +100,13 @@ def _u8(a, shape_tail: int) -> np.ndarray:
 class Engine:
     """One mv_ctx: the devices it shards over, their streams and buffers."""
 
-    def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0):
+    def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0, batch: bool = True):
+        """batch=False sets MV_FLAG_NO_BATCH: host-buffer verifies check every signature alone."""
         self.lib = load_library()
         mask = 0
         for d in devices:
             mask |= 1 << int(d)
-        cfg = _Config(mask, max_batch, 0)
+        cfg = _Config(mask, max_batch, 0 if batch else FLAG_NO_BATCH)
         h = ctypes.c_void_p()
         rc = self.lib.mv_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != MV_OK:
@@ -201,6 +206,23 @@ class Engine:
                                                    n, ctypes.c_void_p(d_status.data_ptr()),
                                                    ctypes.c_void_p(stream_handle or None)),
                     "mv_dev_ed25519_verify")
+
+    def dev_verify_batch(self, device: int, d_msg, d_sig, d_pk, d_status, d_batch_ok=None, stream_handle: int = 0,
+                         d_key_idx=None):
+        """Batch path (one combined equation, exact fallback) on device tensors; enqueue only."""
+        n = d_msg.shape[0]
+        vp = ctypes.c_void_p
+        self._check(self.lib.mv_dev_ed25519_verify_batch(
+            self.ctx, device, vp(d_msg.data_ptr()), vp(d_sig.data_ptr()), vp(d_pk.data_ptr()),
+            vp(d_key_idx.data_ptr()) if d_key_idx is not None else None, n, vp(d_status.data_ptr()),
+            vp(d_batch_ok.data_ptr()) if d_batch_ok is not None else None, vp(stream_handle or None)),
+            "mv_dev_ed25519_verify_batch")
+
+    def batch_stats(self) -> Tuple[int, int]:
+        """(batches tried, batches that fell back to per-signature verification) on the host path."""
+        b, f = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.mv_batch_stats(self.ctx, ctypes.byref(b), ctypes.byref(f)), "mv_batch_stats")
+        return b.value, f.value
 
     def dev_sign(self, device: int, d_seed, d_msg, d_pk, d_sig, stream_handle: int = 0):
         n = d_seed.shape[0]

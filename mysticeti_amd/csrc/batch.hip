@@ -1,0 +1,538 @@
+// Batch ed25519 verification on gfx950: one random linear combination of the whole
+// batch, checked as a single multi-scalar multiplication (bucket method), with an
+// exact per-signature fallback on the device when the combined equation fails.
+//
+// Semantics: ed25519-consensus 2.1.0 `batch::Verifier` (the ZIP-215 batch rule that
+// is designed to agree with the single `VerificationKey::verify` called at
+// mysticeti-core/src/crypto.rs:188): for signatures (A_i, R_i, s_i) with challenges
+// k_i and independent uniformly random 128-bit z_i,
+//     [8]( -[sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i ) == O.
+// Every individually valid signature satisfies [8]([s_i]B - [k_i]A_i - R_i) = O, so a
+// batch of valid signatures always passes; a batch holding an invalid one passes with
+// probability <= 2^-128 over the z_i. Per-signature preconditions (s < l, A and R
+// decode) are decided exactly in k_bv_prep and excluded from the combination. When
+// the combination fails, k_verify (kernels.hip) re-verifies every signature of the
+// batch individually (it reads the batch flag and exits at once when it passed), so
+// every verdict is the single-verify verdict.
+//
+// Pipeline (one batch of n signatures, all on one stream):
+//   k_bv_prep     lane per signature: SHA-512 challenge, ZIP-215 decode of A and R,
+//                 z_i = BLAKE2b(secret || call || i), scalars z_i and z_i k_i mod l,
+//                 affine points (y+x, y-x, 2dxy) to HBM, bucket histogram, sum z_i s_i
+//   k_scan_*      exclusive scan of the histogram -> bucket offsets
+//   k_bv_scatter  lane per signature: (point, sign) entries into their buckets
+//   k_bv_bucket   lane per 4-bucket segment of a window: bucket sums and the
+//                 segment's running sums (V = sum (b - b0) B_b, T = sum B_b)
+//   k_bv_reduce   tree over segments (fan-in 8) of the pairs (V, T) per window
+//   k_bv_final    Horner over the 16 window sums, -[sum z s]B, [8], identity test
+// Windows: signed radix 2^16, |digit| <= 2^15; R scalars use windows 0..8 (8 + carry),
+// A scalars (< l < 2^253) windows 0..15.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fe25519.h"
+#include "ge25519.h"
+#include "hash_dev.h"
+#include "kernels.h"
+#include "scalar25519.h"
+#include "tables.h"
+
+namespace mv {
+
+constexpr int BV_C = 16;                    // window bits
+constexpr int BV_NB = 1 << (BV_C - 1);      // bucket magnitudes 1..2^15 per window
+constexpr int BV_NW = 16;                   // windows
+constexpr int BV_NWR = 9;                   // windows of the 128-bit R scalars
+constexpr int BV_NK = BV_NW * BV_NB;        // bucket keys, key = w * NB + |d| - 1
+constexpr int BV_G = 4;                     // buckets per segment lane
+constexpr int BV_SEGW = BV_NB / BV_G;       // segments per window
+constexpr int BV_NSEG = BV_NW * BV_SEGW;
+constexpr int BV_FAN = 8;                   // reduction fan-in
+constexpr int PT_QUADS = 7;                 // precomp point, 27 words + pad
+constexpr int P3_QUADS = 9;
+constexpr int SC_QUADS = 3;                 // z (4 words), z*k mod l (8 words)
+constexpr int BSUM_WORDS = 12;              // z * s < 2^381
+
+// signed radix-2^16 digit w of a little-endian scalar, running carry in/out;
+// digit in [-2^15, 2^15 - 1] (v = 16 bits + carry <= 2^16)
+MV_DEV int bv_digit(uint32_t word, int half, uint32_t& carry) {
+  const uint32_t v = (half ? (word >> 16) : (word & 0xffffu)) + carry;
+  carry = v >= (1u << 15) ? 1u : 0u;
+  return (int)v - (int)(carry << 16);
+}
+
+// Calls fn(window, digit) for every nonzero digit of (z, zk).
+template <class Fn>
+MV_DEV void bv_for_digits(const uint32_t z[4], const uint32_t zk[8], Fn fn) {
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    const int d = bv_digit(z[w >> 1], w & 1, carry);
+    if (d) fn(w, d, 0);
+  }
+  if (carry) fn(8, 1, 0);
+  carry = 0;
+#pragma unroll
+  for (int w = 0; w < 16; w++) {
+    const int d = bv_digit(zk[w >> 1], w & 1, carry);
+    if (d) fn(w, d, 1);
+  }
+}
+
+MV_DEV void precomp_from_affine(precomp& pc, const p3& P) {
+  fe d2;
+  fe_const(d2, K_D2);
+  fe_addn(pc.ypx, P.Y, P.X);
+  fe_sub(pc.ymx, P.Y, P.X);
+  fe_mul(pc.xy2d, P.T, d2);  // P.Z = 1, P.T = xy
+}
+
+MV_DEV void pt_store(uint4* pts, size_t idx, const precomp& pc) {
+  uint4 q[7];
+  precomp_to_quads(q, pc);
+  uint4* p = pts + idx * PT_QUADS;
+#pragma unroll
+  for (int i = 0; i < 7; i++) p[i] = q[i];
+}
+MV_DEV void pt_load(precomp& pc, const uint4* pts, uint32_t idx) {
+  const uint4* p = pts + (size_t)idx * PT_QUADS;
+  uint4 q[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) q[i] = p[i];
+  quads_to_precomp(pc, q);
+}
+MV_DEV void p3_store(uint4* a, size_t idx, const p3& P) {
+  uint4 q[9];
+  p3_to_quads(q, P);
+  uint4* p = a + idx * P3_QUADS;
+#pragma unroll
+  for (int i = 0; i < 9; i++) p[i] = q[i];
+}
+MV_DEV void p3_load(p3& P, const uint4* a, size_t idx) {
+  const uint4* p = a + idx * P3_QUADS;
+  uint4 q[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) q[i] = p[i];
+  quads_to_p3(P, q);
+}
+// P += Q (both extended)
+MV_DEV void p3_acc(p3& P, const p3& Q) {
+  cached c;
+  p1p1 t;
+  p3_to_cached(c, Q);
+  p3_add_cached(t, P, c);
+  p1p1_to_p3(P, t);
+}
+MV_DEV void p3_dbl_n(p3& P, int n) {
+  if (n <= 0) return;
+  p2 q;
+  p1p1 t;
+  q.X = P.X; q.Y = P.Y; q.Z = P.Z;
+  for (int i = 1; i < n; i++) {
+    p2_dbl(t, q);
+    p1p1_to_p2(q, t);
+  }
+  p2_dbl(t, q);
+  p1p1_to_p3(P, t);
+}
+
+// ---------------------------------------------------------------- k_bv_prep
+struct BvKey {
+  uint32_t w[10];  // 32-byte secret, 64-bit call counter
+};
+
+__global__ void __launch_bounds__(256, 2)
+    k_bv_prep(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
+              const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, uint4* __restrict__ pts,
+              uint4* __restrict__ scal, uint32_t* __restrict__ counts, unsigned long long* __restrict__ bsum_part,
+              uint8_t* __restrict__ status) {
+  __shared__ unsigned long long sbsum[BSUM_WORDS];
+  if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = gid < n;
+  const uint32_t idx = live ? gid : n - 1;
+
+  uint32_t aw[8], rw[8], sw[8], mw[8];
+  load8(aw, pk + 32 * (size_t)(key_idx ? key_idx[idx] : idx));
+  load8(rw, sig + 64 * (size_t)idx);
+  load8(sw, sig + 64 * (size_t)idx + 32);
+  load8(mw, msg + 32 * (size_t)idx);
+  const bool s_ok = sc_is_canonical(sw);
+  uint32_t k[8];
+  {
+    uint32_t kin[24], h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      kin[i] = rw[i];
+      kin[8 + i] = aw[i];
+      kin[16 + i] = mw[i];
+    }
+    sha512_short(h, kin, 96);
+    sc_reduce512(k, h);
+  }
+  p3 A, R;
+  bool okA, okR;
+  decompress_x2(A, okA, aw, R, okR, rw);
+  const bool ok = live && okA && okR && s_ok;
+
+  // z = first 128 bits of BLAKE2b-256(secret || call || i)
+  uint32_t z[4];
+  {
+    uint64_t m[16], h[8];
+#pragma unroll
+    for (int i = 0; i < 5; i++) m[i] = (uint64_t)key.w[2 * i] | ((uint64_t)key.w[2 * i + 1] << 32);
+    m[5] = gid;
+#pragma unroll
+    for (int i = 6; i < 16; i++) m[i] = 0;
+    b2_init256(h);
+    b2_compress(h, m, 48, true);
+    z[0] = (uint32_t)h[0];
+    z[1] = (uint32_t)(h[0] >> 32);
+    z[2] = (uint32_t)h[1];
+    z[3] = (uint32_t)(h[1] >> 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) z[i] = ok ? z[i] : 0u;
+  uint32_t zk[8], z8[8], zero[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    z8[i] = i < 4 ? z[i] : 0u;
+    zero[i] = 0;
+  }
+  sc_muladd(zk, z8, k, zero);  // z * k mod l (0 when !ok)
+
+  if (live) {
+    precomp pc;
+    precomp_from_affine(pc, R);
+    pt_store(pts, gid, pc);
+    precomp_from_affine(pc, A);
+    pt_store(pts, (size_t)n + gid, pc);
+    uint4* sc = scal + (size_t)gid * SC_QUADS;
+    sc[0] = make_uint4(z[0], z[1], z[2], z[3]);
+    sc[1] = make_uint4(zk[0], zk[1], zk[2], zk[3]);
+    sc[2] = make_uint4(zk[4], zk[5], zk[6], zk[7]);
+    status[gid] = !okA ? 2 : (ok ? 0 : 1);
+  }
+  // bucket histogram
+  bv_for_digits(z, zk, [&](int w, int d, int) {
+    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+    atomicAdd(&counts[w * BV_NB + mag - 1], 1u);
+  });
+  // z * s (12 words, not reduced), summed per workgroup
+  {
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int c = 0; c < 11; c++) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (c - i >= 0 && c - i < 8) mac(acc, c2, z[i], sw[c - i]);
+      atomicAdd(&sbsum[c], (unsigned long long)(uint32_t)acc);
+      acc = (acc >> 32) | ((uint64_t)c2 << 32);
+      c2 = 0;
+    }
+    atomicAdd(&sbsum[11], (unsigned long long)(uint32_t)acc);
+  }
+  __syncthreads();
+  if (threadIdx.x < BSUM_WORDS) bsum_part[(size_t)blockIdx.x * BSUM_WORDS + threadIdx.x] = sbsum[threadIdx.x];
+}
+
+// ---------------------------------------------------------------- scan
+// exclusive scan of counts[NK]: 1024 keys per 256-thread block (4 per thread)
+constexpr int SCAN_PER_BLOCK = 1024;
+constexpr int SCAN_BLOCKS = BV_NK / SCAN_PER_BLOCK;  // 512
+
+MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
+  const int t = threadIdx.x;
+  sm[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    uint32_t x = t >= o ? sm[t - o] : 0u;
+    __syncthreads();
+    sm[t] += x;
+    __syncthreads();
+  }
+  total = sm[255];
+  const uint32_t incl = sm[t];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offs,
+                                                     uint32_t* __restrict__ btot) {
+  __shared__ uint32_t sm[256];
+  const uint32_t base = blockIdx.x * SCAN_PER_BLOCK + threadIdx.x * 4;
+  const uint4 c = *reinterpret_cast<const uint4*>(counts + base);
+  uint32_t total;
+  const uint32_t ex = block_excl_scan256(c.x + c.y + c.z + c.w, sm, total);
+  *reinterpret_cast<uint4*>(offs + base) = make_uint4(ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z);
+  if (threadIdx.x == 0) btot[blockIdx.x] = total;
+}
+__global__ void __launch_bounds__(256) k_scan_top(uint32_t* __restrict__ btot, uint32_t* __restrict__ offs) {
+  __shared__ uint32_t sm[256];
+  // 512 block totals, 2 per thread
+  const uint32_t a = btot[2 * threadIdx.x], b = btot[2 * threadIdx.x + 1];
+  uint32_t total;
+  const uint32_t ex = block_excl_scan256(a + b, sm, total);
+  btot[2 * threadIdx.x] = ex;
+  btot[2 * threadIdx.x + 1] = ex + a;
+  if (threadIdx.x == 0) offs[BV_NK] = total;
+}
+__global__ void __launch_bounds__(256) k_scan_add(const uint32_t* __restrict__ btot, uint32_t* __restrict__ offs,
+                                                  uint32_t* __restrict__ cursor) {
+  const uint32_t base = blockIdx.x * SCAN_PER_BLOCK + threadIdx.x * 4;
+  const uint32_t add = btot[blockIdx.x];
+  uint4 o = *reinterpret_cast<const uint4*>(offs + base);
+  o.x += add; o.y += add; o.z += add; o.w += add;
+  *reinterpret_cast<uint4*>(offs + base) = o;
+  *reinterpret_cast<uint4*>(cursor + base) = o;
+}
+
+// ---------------------------------------------------------------- scatter
+__global__ void __launch_bounds__(256) k_bv_scatter(const uint4* __restrict__ scal, uint32_t n,
+                                                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ ents) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  const uint4* sc = scal + (size_t)gid * SC_QUADS;
+  const uint4 q0 = sc[0], q1 = sc[1], q2 = sc[2];
+  const uint32_t z[4] = {q0.x, q0.y, q0.z, q0.w};
+  const uint32_t zk[8] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+  bv_for_digits(z, zk, [&](int w, int d, int isA) {
+    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+    const uint32_t pos = atomicAdd(&cursor[w * BV_NB + mag - 1], 1u);
+    const uint32_t pt = isA ? n + gid : gid;
+    ents[pos] = (pt << 1) | (d < 0 ? 1u : 0u);
+  });
+}
+
+// ---------------------------------------------------------------- buckets
+// Lane = segment (w, j): buckets of magnitude j*G + 1 .. j*G + G. Running sums from
+// the top bucket: T = sum of the segment's buckets, V = sum (m - j*G) * B_m.
+// The window's sum is then sum_j (V_j + j*G * T_j) (k_bv_reduce).
+__global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ ents, uint4* __restrict__ segV,
+                                                   uint4* __restrict__ segT) {
+  const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sidx >= (uint32_t)BV_NSEG) return;
+  const uint32_t key0 = sidx * BV_G;  // == w * NB + j * G
+  p3 T, S;
+  p3_identity(T);
+  p3_identity(S);
+  for (int b = BV_G - 1; b >= 0; b--) {
+    const uint32_t e0 = offs[key0 + b], e1 = offs[key0 + b + 1];
+    uint32_t e = e0;
+    uint32_t ent = e < e1 ? ents[e] : 0u;
+    while (e < e1) {
+      precomp pc;
+      pt_load(pc, pts, ent >> 1);
+      const bool neg = ent & 1u;
+      e++;
+      if (e < e1) ent = ents[e];  // next index ahead of the add
+      precomp_cneg(pc, neg);
+      p1p1 t;
+      p3_add_precomp(t, T, pc);
+      p1p1_to_p3(T, t);
+    }
+    p3_acc(S, T);
+  }
+  p3_store(segV, sidx, S);
+  p3_store(segT, sidx, T);
+}
+
+// ---------------------------------------------------------------- reduction
+// Elements (V, T) of one window with indices m = 0..cnt-1 stand for V + (m * scale) T.
+// Groups of FAN consecutive elements m = FAN*q + t become one element with index q:
+//   V' = sum V_t + scale * sum_t t T_t,   T' = sum T_t,   scale' = FAN * scale.
+// scale is a power of two (log2 = shift): the multiplication is `shift` doublings.
+__global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV, const uint4* __restrict__ inT,
+                                                  uint32_t cnt_in, int fan, int shift, uint4* __restrict__ outV,
+                                                  uint4* __restrict__ outT) {
+  const uint32_t cnt_out = (cnt_in + fan - 1) / fan;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= cnt_out * BV_NW) return;
+  const uint32_t w = gid / cnt_out, q = gid % cnt_out;
+  const size_t base = (size_t)w * cnt_in + (size_t)q * fan;
+  const int m = (int)min((uint32_t)fan, cnt_in - q * fan);
+  p3 U, Sx, Vs, X;
+  p3_identity(U);
+  p3_identity(Sx);
+  p3_identity(Vs);
+  for (int t = m - 1; t >= 0; t--) {
+    p3_load(X, inT, base + t);
+    p3_acc(U, X);
+    if (t > 0) p3_acc(Sx, U);  // sum_{t>=1} sum_{t'>=t} T_t' = sum t' T_t'
+    p3_load(X, inV, base + t);
+    p3_acc(Vs, X);
+  }
+  p3_dbl_n(Sx, shift);
+  p3_acc(Vs, Sx);
+  p3_store(outV, gid, Vs);
+  p3_store(outT, gid, U);
+}
+
+// ---------------------------------------------------------------- final check
+// One 128-thread block. Wave 0, lane 0: Horner over the window sums (V of the last
+// reduction level, one per window). Wave 1: -[sum z s mod l]B on the LDS B table.
+__global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV,
+                                                  const unsigned long long* __restrict__ bsum_part, uint32_t nparts,
+                                                  const uint4* __restrict__ btab_g, uint32_t* __restrict__ flag) {
+  __shared__ uint4 btab[BT_TABLE];
+  __shared__ unsigned long long sb[BSUM_WORDS];
+  __shared__ uint4 sbp[P3_QUADS];
+  lds_btab_load(btab, btab_g, BT_TABLE);
+  if (threadIdx.x < BSUM_WORDS) sb[threadIdx.x] = 0;
+  __syncthreads();
+  {
+    unsigned long long acc[BSUM_WORDS];
+#pragma unroll
+    for (int c = 0; c < BSUM_WORDS; c++) acc[c] = 0;
+    for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
+#pragma unroll
+      for (int c = 0; c < BSUM_WORDS; c++) acc[c] += bsum_part[(size_t)i * BSUM_WORDS + c];
+    }
+#pragma unroll
+    for (int c = 0; c < BSUM_WORDS; c++) atomicAdd(&sb[c], acc[c]);
+  }
+  __syncthreads();
+  p3 acc;
+  if (threadIdx.x >= 64) {
+    // x = sum z s mod l from the 12 column sums (each < 2^64)
+    uint32_t x[16];
+    unsigned long long carry = 0;
+#pragma unroll
+    for (int c = 0; c < BSUM_WORDS; c++) {
+      const unsigned long long v = sb[c];
+      const unsigned long long lo = (v & 0xffffffffull) + (carry & 0xffffffffull);
+      x[c] = (uint32_t)lo;
+      carry = (v >> 32) + (carry >> 32) + (lo >> 32);
+    }
+    x[12] = (uint32_t)carry;
+    x[13] = (uint32_t)(carry >> 32);
+    x[14] = x[15] = 0;
+    uint32_t r[8], sd[8];
+    sc_reduce512(r, x);
+    sc_recode256(sd, r);
+    p3 P;
+    basemul(P, sd, btab);
+    p3_neg(P, P);
+    if (threadIdx.x == 64) {
+      uint4 q[9];
+      p3_to_quads(q, P);
+#pragma unroll
+      for (int i = 0; i < 9; i++) sbp[i] = q[i];
+    }
+  } else if (threadIdx.x == 0) {
+    p3 S;
+    p3_load(acc, winV, BV_NW - 1);
+    for (int w = BV_NW - 2; w >= 0; w--) {
+      p3_dbl_n(acc, BV_C);
+      p3_load(S, winV, w);
+      p3_acc(acc, S);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint4 q[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) q[i] = sbp[i];
+    p3 P;
+    quads_to_p3(P, q);
+    p3_acc(acc, P);
+    p3_dbl_n(acc, 3);  // cofactor
+    *flag = p3_is_identity(acc) ? 1u : 0u;
+  }
+}
+
+}  // namespace mv
+
+// ---------------------------------------------------------------- launchers
+namespace mvk {
+
+namespace {
+constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+struct BatchLayout {
+  size_t pts, scal, counts, offs, cursor, btot, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
+  explicit BatchLayout(uint32_t n) {
+    using namespace mv;
+    const size_t nblk = (n + 255) / 256;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o += align256(bytes); return r; };
+    pts = take((size_t)2 * n * PT_QUADS * 16);
+    scal = take((size_t)n * SC_QUADS * 16);
+    counts = take((size_t)BV_NK * 4);
+    offs = take((size_t)(BV_NK + 1) * 4);
+    cursor = take((size_t)BV_NK * 4);
+    btot = take((size_t)SCAN_BLOCKS * 4);
+    ents = take((size_t)(BV_NWR + BV_NW) * n * 4);
+    segV = take((size_t)BV_NSEG * P3_QUADS * 16);
+    segT = take((size_t)BV_NSEG * P3_QUADS * 16);
+    const size_t lv = (size_t)(BV_NSEG / BV_FAN) * P3_QUADS * 16;
+    rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
+    bsum = take(nblk * BSUM_WORDS * 8);
+    flag = take(4);
+    total = o;
+  }
+};
+}  // namespace
+
+size_t batch_scratch_bytes(uint32_t n) { return BatchLayout(n).total; }
+
+hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                               uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
+                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out) {
+  using namespace mv;
+  if (n == 0) return hipSuccess;
+  const BatchLayout L(n);
+  char* base = static_cast<char*>(bscratch);
+  uint4* pts = (uint4*)(base + L.pts);
+  uint4* scal = (uint4*)(base + L.scal);
+  uint32_t* counts = (uint32_t*)(base + L.counts);
+  uint32_t* offs = (uint32_t*)(base + L.offs);
+  uint32_t* cursor = (uint32_t*)(base + L.cursor);
+  uint32_t* btot = (uint32_t*)(base + L.btot);
+  uint32_t* ents = (uint32_t*)(base + L.ents);
+  uint4* segV = (uint4*)(base + L.segV);
+  uint4* segT = (uint4*)(base + L.segT);
+  uint4* rv[2] = {(uint4*)(base + L.rV0), (uint4*)(base + L.rV1)};
+  uint4* rt[2] = {(uint4*)(base + L.rT0), (uint4*)(base + L.rT1)};
+  unsigned long long* bsum = (unsigned long long*)(base + L.bsum);
+  uint32_t* flag = (uint32_t*)(base + L.flag);
+  if (flag_out) *flag_out = flag;
+  const uint32_t nblk = (n + 255) / 256;
+  hipError_t e = hipMemsetAsync(counts, 0, (size_t)BV_NK * 4, s);
+  if (e != hipSuccess) return e;
+  BvKey k;
+  for (int i = 0; i < 10; i++) k.w[i] = key[i];
+  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, counts, bsum,
+                     status);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(SCAN_BLOCKS), dim3(256), 0, s, counts, offs, btot);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, btot, offs);
+  hipLaunchKernelGGL(k_scan_add, dim3(SCAN_BLOCKS), dim3(256), 0, s, btot, offs, cursor);
+  hipLaunchKernelGGL(k_bv_scatter, dim3(nblk), dim3(256), 0, s, scal, n, cursor, ents);
+  hipLaunchKernelGGL(k_bv_bucket, dim3(BV_NSEG / 256), dim3(256), 0, s, pts, offs, ents, segV, segT);
+  const uint4* inV = segV;
+  const uint4* inT = segT;
+  uint32_t cnt = BV_SEGW;
+  int shift = 2;  // log2(BV_G)
+  int pp = 0;
+  while (cnt > 1) {
+    const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
+    const uint32_t out = (cnt + fan - 1) / fan;
+    const uint32_t lanes = out * BV_NW;
+    hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rv[pp],
+                       rt[pp]);
+    inV = rv[pp];
+    inT = rt[pp];
+    pp ^= 1;
+    shift += fan == 8 ? 3 : (fan == 4 ? 2 : 1);
+    cnt = out;
+  }
+  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, bsum, nblk, (const uint4*)btab, flag);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // exact fallback: re-verifies every signature iff the combination failed
+  return launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag);
+}
+
+}  // namespace mvk

@@ -6,6 +6,7 @@
 // (one stream per device, no collective: only per-item verdicts come back), in
 // chunks of at most cfg.max_batch items. Calls on one ctx are serialised by a mutex.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -73,6 +74,7 @@ struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
   DevBuf btab, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2, committee_pk;
+  DevBuf bscratch;  // batch-path scratch (batch.hip BatchLayout)
   HostBuf h_in, h_out;
   bool committee_loaded = false;
 };
@@ -84,6 +86,10 @@ struct mv_ctx {
   std::vector<Device> devs;
   std::string err;
   uint32_t max_batch = 1u << 20;
+  uint32_t flags = 0;
+  uint32_t secret[8] = {0};         // batch-path z_i PRF key (from /dev/urandom)
+  std::atomic<uint64_t> calls{0};   // batch calls, the PRF's per-call input
+  std::atomic<uint64_t> batches{0}, fallbacks{0};
   bool has_committee = false;
   mvh::Committee committee;
 };
@@ -127,6 +133,21 @@ mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
   return MV_OK;
 }
 
+// Enqueues the batch path (batch.hip) for n signatures on stream s.
+mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
+                        const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s, uint32_t** flag) {
+  HIPCHK(ctx, dev.bscratch.ensure(mvk::batch_scratch_bytes(n)));
+  HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(n)));
+  uint32_t key[10];
+  memcpy(key, ctx->secret, 32);
+  const uint64_t call = ctx->calls.fetch_add(1);
+  key[8] = (uint32_t)call;
+  key[9] = (uint32_t)(call >> 32);
+  HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscratch.p,
+                                       dev.scratch.p, d_status, s, flag));
+  return MV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -148,6 +169,16 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   uint32_t mask = cfg && cfg->device_mask ? cfg->device_mask : 1u;
   mv_ctx* ctx = new mv_ctx();
   if (cfg && cfg->max_batch) ctx->max_batch = cfg->max_batch;
+  if (cfg) ctx->flags = cfg->flags;
+  {
+    FILE* f = fopen("/dev/urandom", "rb");
+    size_t got = f ? fread(ctx->secret, 1, sizeof(ctx->secret), f) : 0;
+    if (f) fclose(f);
+    if (got != sizeof(ctx->secret)) {
+      delete ctx;
+      return MV_E_INVALID_ARG;  // no entropy source: refuse rather than use predictable z_i
+    }
+  }
   for (int d = 0; d < 32; d++) {
     if (!(mask & (1u << d))) continue;
     if (d >= ndev) {
@@ -179,7 +210,7 @@ void mv_destroy(mv_ctx* ctx) {
     (void)hipSetDevice(dev.id);
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
     for (DevBuf* b : {&dev.btab, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status, &dev.bytes,
-                      &dev.off, &dev.len, &dev.out2, &dev.committee_pk})
+                      &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.bscratch})
       b->release();
     dev.h_in.release();
     dev.h_out.release();
@@ -284,7 +315,6 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
       HIPCHK(ctx, dev.msg.ensure(32 * (size_t)m));
       HIPCHK(ctx, dev.sig.ensure(64 * (size_t)m));
       HIPCHK(ctx, dev.status.ensure(m));
-      HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
       HIPCHK(ctx, hipMemcpyAsync(dev.msg.p, msg + 32 * i, 32 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(dev.sig.p, sig + 64 * i, 64 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
       const uint8_t* dpk;
@@ -299,10 +329,24 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
         dpk = dev.committee_pk.as<uint8_t>();
         dki = dev.keyidx.as<uint32_t>();
       }
-      HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m, dev.btab.p,
-                                     dev.scratch.p, dev.status.as<uint8_t>(), dev.stream));
+      uint32_t* d_flag = nullptr;
+      uint32_t h_flag = 1;
+      if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
+        mv_status st = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m,
+                                     dev.status.as<uint8_t>(), dev.stream, &d_flag);
+        if (st != MV_OK) return st;
+        HIPCHK(ctx, hipMemcpyAsync(&h_flag, d_flag, 4, hipMemcpyDeviceToHost, dev.stream));
+      } else {
+        HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
+        HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m, dev.btab.p,
+                                       dev.scratch.p, dev.status.as<uint8_t>(), dev.stream));
+      }
       HIPCHK(ctx, hipMemcpyAsync(status + i, dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
+      if (d_flag) {
+        ctx->batches++;
+        if (!h_flag) ctx->fallbacks++;
+      }
     }
     return MV_OK;
   });
@@ -423,6 +467,32 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
   HIPCHK(ctx, dev->scratch.ensure(mvk::verify_scratch_bytes(n)));
   HIPCHK(ctx, mvk::launch_verify(d_msg, d_sig, d_pk, nullptr, n, dev->btab.p, dev->scratch.p, d_status, s));
+  return MV_OK;
+}
+
+mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
+                                      const uint8_t* d_pk, const uint32_t* d_key_idx, uint32_t n,
+                                      uint8_t* d_status, uint32_t* d_batch_ok, void* stream) {
+  if (!ctx || (n && (!d_msg || !d_sig || !d_pk || !d_status))) return set_err(ctx, MV_E_INVALID_ARG, "bad args");
+  if ((((uintptr_t)d_msg) | ((uintptr_t)d_sig) | ((uintptr_t)d_pk)) & 15)
+    return set_err(ctx, MV_E_INVALID_ARG, "device inputs must be 16-byte aligned");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  Device* dev = find_dev(ctx, device);
+  if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
+  if (n == 0) return MV_OK;
+  HIPCHK(ctx, hipSetDevice(dev->id));
+  hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
+  uint32_t* d_flag = nullptr;
+  mv_status st = enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, &d_flag);
+  if (st != MV_OK) return st;
+  if (d_batch_ok) HIPCHK(ctx, hipMemcpyAsync(d_batch_ok, d_flag, 4, hipMemcpyDeviceToDevice, s));
+  return MV_OK;
+}
+
+mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks) {
+  if (!ctx) return MV_E_INVALID_ARG;
+  if (batches) *batches = ctx->batches.load();
+  if (fallbacks) *fallbacks = ctx->fallbacks.load();
   return MV_OK;
 }
 

@@ -9,7 +9,8 @@ size_t verify_scratch_bytes(uint32_t n);
 size_t btable_bytes();
 hipError_t launch_btable_init(void* d_btab, hipStream_t s);
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
-                         uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s);
+                         uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
+                         const uint32_t* skip = nullptr);
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
                        uint8_t* sig, hipStream_t s);
 hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
@@ -17,4 +18,11 @@ hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_
 hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                              uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
 hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s);
+// batch.hip: random-linear-combination batch verify with exact on-device fallback.
+// key = 32-byte secret + 64-bit call counter (the z_i PRF key); *flag_out receives the
+// device address of the batch flag (1 = the combined equation held).
+size_t batch_scratch_bytes(uint32_t n);
+hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                               uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
+                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out);
 }  // namespace mvk

@@ -1,0 +1,164 @@
+"""GPU: the batch path (batch.hip: one random linear combination checked as a
+multi-scalar multiplication, exact per-signature fallback on the device).
+
+Verdicts must equal the single-signature verdicts (oracle / golden fixtures) in every
+case. The batch counters show which way each batch went: all-valid batches, including
+ZIP-215 edge cases that single verification accepts (small-order and mixed-order A/R,
+non-canonical encodings), must pass the combined equation without falling back;
+batches with an invalid signature must fall back and still be exact.
+"""
+import numpy as np
+import pytest
+
+import mysticeti_amd as M
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def arr(hexes, w):
+    return np.frombuffer(b"".join(bytes.fromhex(h) for h in hexes), dtype=np.uint8).reshape(-1, w)
+
+
+def signed(engine, n, seed):
+    rng = np.random.default_rng(seed)
+    s = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    m = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    pk, sig = engine.ed25519_sign(s, m)
+    return m, sig, pk
+
+
+def stats_delta(engine, fn):
+    b0, f0 = engine.batch_stats()
+    out = fn()
+    b1, f1 = engine.batch_stats()
+    return out, b1 - b0, f1 - f0
+
+
+@pytest.mark.parametrize("n", [M.BATCH_MIN, M.BATCH_MIN + 1, 5000, 65536 + 17])
+def test_valid_batches_pass_without_fallback(engine, n):
+    msg, sig, pk = signed(engine, n, n)
+    st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+    assert (st == 0).all()
+    assert nb == 1 and nf == 0
+
+
+def test_one_bad_signature_falls_back_exactly(engine):
+    n = 8192
+    msg, sig, pk = signed(engine, n, 1)
+    for where, byte in [(0, 5), (n - 1, 40), (4321, 63)]:
+        s2 = sig.copy()
+        s2[where, byte] ^= 0x10
+        st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, s2, pk))
+        ref = O.verify_batch(pk, s2, msg)
+        assert (st == ref).all()
+        assert nb == 1 and nf == 1
+        assert st[where] != 0 and (np.delete(st, where) == 0).all()
+
+
+def test_wrong_message_falls_back(engine):
+    n = 4096
+    msg, sig, pk = signed(engine, n, 2)
+    m2 = msg.copy()
+    m2[77, 0] ^= 1
+    st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(m2, sig, pk))
+    assert nf == 1 and st[77] == 1 and (np.delete(st, 77) == 0).all()
+
+
+def test_prerejected_items_do_not_fail_the_batch(engine, golden):
+    """s >= l, undecodable R and undecodable A are decided per signature before the
+    combination and excluded from it: the batch still passes, the verdicts are exact."""
+    n = 4096
+    msg, sig, pk = signed(engine, n, 3)
+    sig, pk = sig.copy(), pk.copy()
+    l_bytes = (2**252 + 27742317777372353535851937790883648493).to_bytes(32, "little")
+    sig[10, 32:] = np.frombuffer(l_bytes, np.uint8)  # s = l
+    sig[11, 63] |= 0x80                              # s with bit 255
+    cases = golden("zip215_corpus.json")
+    bad_r = next(c for c in cases if c["status"] == 1 and c["note"].startswith("R undecodable"))
+    bad_a = next(c for c in cases if c["status"] == 2)
+    sig[12, :32] = np.frombuffer(bytes.fromhex(bad_r["sig"])[:32], np.uint8)
+    pk[13] = np.frombuffer(bytes.fromhex(bad_a["pk"]), np.uint8)
+    st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+    ref = O.verify_batch(pk, sig, msg)
+    assert (st == ref).all()
+    assert list(st[10:14]) == [1, 1, 1, 2]
+    assert nb == 1 and nf == 0
+
+
+def test_zip215_accepts_pass_the_combination(engine, golden):
+    """Every corpus case single verification accepts (small-order A and R, mixed-order
+    points, non-canonical y, x = 0 with the sign bit) is also accepted by the combined
+    cofactored equation: no fallback."""
+    cases = [c for c in golden("zip215_corpus.json") if c["status"] == 0]
+    assert len(cases) > 200
+    # the small-order s = 0 pairs carry a 5-byte message in the corpus; their verdict
+    # does not depend on the message (test_gpu_verify.test_zip215_small_order_msgs)
+    m0 = arr([c["msg"] if len(c["msg"]) == 64 else "00" * 32 for c in cases], 32)
+    s0, p0 = arr([c["sig"] for c in cases], 64), arr([c["pk"] for c in cases], 32)
+    msg, sig, pk = signed(engine, M.BATCH_MIN, 4)
+    msg, sig, pk = np.concatenate([m0, msg]), np.concatenate([s0, sig]), np.concatenate([p0, pk])
+    st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+    assert (st == 0).all()
+    assert nb == 1 and nf == 0
+
+
+def test_zip215_corpus_through_batch_path(engine, golden):
+    cases = [c for c in golden("zip215_corpus.json") if len(c["msg"]) == 64]
+    m0, s0, p0 = arr([c["msg"] for c in cases], 32), arr([c["sig"] for c in cases], 64), arr([c["pk"] for c in cases], 32)
+    reps = M.BATCH_MIN // len(cases) + 1
+    msg, sig, pk = np.tile(m0, (reps, 1)), np.tile(s0, (reps, 1)), np.tile(p0, (reps, 1))
+    st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+    want = np.tile(np.array([c["status"] for c in cases], np.uint8), reps)
+    assert nb == 1
+    assert (st == want).all()
+
+
+def test_committee_key_index(engine):
+    """key_idx rows (committee keys, the block path's layout) through the batch path."""
+    rng = np.random.default_rng(5)
+    seeds = rng.integers(0, 256, size=(7, 32), dtype=np.uint8)
+    n = 6000
+    ki = rng.integers(0, 7, size=n).astype(np.uint32)
+    msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    pk, sig = engine.ed25519_sign(seeds[ki], msg)
+    engine.set_committee(pk[[int(np.nonzero(ki == a)[0][0]) for a in range(7)]], np.ones(7, np.uint64))
+    sig[99, 3] ^= 4
+    st = engine.ed25519_verify(msg, sig, key_idx=ki)
+    assert st[99] == 1 and (np.delete(st, 99) == 0).all()
+
+
+def test_batch_and_single_paths_agree(golden):
+    rng = np.random.default_rng(6)
+    n = 4500
+    with M.Engine(devices=(0,), batch=False) as single, M.Engine(devices=(0,)) as batched:
+        msg, sig, pk = signed(single, n, 7)
+        sig = sig.copy()
+        bad = rng.random(n) < 0.002
+        sig[bad, 33] ^= 2
+        a = single.ed25519_verify(msg, sig, pk)
+        b = batched.ed25519_verify(msg, sig, pk)
+        assert (a == b).all() and (a[bad] == 1).all()
+        assert single.batch_stats() == (0, 0) and batched.batch_stats() == (1, 1)
+
+
+def test_device_api_flag(engine):
+    import torch
+
+    n = 8192
+    msg, sig, pk = signed(engine, n, 8)
+    dev = torch.device("cuda", 0)
+    dm, ds, dp = (torch.from_numpy(x.copy()).to(dev) for x in (msg, sig, pk))
+    dst = torch.full((n,), 255, dtype=torch.uint8, device=dev)
+    ok = torch.zeros(1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    engine.dev_verify_batch(0, dm, ds, dp, dst, ok)
+    torch.cuda.synchronize()
+    assert int(ok.item()) == 1 and (dst.cpu().numpy() == 0).all()
+    ds[17, 50] ^= 1
+    dst.fill_(255)
+    torch.cuda.synchronize()
+    engine.dev_verify_batch(0, dm, ds, dp, dst, ok)
+    torch.cuda.synchronize()
+    st = dst.cpu().numpy()
+    assert int(ok.item()) == 0 and st[17] == 1 and (np.delete(st, 17) == 0).all()

@@ -52,11 +52,11 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 3; rep++) {
     CK(hipEventRecord(e0, 0));
     if (occ == 1)
-      hipLaunchKernelGGL(mv::k_verify<1>, grid, block, 0, 0, msg, sig, pk, nullptr, n, btab, scr, st);
+      hipLaunchKernelGGL(mv::k_verify<1>, grid, block, 0, 0, msg, sig, pk, nullptr, n, btab, scr, st, (const uint32_t*)nullptr);
     else if (occ == 3)
-      hipLaunchKernelGGL(mv::k_verify<3>, grid, block, 0, 0, msg, sig, pk, nullptr, n, btab, scr, st);
+      hipLaunchKernelGGL(mv::k_verify<3>, grid, block, 0, 0, msg, sig, pk, nullptr, n, btab, scr, st, (const uint32_t*)nullptr);
     else
-      hipLaunchKernelGGL(mv::k_verify<2>, grid, block, 0, 0, msg, sig, pk, nullptr, n, btab, scr, st);
+      hipLaunchKernelGGL(mv::k_verify<2>, grid, block, 0, 0, msg, sig, pk, nullptr, n, btab, scr, st, (const uint32_t*)nullptr);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
