@@ -98,6 +98,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20, help="0 disables the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--path", choices=["batch", "single"], default="batch",
+                    help="batch: one combined equation per step (batch.hip) with exact fallback; "
+                         "single: every signature verified alone (k_verify)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -134,8 +137,13 @@ def main():
     eng.dev_sign(local_rank, d_seed, d_msg, d_pk, d_sig, stream.cuda_stream)
     torch.cuda.synchronize(dev)
 
-    def step():
-        eng.dev_verify(local_rank, d_msg, d_sig, d_pk, d_status, stream.cuda_stream)
+    d_ok = torch.zeros(1, dtype=torch.int32, device=dev)
+    if args.path == "batch":
+        def step():
+            eng.dev_verify_batch(local_rank, d_msg, d_sig, d_pk, d_status, d_ok, stream.cuda_stream)
+    else:
+        def step():
+            eng.dev_verify(local_rank, d_msg, d_sig, d_pk, d_status, stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()

@@ -126,9 +126,9 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
                                 const uint8_t* d_pk, uint32_t n, uint8_t* d_status, void* stream);
 /* Batch path on device buffers: verdicts identical to mv_dev_ed25519_verify. The combined
  * equation [8](-[sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i) == O with secret random
- * 128-bit z_i (BLAKE2b PRF keyed per context and call) is checked first; if it fails, every
+ * 127-bit z_i (BLAKE2b PRF keyed per context and call) is checked first; if it fails, every
  * signature is re-verified individually on the same stream, so each verdict is exact (an
- * invalid signature survives a passing combination with probability <= 2^-128).
+ * invalid signature survives a passing combination with probability <= 2^-127).
  * `d_pk` rows are indexed by item, or by `d_key_idx` (device array) when it is non-NULL.
  * Enqueues only; `d_batch_ok` (optional, device, 4 bytes) receives 1 if the combination held. */
 mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,

@@ -5,11 +5,11 @@
 // Semantics: ed25519-consensus 2.1.0 `batch::Verifier` (the ZIP-215 batch rule that
 // is designed to agree with the single `VerificationKey::verify` called at
 // mysticeti-core/src/crypto.rs:188): for signatures (A_i, R_i, s_i) with challenges
-// k_i and independent uniformly random 128-bit z_i,
+// k_i and independent uniformly random 127-bit z_i,
 //     [8]( -[sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i ) == O.
 // Every individually valid signature satisfies [8]([s_i]B - [k_i]A_i - R_i) = O, so a
 // batch of valid signatures always passes; a batch holding an invalid one passes with
-// probability <= 2^-128 over the z_i. Per-signature preconditions (s < l, A and R
+// probability <= 2^-127 over the z_i. Per-signature preconditions (s < l, A and R
 // decode) are decided exactly in k_bv_prep and excluded from the combination. When
 // the combination fails, k_verify (kernels.hip) re-verifies every signature of the
 // batch individually (it reads the batch flag and exits at once when it passed), so
@@ -19,13 +19,13 @@
 //   k_bv_prep     lane per signature: SHA-512 challenge, ZIP-215 decode of A and R,
 //                 z_i = BLAKE2b(secret || call || i), scalars z_i and z_i k_i mod l,
 //                 affine points (y+x, y-x, 2dxy) to HBM, bucket histogram, sum z_i s_i
-//   k_scan_*      exclusive scan of the histogram -> bucket offsets
-//   k_bv_scatter  lane per signature: (point, sign) entries into their buckets
-//   k_bv_bucket   lane per 4-bucket segment of a window: bucket sums and the
+//   k_part_*, k_fine_sort   two-pass counting sort of the (bucket, point) entries
+//                 (LDS histograms and ranks; no global atomics)
+//   k_bv_bucket   lane per 2-bucket segment of a window: bucket sums and the
 //                 segment's running sums (V = sum (b - b0) B_b, T = sum B_b)
 //   k_bv_reduce   tree over segments (fan-in 8) of the pairs (V, T) per window
 //   k_bv_final    Horner over the 16 window sums, -[sum z s]B, [8], identity test
-// Windows: signed radix 2^16, |digit| <= 2^15; R scalars use windows 0..8 (8 + carry),
+// Windows: signed radix 2^16, |digit| <= 2^15; R scalars (z < 2^127) use windows 0..7,
 // A scalars (< l < 2^253) windows 0..15.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -42,9 +42,11 @@ namespace mv {
 constexpr int BV_C = 16;                    // window bits
 constexpr int BV_NB = 1 << (BV_C - 1);      // bucket magnitudes 1..2^15 per window
 constexpr int BV_NW = 16;                   // windows
-constexpr int BV_NWR = 9;                   // windows of the 128-bit R scalars
+constexpr int BV_NWR = 8;                   // windows of the 127-bit R scalars
 constexpr int BV_NK = BV_NW * BV_NB;        // bucket keys, key = w * NB + |d| - 1
-constexpr int BV_G = 4;                     // buckets per segment lane
+constexpr int BV_G = 2;                     // buckets per segment lane
+constexpr int BV_FINE_BITS = 10;            // bucket sort: partition = key >> 10 (window +
+constexpr int BV_NPART = BV_NK >> BV_FINE_BITS;  // 5 high magnitude bits), then 1024 buckets
 constexpr int BV_SEGW = BV_NB / BV_G;       // segments per window
 constexpr int BV_NSEG = BV_NW * BV_SEGW;
 constexpr int BV_FAN = 8;                   // reduction fan-in
@@ -61,23 +63,34 @@ MV_DEV int bv_digit(uint32_t word, int half, uint32_t& carry) {
   return (int)v - (int)(carry << 16);
 }
 
-// Calls fn(window, digit) for every nonzero digit of (z, zk).
+// Calls fn(window, digit, isA) for every nonzero digit of (z, zk). z < 2^127 and
+// zk < 2^253 leave the top windows (7 and 15) with a value <= 2^15 after the carry,
+// so they take it unsigned: no carry window, and no bucket collects half the batch.
 template <class Fn>
 MV_DEV void bv_for_digits(const uint32_t z[4], const uint32_t zk[8], Fn fn) {
   uint32_t carry = 0;
 #pragma unroll
-  for (int w = 0; w < 8; w++) {
+  for (int w = 0; w < 7; w++) {
     const int d = bv_digit(z[w >> 1], w & 1, carry);
     if (d) fn(w, d, 0);
   }
-  if (carry) fn(8, 1, 0);
+  {
+    const int d = (int)((z[3] >> 16) + carry);
+    if (d) fn(7, d, 0);
+  }
   carry = 0;
 #pragma unroll
-  for (int w = 0; w < 16; w++) {
+  for (int w = 0; w < 15; w++) {
     const int d = bv_digit(zk[w >> 1], w & 1, carry);
     if (d) fn(w, d, 1);
   }
+  {
+    const int d = (int)((zk[7] >> 16) + carry);
+    if (d) fn(15, d, 1);
+  }
 }
+
+MV_DEV uint32_t bv_key(int w, int d) { return (uint32_t)w * BV_NB + (uint32_t)(d < 0 ? -d : d) - 1u; }
 
 MV_DEV void precomp_from_affine(precomp& pc, const p3& P) {
   fe d2;
@@ -144,10 +157,12 @@ struct BvKey {
 __global__ void __launch_bounds__(256, 2)
     k_bv_prep(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
               const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, uint4* __restrict__ pts,
-              uint4* __restrict__ scal, uint32_t* __restrict__ counts, unsigned long long* __restrict__ bsum_part,
+              uint4* __restrict__ scal, uint32_t* __restrict__ pcount, unsigned long long* __restrict__ bsum_part,
               uint8_t* __restrict__ status) {
   __shared__ unsigned long long sbsum[BSUM_WORDS];
+  __shared__ uint32_t hist[BV_NPART];
   if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < BV_NPART; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = gid < n;
@@ -190,7 +205,7 @@ __global__ void __launch_bounds__(256, 2)
     z[0] = (uint32_t)h[0];
     z[1] = (uint32_t)(h[0] >> 32);
     z[2] = (uint32_t)h[1];
-    z[3] = (uint32_t)(h[1] >> 32);
+    z[3] = (uint32_t)(h[1] >> 32) & 0x7fffffffu;  // z < 2^127
   }
 #pragma unroll
   for (int i = 0; i < 4; i++) z[i] = ok ? z[i] : 0u;
@@ -214,11 +229,8 @@ __global__ void __launch_bounds__(256, 2)
     sc[2] = make_uint4(zk[4], zk[5], zk[6], zk[7]);
     status[gid] = !okA ? 2 : (ok ? 0 : 1);
   }
-  // bucket histogram
-  bv_for_digits(z, zk, [&](int w, int d, int) {
-    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-    atomicAdd(&counts[w * BV_NB + mag - 1], 1u);
-  });
+  // this chunk's entries per partition (LDS atomics; no global atomics anywhere)
+  bv_for_digits(z, zk, [&](int w, int d, int) { atomicAdd(&hist[bv_key(w, d) >> BV_FINE_BITS], 1u); });
   // z * s (12 words, not reduced), summed per workgroup
   {
     uint64_t acc = 0;
@@ -236,13 +248,17 @@ __global__ void __launch_bounds__(256, 2)
   }
   __syncthreads();
   if (threadIdx.x < BSUM_WORDS) bsum_part[(size_t)blockIdx.x * BSUM_WORDS + threadIdx.x] = sbsum[threadIdx.x];
+  for (int i = threadIdx.x; i < BV_NPART; i += blockDim.x) pcount[(size_t)blockIdx.x * BV_NPART + i] = hist[i];
 }
 
-// ---------------------------------------------------------------- scan
-// exclusive scan of counts[NK]: 1024 keys per 256-thread block (4 per thread)
-constexpr int SCAN_PER_BLOCK = 1024;
-constexpr int SCAN_BLOCKS = BV_NK / SCAN_PER_BLOCK;  // 512
-
+// ---------------------------------------------------------------- bucket sort
+// Two-pass counting sort of the (bucket key, point) entries without global atomics:
+//   k_part_scan / k_part_top   exclusive offsets of every (chunk, partition) run from the
+//                              per-chunk partition counts k_bv_prep wrote
+//   k_part_scatter             chunk = 256 signatures: entries (key, point) into their
+//                              partition, runs ordered by chunk, ranks from LDS atomics
+//   k_fine_sort                workgroup per partition: counting sort by the low 10 key
+//                              bits in LDS -> final bucket lists and bucket offsets
 MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
   const int t = threadIdx.x;
   sm[t] = v;
@@ -259,76 +275,131 @@ MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
   return incl - v;
 }
 
-__global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offs,
-                                                     uint32_t* __restrict__ btot) {
+// block p: scan of pcount[c][p] over the nchunk chunks -> poff[c][p], ptot[p]
+__global__ void __launch_bounds__(256) k_part_scan(const uint32_t* __restrict__ pcount, uint32_t nchunk,
+                                                   uint32_t* __restrict__ poff, uint32_t* __restrict__ ptot) {
   __shared__ uint32_t sm[256];
-  const uint32_t base = blockIdx.x * SCAN_PER_BLOCK + threadIdx.x * 4;
-  const uint4 c = *reinterpret_cast<const uint4*>(counts + base);
+  const uint32_t p = blockIdx.x;
+  const uint32_t per = (nchunk + 255) / 256;
+  const uint32_t c0 = threadIdx.x * per, c1 = min(nchunk, c0 + per);
+  uint32_t sum = 0;
+  for (uint32_t c = c0; c < c1; c++) sum += pcount[(size_t)c * BV_NPART + p];
   uint32_t total;
-  const uint32_t ex = block_excl_scan256(c.x + c.y + c.z + c.w, sm, total);
-  *reinterpret_cast<uint4*>(offs + base) = make_uint4(ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z);
-  if (threadIdx.x == 0) btot[blockIdx.x] = total;
+  uint32_t run = block_excl_scan256(sum, sm, total);
+  for (uint32_t c = c0; c < c1; c++) {
+    const uint32_t v = pcount[(size_t)c * BV_NPART + p];
+    poff[(size_t)c * BV_NPART + p] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) ptot[p] = total;
 }
-__global__ void __launch_bounds__(256) k_scan_top(uint32_t* __restrict__ btot, uint32_t* __restrict__ offs) {
+// exclusive scan of the 512 partition totals -> pstart[0..512]
+__global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ ptot, uint32_t* __restrict__ pstart) {
   __shared__ uint32_t sm[256];
-  // 512 block totals, 2 per thread
-  const uint32_t a = btot[2 * threadIdx.x], b = btot[2 * threadIdx.x + 1];
+  const uint32_t a = ptot[2 * threadIdx.x], b = ptot[2 * threadIdx.x + 1];
   uint32_t total;
   const uint32_t ex = block_excl_scan256(a + b, sm, total);
-  btot[2 * threadIdx.x] = ex;
-  btot[2 * threadIdx.x + 1] = ex + a;
-  if (threadIdx.x == 0) offs[BV_NK] = total;
+  pstart[2 * threadIdx.x] = ex;
+  pstart[2 * threadIdx.x + 1] = ex + a;
+  if (threadIdx.x == 0) pstart[BV_NPART] = total;
 }
-__global__ void __launch_bounds__(256) k_scan_add(const uint32_t* __restrict__ btot, uint32_t* __restrict__ offs,
-                                                  uint32_t* __restrict__ cursor) {
-  const uint32_t base = blockIdx.x * SCAN_PER_BLOCK + threadIdx.x * 4;
-  const uint32_t add = btot[blockIdx.x];
-  uint4 o = *reinterpret_cast<const uint4*>(offs + base);
-  o.x += add; o.y += add; o.z += add; o.w += add;
-  *reinterpret_cast<uint4*>(offs + base) = o;
-  *reinterpret_cast<uint4*>(cursor + base) = o;
-}
-
-// ---------------------------------------------------------------- scatter
-__global__ void __launch_bounds__(256) k_bv_scatter(const uint4* __restrict__ scal, uint32_t n,
-                                                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ ents) {
+__global__ void __launch_bounds__(256) k_part_scatter(const uint4* __restrict__ scal, uint32_t n,
+                                                      const uint32_t* __restrict__ poff,
+                                                      const uint32_t* __restrict__ pstart,
+                                                      unsigned long long* __restrict__ tmp) {
+  __shared__ uint32_t rank[BV_NPART];
+  for (int i = threadIdx.x; i < BV_NPART; i += blockDim.x) rank[i] = 0;
+  __syncthreads();
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= n) return;
-  const uint4* sc = scal + (size_t)gid * SC_QUADS;
-  const uint4 q0 = sc[0], q1 = sc[1], q2 = sc[2];
-  const uint32_t z[4] = {q0.x, q0.y, q0.z, q0.w};
-  const uint32_t zk[8] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-  bv_for_digits(z, zk, [&](int w, int d, int isA) {
-    const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-    const uint32_t pos = atomicAdd(&cursor[w * BV_NB + mag - 1], 1u);
-    const uint32_t pt = isA ? n + gid : gid;
-    ents[pos] = (pt << 1) | (d < 0 ? 1u : 0u);
-  });
+  if (gid < n) {
+    const uint4* sc = scal + (size_t)gid * SC_QUADS;
+    const uint4 q0 = sc[0], q1 = sc[1], q2 = sc[2];
+    const uint32_t z[4] = {q0.x, q0.y, q0.z, q0.w};
+    const uint32_t zk[8] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    const uint32_t* po = poff + (size_t)blockIdx.x * BV_NPART;
+    bv_for_digits(z, zk, [&](int w, int d, int isA) {
+      const uint32_t key = bv_key(w, d);
+      const uint32_t p = key >> BV_FINE_BITS;
+      const uint32_t r = atomicAdd(&rank[p], 1u);
+      const uint32_t pt = isA ? n + gid : gid;
+      tmp[pstart[p] + po[p] + r] = ((unsigned long long)key << 32) | (pt << 1) | (d < 0 ? 1u : 0u);
+    });
+  }
+}
+// block p: the partition's entries sorted by bucket into ents; offs[key] for its 1024 keys
+__global__ void __launch_bounds__(256) k_fine_sort(const unsigned long long* __restrict__ tmp,
+                                                   const uint32_t* __restrict__ pstart, uint32_t* __restrict__ ents,
+                                                   uint32_t* __restrict__ offs) {
+  constexpr int NF = 1 << BV_FINE_BITS;
+  __shared__ uint32_t cnt[NF];
+  __shared__ uint32_t sm[256];
+  const uint32_t p = blockIdx.x;
+  const uint32_t s = pstart[p], e = pstart[p + 1];
+  for (int i = threadIdx.x; i < NF; i += 256) cnt[i] = 0;
+  __syncthreads();
+  for (uint32_t i = s + threadIdx.x; i < e; i += 256) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
+  __syncthreads();
+  const uint32_t c0 = cnt[4 * threadIdx.x], c1 = cnt[4 * threadIdx.x + 1], c2 = cnt[4 * threadIdx.x + 2],
+                 c3 = cnt[4 * threadIdx.x + 3];
+  uint32_t total;
+  const uint32_t ex = block_excl_scan256(c0 + c1 + c2 + c3, sm, total);
+  const uint32_t o0 = ex, o1 = ex + c0, o2 = o1 + c1, o3 = o2 + c2;
+  *reinterpret_cast<uint4*>(offs + (size_t)p * NF + 4 * threadIdx.x) = make_uint4(s + o0, s + o1, s + o2, s + o3);
+  if (p == BV_NPART - 1 && threadIdx.x == 0) offs[BV_NK] = e;
+  cnt[4 * threadIdx.x] = o0;
+  cnt[4 * threadIdx.x + 1] = o1;
+  cnt[4 * threadIdx.x + 2] = o2;
+  cnt[4 * threadIdx.x + 3] = o3;
+  __syncthreads();
+  for (uint32_t i = s + threadIdx.x; i < e; i += 256) {
+    const unsigned long long v = tmp[i];
+    const uint32_t r = atomicAdd(&cnt[(uint32_t)(v >> 32) & (NF - 1)], 1u);
+    ents[s + r] = (uint32_t)v;
+  }
 }
 
 // ---------------------------------------------------------------- buckets
 // Lane = segment (w, j): buckets of magnitude j*G + 1 .. j*G + G. Running sums from
 // the top bucket: T = sum of the segment's buckets, V = sum (m - j*G) * B_m.
-// The window's sum is then sum_j (V_j + j*G * T_j) (k_bv_reduce).
+// The window's sum is then sum_j (V_j + j*G * T_j) (k_bv_reduce). Windows are laid
+// out high-first in the grid (window 15's buckets hold twice the entries), and each
+// point is loaded one add ahead.
 __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ ents, uint4* __restrict__ segV,
                                                    uint4* __restrict__ segT) {
-  const uint32_t sidx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sidx >= (uint32_t)BV_NSEG) return;
+  const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lin >= (uint32_t)BV_NSEG) return;
+  const uint32_t sidx = (uint32_t)(BV_NW - 1 - lin / BV_SEGW) * BV_SEGW + lin % BV_SEGW;
   const uint32_t key0 = sidx * BV_G;  // == w * NB + j * G
   p3 T, S;
   p3_identity(T);
   p3_identity(S);
+  // entries are consumed from the segment's end (top bucket) down, one load ahead
+  const uint32_t e_lo = offs[key0], e_hi = offs[key0 + BV_G];
+  uint32_t e = e_hi;
+  uint4 q[7];
+  uint32_t ent = 0;
+  if (e > e_lo) {
+    e--;
+    ent = ents[e];
+    const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+#pragma unroll
+    for (int i = 0; i < 7; i++) q[i] = p[i];
+  }
   for (int b = BV_G - 1; b >= 0; b--) {
-    const uint32_t e0 = offs[key0 + b], e1 = offs[key0 + b + 1];
-    uint32_t e = e0;
-    uint32_t ent = e < e1 ? ents[e] : 0u;
-    while (e < e1) {
+    const uint32_t b0 = offs[key0 + b];
+    const uint32_t b1 = b == BV_G - 1 ? e_hi : offs[key0 + b + 1];
+    for (uint32_t k = b1; k > b0; k--) {
       precomp pc;
-      pt_load(pc, pts, ent >> 1);
+      quads_to_precomp(pc, q);
       const bool neg = ent & 1u;
-      e++;
-      if (e < e1) ent = ents[e];  // next index ahead of the add
+      if (e > e_lo) {  // next point in flight during this add
+        e--;
+        ent = ents[e];
+        const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+#pragma unroll
+        for (int i = 0; i < 7; i++) q[i] = p[i];
+      }
       precomp_cneg(pc, neg);
       p1p1 t;
       p3_add_precomp(t, T, pc);
@@ -452,7 +523,7 @@ namespace mvk {
 namespace {
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BatchLayout {
-  size_t pts, scal, counts, offs, cursor, btot, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
+  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
   explicit BatchLayout(uint32_t n) {
     using namespace mv;
     const size_t nblk = (n + 255) / 256;
@@ -460,10 +531,12 @@ struct BatchLayout {
     auto take = [&](size_t bytes) { size_t r = o; o += align256(bytes); return r; };
     pts = take((size_t)2 * n * PT_QUADS * 16);
     scal = take((size_t)n * SC_QUADS * 16);
-    counts = take((size_t)BV_NK * 4);
+    pcount = take(nblk * BV_NPART * 4);
+    poff = take(nblk * BV_NPART * 4);
+    ptot = take((size_t)BV_NPART * 4);
+    pstart = take((size_t)(BV_NPART + 1) * 4);
+    tmp = take((size_t)(BV_NWR + BV_NW) * n * 8);
     offs = take((size_t)(BV_NK + 1) * 4);
-    cursor = take((size_t)BV_NK * 4);
-    btot = take((size_t)SCAN_BLOCKS * 4);
     ents = take((size_t)(BV_NWR + BV_NW) * n * 4);
     segV = take((size_t)BV_NSEG * P3_QUADS * 16);
     segT = take((size_t)BV_NSEG * P3_QUADS * 16);
@@ -487,10 +560,12 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   char* base = static_cast<char*>(bscratch);
   uint4* pts = (uint4*)(base + L.pts);
   uint4* scal = (uint4*)(base + L.scal);
-  uint32_t* counts = (uint32_t*)(base + L.counts);
+  uint32_t* pcount = (uint32_t*)(base + L.pcount);
+  uint32_t* poff = (uint32_t*)(base + L.poff);
+  uint32_t* ptot = (uint32_t*)(base + L.ptot);
+  uint32_t* pstart = (uint32_t*)(base + L.pstart);
+  unsigned long long* tmp = (unsigned long long*)(base + L.tmp);
   uint32_t* offs = (uint32_t*)(base + L.offs);
-  uint32_t* cursor = (uint32_t*)(base + L.cursor);
-  uint32_t* btot = (uint32_t*)(base + L.btot);
   uint32_t* ents = (uint32_t*)(base + L.ents);
   uint4* segV = (uint4*)(base + L.segV);
   uint4* segT = (uint4*)(base + L.segT);
@@ -500,21 +575,20 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   uint32_t* flag = (uint32_t*)(base + L.flag);
   if (flag_out) *flag_out = flag;
   const uint32_t nblk = (n + 255) / 256;
-  hipError_t e = hipMemsetAsync(counts, 0, (size_t)BV_NK * 4, s);
-  if (e != hipSuccess) return e;
+  hipError_t e;
   BvKey k;
   for (int i = 0; i < 10; i++) k.w[i] = key[i];
-  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, counts, bsum,
+  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, pcount, bsum,
                      status);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(SCAN_BLOCKS), dim3(256), 0, s, counts, offs, btot);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, btot, offs);
-  hipLaunchKernelGGL(k_scan_add, dim3(SCAN_BLOCKS), dim3(256), 0, s, btot, offs, cursor);
-  hipLaunchKernelGGL(k_bv_scatter, dim3(nblk), dim3(256), 0, s, scal, n, cursor, ents);
+  hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART), dim3(256), 0, s, pcount, nblk, poff, ptot);
+  hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, pstart);
+  hipLaunchKernelGGL(k_part_scatter, dim3(nblk), dim3(256), 0, s, scal, n, poff, pstart, tmp);
+  hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(256), 0, s, tmp, pstart, ents, offs);
   hipLaunchKernelGGL(k_bv_bucket, dim3(BV_NSEG / 256), dim3(256), 0, s, pts, offs, ents, segV, segT);
   const uint4* inV = segV;
   const uint4* inT = segT;
   uint32_t cnt = BV_SEGW;
-  int shift = 2;  // log2(BV_G)
+  int shift = BV_G == 4 ? 2 : (BV_G == 2 ? 1 : 0);  // log2(BV_G)
   int pp = 0;
   while (cnt > 1) {
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;

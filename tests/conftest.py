@@ -15,6 +15,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def engine():
+    # torch ships its own HIP runtime: it must initialise the device before the
+    # library's runtime does, or torch.cuda reports no devices (device-API tests
+    # hand torch-allocated HBM to the library, as bench.py does)
+    import torch
+
+    torch.cuda.init()
     import mysticeti_amd as M
 
     eng = M.Engine(devices=(0,))

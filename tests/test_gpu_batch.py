@@ -46,7 +46,7 @@ def test_valid_batches_pass_without_fallback(engine, n):
 def test_one_bad_signature_falls_back_exactly(engine):
     n = 8192
     msg, sig, pk = signed(engine, n, 1)
-    for where, byte in [(0, 5), (n - 1, 40), (4321, 63)]:
+    for where, byte in [(0, 33), (n - 1, 40), (4321, 50)]:  # s bytes: s stays < l, R decodes
         s2 = sig.copy()
         s2[where, byte] ^= 0x10
         st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, s2, pk))
