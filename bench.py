@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20, help="0 disables the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, help="batch path: streams the steps alternate over")
     ap.add_argument("--path", choices=["batch", "single"], default="batch",
                     help="batch: one combined equation per step (batch.hip) with exact fallback; "
                          "single: every signature verified alone (k_verify)")
@@ -128,44 +129,57 @@ def main():
     d_msg = torch.from_numpy(msg_h.copy()).to(dev)
     d_pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    d_status = torch.full((n,), 255, dtype=torch.uint8, device=dev)
-    # a dedicated non-default stream: the library launches on it and the HIP events
-    # below are recorded on it, so kernel_ms times exactly the verify launches
-    stream = torch.cuda.Stream(dev)
-    assert stream.cuda_stream != 0
+    # dedicated non-default streams: the library launches on them and the HIP events
+    # below are recorded on them, so kernel_ms times exactly the verify launches. The
+    # batch path alternates two streams so that one batch's latency-bound tail (window
+    # reduction, final check: a few waves) runs beside the next batch's full-chip kernels.
+    nstreams = args.streams if args.path == "batch" else 1
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    assert all(st.cuda_stream != 0 for st in streams)
+    d_status = [torch.full((n,), 255, dtype=torch.uint8, device=dev) for _ in range(nstreams)]
+    d_ok = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(nstreams)]
     torch.cuda.synchronize(dev)  # the H2D copies above ran on the default stream
-    eng.dev_sign(local_rank, d_seed, d_msg, d_pk, d_sig, stream.cuda_stream)
+    eng.dev_sign(local_rank, d_seed, d_msg, d_pk, d_sig, streams[0].cuda_stream)
     torch.cuda.synchronize(dev)
 
-    d_ok = torch.zeros(1, dtype=torch.int32, device=dev)
-    if args.path == "batch":
-        def step():
-            eng.dev_verify_batch(local_rank, d_msg, d_sig, d_pk, d_status, d_ok, stream.cuda_stream)
-    else:
-        def step():
-            eng.dev_verify(local_rank, d_msg, d_sig, d_pk, d_status, stream.cuda_stream)
+    state = {"i": 0}
+
+    def step():
+        j = state["i"] % nstreams
+        state["i"] += 1
+        if args.path == "batch":
+            eng.dev_verify_batch(local_rank, d_msg, d_sig, d_pk, d_status[j], d_ok[j], streams[j].cuda_stream)
+        else:
+            eng.dev_verify(local_rank, d_msg, d_sig, d_pk, d_status[j], streams[j].cuda_stream)
 
     for _ in range(args.warmup):
         step()
+    torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    state = {"first": True}
+    ev_side = [torch.cuda.Event() for _ in range(nstreams)]
 
     def timed_step():
-        if state["first"]:
-            ev0.record(stream)  # HIP events on the launch stream bracket the K launches
-            state["first"] = False
+        if state["i"] == args.warmup:
+            ev0.record(streams[0])  # HIP events on the launch streams bracket the K steps
+            for st in streams[1:]:
+                st.wait_event(ev0)
         step()
 
-    def sync():
+    def close_and_sync():
+        if state["i"] > args.warmup:
+            for st, ev in zip(streams[1:], ev_side[1:]):
+                ev.record(st)
+                streams[0].wait_event(ev)
+            ev1.record(streams[0])
         torch.cuda.synchronize(dev)
 
-    elapsed = timed_region(timed_step, args.steps, lambda: (ev1.record(stream) if not state["first"] else None,
-                                                            sync()), dist)
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step, on this stream
+    elapsed = timed_region(timed_step, args.steps, close_and_sync, dist)
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # device time per step on the launch streams
+    batch_ok = all(int(x.item()) == 1 for x in d_ok) if args.path == "batch" else None
 
-    status = d_status.cpu().numpy()
+    status = d_status[(args.warmup + args.steps - 1) % nstreams].cpu().numpy()
     accepted = int((status == 0).sum())
-    ok = accepted == n
+    ok = accepted == n and all((x.cpu().numpy() == 0).all() for x in d_status)
     parity = None
     if rank == 0 and n == (1 << 20):
         gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_config2.json")))
@@ -218,6 +232,8 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "correct": bool(ok),
+            "path": args.path,
+            "batch_equation_held": batch_ok,
             "parity_sha256": parity,
         }
         if cpu:

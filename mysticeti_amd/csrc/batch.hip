@@ -259,17 +259,18 @@ __global__ void __launch_bounds__(256, 2)
 //                              partition, runs ordered by chunk, ranks from LDS atomics
 //   k_fine_sort                workgroup per partition: counting sort by the low 10 key
 //                              bits in LDS -> final bucket lists and bucket offsets
+template <int NT = 256>
 MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
   const int t = threadIdx.x;
   sm[t] = v;
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
+  for (int o = 1; o < NT; o <<= 1) {
     uint32_t x = t >= o ? sm[t - o] : 0u;
     __syncthreads();
     sm[t] += x;
     __syncthreads();
   }
-  total = sm[255];
+  total = sm[NT - 1];
   const uint32_t incl = sm[t];
   __syncthreads();
   return incl - v;
@@ -326,32 +327,29 @@ __global__ void __launch_bounds__(256) k_part_scatter(const uint4* __restrict__ 
     });
   }
 }
-// block p: the partition's entries sorted by bucket into ents; offs[key] for its 1024 keys
-__global__ void __launch_bounds__(256) k_fine_sort(const unsigned long long* __restrict__ tmp,
-                                                   const uint32_t* __restrict__ pstart, uint32_t* __restrict__ ents,
-                                                   uint32_t* __restrict__ offs) {
+// block p: the partition's entries sorted by bucket into ents; offs[key] for its 1024
+// keys. 1024 threads, one bin each; the biggest partitions (window 15's, whose digits
+// stop at 2^13) are scheduled first.
+__global__ void __launch_bounds__(1024) k_fine_sort(const unsigned long long* __restrict__ tmp,
+                                                    const uint32_t* __restrict__ pstart, uint32_t* __restrict__ ents,
+                                                    uint32_t* __restrict__ offs) {
   constexpr int NF = 1 << BV_FINE_BITS;
   __shared__ uint32_t cnt[NF];
-  __shared__ uint32_t sm[256];
-  const uint32_t p = blockIdx.x;
+  __shared__ uint32_t sm[NF];
+  const uint32_t p = BV_NPART - 1 - blockIdx.x;
   const uint32_t s = pstart[p], e = pstart[p + 1];
-  for (int i = threadIdx.x; i < NF; i += 256) cnt[i] = 0;
+  cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (uint32_t i = s + threadIdx.x; i < e; i += 256) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
+  for (uint32_t i = s + threadIdx.x; i < e; i += NF) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
   __syncthreads();
-  const uint32_t c0 = cnt[4 * threadIdx.x], c1 = cnt[4 * threadIdx.x + 1], c2 = cnt[4 * threadIdx.x + 2],
-                 c3 = cnt[4 * threadIdx.x + 3];
+  const uint32_t c = cnt[threadIdx.x];
   uint32_t total;
-  const uint32_t ex = block_excl_scan256(c0 + c1 + c2 + c3, sm, total);
-  const uint32_t o0 = ex, o1 = ex + c0, o2 = o1 + c1, o3 = o2 + c2;
-  *reinterpret_cast<uint4*>(offs + (size_t)p * NF + 4 * threadIdx.x) = make_uint4(s + o0, s + o1, s + o2, s + o3);
+  const uint32_t ex = block_excl_scan256<NF>(c, sm, total);
+  offs[(size_t)p * NF + threadIdx.x] = s + ex;
   if (p == BV_NPART - 1 && threadIdx.x == 0) offs[BV_NK] = e;
-  cnt[4 * threadIdx.x] = o0;
-  cnt[4 * threadIdx.x + 1] = o1;
-  cnt[4 * threadIdx.x + 2] = o2;
-  cnt[4 * threadIdx.x + 3] = o3;
+  cnt[threadIdx.x] = ex;
   __syncthreads();
-  for (uint32_t i = s + threadIdx.x; i < e; i += 256) {
+  for (uint32_t i = s + threadIdx.x; i < e; i += NF) {
     const unsigned long long v = tmp[i];
     const uint32_t r = atomicAdd(&cnt[(uint32_t)(v >> 32) & (NF - 1)], 1u);
     ents[s + r] = (uint32_t)v;
@@ -583,7 +581,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART), dim3(256), 0, s, pcount, nblk, poff, ptot);
   hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, pstart);
   hipLaunchKernelGGL(k_part_scatter, dim3(nblk), dim3(256), 0, s, scal, n, poff, pstart, tmp);
-  hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(256), 0, s, tmp, pstart, ents, offs);
+  hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(1024), 0, s, tmp, pstart, ents, offs);
   hipLaunchKernelGGL(k_bv_bucket, dim3(BV_NSEG / 256), dim3(256), 0, s, pts, offs, ents, segV, segT);
   const uint4* inV = segV;
   const uint4* inT = segT;

@@ -74,7 +74,14 @@ struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
   DevBuf btab, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2, committee_pk;
-  DevBuf bscratch;  // batch-path scratch (batch.hip BatchLayout)
+  // batch-path scratch ring: consecutive batch calls alternate between two slots, so a
+  // batch on one stream can run while the previous one (on another stream) finishes its
+  // latency-bound tail; an event per slot orders reuse across streams
+  static constexpr int kSlots = 2;
+  DevBuf bscr[kSlots], vscr[kSlots];
+  hipEvent_t slot_done[kSlots] = {nullptr, nullptr};
+  bool slot_used[kSlots] = {false, false};
+  int next_slot = 0;
   HostBuf h_in, h_out;
   bool committee_loaded = false;
 };
@@ -135,16 +142,26 @@ mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
 
 // Enqueues the batch path (batch.hip) for n signatures on stream s.
 mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
-                        const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s, uint32_t** flag) {
-  HIPCHK(ctx, dev.bscratch.ensure(mvk::batch_scratch_bytes(n)));
-  HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(n)));
+                        const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s, uint32_t* flag_dst,
+                        bool flag_dst_host) {
+  const int slot = dev.next_slot;
+  dev.next_slot = (slot + 1) % Device::kSlots;
+  if (!dev.slot_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.slot_done[slot], hipEventDisableTiming));
+  if (dev.slot_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.slot_done[slot], 0));
+  HIPCHK(ctx, dev.bscr[slot].ensure(mvk::batch_scratch_bytes(n)));
+  HIPCHK(ctx, dev.vscr[slot].ensure(mvk::verify_scratch_bytes(n)));
   uint32_t key[10];
   memcpy(key, ctx->secret, 32);
   const uint64_t call = ctx->calls.fetch_add(1);
   key[8] = (uint32_t)call;
   key[9] = (uint32_t)(call >> 32);
-  HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscratch.p,
-                                       dev.scratch.p, d_status, s, flag));
+  uint32_t* flag = nullptr;
+  HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscr[slot].p,
+                                       dev.vscr[slot].p, d_status, s, &flag));
+  if (flag_dst)
+    HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, flag_dst_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, s));
+  HIPCHK(ctx, hipEventRecord(dev.slot_done[slot], s));
+  dev.slot_used[slot] = true;
   return MV_OK;
 }
 
@@ -210,8 +227,11 @@ void mv_destroy(mv_ctx* ctx) {
     (void)hipSetDevice(dev.id);
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
     for (DevBuf* b : {&dev.btab, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status, &dev.bytes,
-                      &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.bscratch})
+                      &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0],
+                      &dev.vscr[1]})
       b->release();
+    for (hipEvent_t ev : dev.slot_done)
+      if (ev) (void)hipEventDestroy(ev);
     dev.h_in.release();
     dev.h_out.release();
     if (dev.stream) (void)hipStreamDestroy(dev.stream);
@@ -329,13 +349,13 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
         dpk = dev.committee_pk.as<uint8_t>();
         dki = dev.keyidx.as<uint32_t>();
       }
-      uint32_t* d_flag = nullptr;
+      bool batched = false;
       uint32_t h_flag = 1;
       if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
         mv_status st = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m,
-                                     dev.status.as<uint8_t>(), dev.stream, &d_flag);
+                                     dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
         if (st != MV_OK) return st;
-        HIPCHK(ctx, hipMemcpyAsync(&h_flag, d_flag, 4, hipMemcpyDeviceToHost, dev.stream));
+        batched = true;
       } else {
         HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
         HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m, dev.btab.p,
@@ -343,7 +363,7 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
       }
       HIPCHK(ctx, hipMemcpyAsync(status + i, dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-      if (d_flag) {
+      if (batched) {
         ctx->batches++;
         if (!h_flag) ctx->fallbacks++;
       }
@@ -482,11 +502,7 @@ mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_
   if (n == 0) return MV_OK;
   HIPCHK(ctx, hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
-  uint32_t* d_flag = nullptr;
-  mv_status st = enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, &d_flag);
-  if (st != MV_OK) return st;
-  if (d_batch_ok) HIPCHK(ctx, hipMemcpyAsync(d_batch_ok, d_flag, 4, hipMemcpyDeviceToDevice, s));
-  return MV_OK;
+  return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok, false);
 }
 
 mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks) {
