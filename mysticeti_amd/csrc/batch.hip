@@ -18,10 +18,10 @@
 // Pipeline (one batch of n signatures, all on one stream):
 //   k_bv_prep     lane per signature: SHA-512 challenge, ZIP-215 decode of A and R,
 //                 z_i = BLAKE2b(secret || call || i), scalars z_i and z_i k_i mod l,
-//                 affine points (y+x, y-x, 2dxy) to HBM, bucket histogram, sum z_i s_i
+//                 affine points (y+x, y-x, 2dxy) to HBM, sum z_i s_i
 //   k_part_*, k_fine_sort   two-pass counting sort of the (bucket, point) entries
 //                 (LDS histograms and ranks; no global atomics)
-//   k_bv_bucket   lane per 2-bucket segment of a window: bucket sums and the
+//   k_bv_bucket   lane per bucket (segment of BV_G buckets) of a window: bucket sums and the
 //                 segment's running sums (V = sum (b - b0) B_b, T = sum B_b)
 //   k_bv_reduce   tree over segments (fan-in 8) of the pairs (V, T) per window
 //   k_bv_final    Horner over the 16 window sums, -[sum z s]B, [8], identity test
@@ -44,9 +44,9 @@ constexpr int BV_NB = 1 << (BV_C - 1);      // bucket magnitudes 1..2^15 per win
 constexpr int BV_NW = 16;                   // windows
 constexpr int BV_NWR = 8;                   // windows of the 127-bit R scalars
 constexpr int BV_NK = BV_NW * BV_NB;        // bucket keys, key = w * NB + |d| - 1
-constexpr int BV_G = 2;                     // buckets per segment lane
-constexpr int BV_FINE_BITS = 10;            // bucket sort: partition = key >> 10 (window +
-constexpr int BV_NPART = BV_NK >> BV_FINE_BITS;  // 5 high magnitude bits), then 1024 buckets
+constexpr int BV_G = 1;                     // buckets per segment lane
+constexpr int BV_FINE_BITS = 8;             // bucket sort: partition = key >> 8 (window +
+constexpr int BV_NPART = BV_NK >> BV_FINE_BITS;  // 7 high magnitude bits), then 256 buckets
 constexpr int BV_SEGW = BV_NB / BV_G;       // segments per window
 constexpr int BV_NSEG = BV_NW * BV_SEGW;
 constexpr int BV_FAN = 8;                   // reduction fan-in
@@ -157,12 +157,9 @@ struct BvKey {
 __global__ void __launch_bounds__(256, 2)
     k_bv_prep(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
               const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, uint4* __restrict__ pts,
-              uint4* __restrict__ scal, uint32_t* __restrict__ pcount, unsigned long long* __restrict__ bsum_part,
-              uint8_t* __restrict__ status) {
+              uint4* __restrict__ scal, unsigned long long* __restrict__ bsum_part, uint8_t* __restrict__ status) {
   __shared__ unsigned long long sbsum[BSUM_WORDS];
-  __shared__ uint32_t hist[BV_NPART];
   if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
-  for (int i = threadIdx.x; i < BV_NPART; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = gid < n;
@@ -229,8 +226,6 @@ __global__ void __launch_bounds__(256, 2)
     sc[2] = make_uint4(zk[4], zk[5], zk[6], zk[7]);
     status[gid] = !okA ? 2 : (ok ? 0 : 1);
   }
-  // this chunk's entries per partition (LDS atomics; no global atomics anywhere)
-  bv_for_digits(z, zk, [&](int w, int d, int) { atomicAdd(&hist[bv_key(w, d) >> BV_FINE_BITS], 1u); });
   // z * s (12 words, not reduced), summed per workgroup
   {
     uint64_t acc = 0;
@@ -248,16 +243,15 @@ __global__ void __launch_bounds__(256, 2)
   }
   __syncthreads();
   if (threadIdx.x < BSUM_WORDS) bsum_part[(size_t)blockIdx.x * BSUM_WORDS + threadIdx.x] = sbsum[threadIdx.x];
-  for (int i = threadIdx.x; i < BV_NPART; i += blockDim.x) pcount[(size_t)blockIdx.x * BV_NPART + i] = hist[i];
 }
 
 // ---------------------------------------------------------------- bucket sort
 // Two-pass counting sort of the (bucket key, point) entries without global atomics:
-//   k_part_scan / k_part_top   exclusive offsets of every (chunk, partition) run from the
-//                              per-chunk partition counts k_bv_prep wrote
-//   k_part_scatter             chunk = 256 signatures: entries (key, point) into their
+//   k_part_count               chunk = 1024 signatures: entries per partition (LDS)
+//   k_part_scan / k_part_top   exclusive offsets of every (chunk, partition) run
+//   k_part_scatter             per chunk: entries (key, point) into their
 //                              partition, runs ordered by chunk, ranks from LDS atomics
-//   k_fine_sort                workgroup per partition: counting sort by the low 10 key
+//   k_fine_sort                workgroup per partition: counting sort by the low 8 key
 //                              bits in LDS -> final bucket lists and bucket offsets
 template <int NT = 256>
 MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
@@ -276,47 +270,82 @@ MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
   return incl - v;
 }
 
-// block p: scan of pcount[c][p] over the nchunk chunks -> poff[c][p], ptot[p]
+constexpr int PART_CHUNK = 1024;  // signatures per k_part_count / k_part_scatter block
+
+MV_DEV void load_scalars(uint32_t z[4], uint32_t zk[8], const uint4* scal, uint32_t i) {
+  const uint4* sc = scal + (size_t)i * SC_QUADS;
+  const uint4 q0 = sc[0], q1 = sc[1], q2 = sc[2];
+  z[0] = q0.x; z[1] = q0.y; z[2] = q0.z; z[3] = q0.w;
+  zk[0] = q1.x; zk[1] = q1.y; zk[2] = q1.z; zk[3] = q1.w;
+  zk[4] = q2.x; zk[5] = q2.y; zk[6] = q2.z; zk[7] = q2.w;
+}
+// chunk c = 1024 signatures: entries per partition -> pcount[c][p] (LDS atomics only)
+__global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restrict__ scal, uint32_t n,
+                                                           uint32_t* __restrict__ pcount) {
+  __shared__ uint32_t hist[BV_NPART];
+  for (int i = threadIdx.x; i < BV_NPART; i += PART_CHUNK) hist[i] = 0;
+  __syncthreads();
+  const uint32_t gid = blockIdx.x * PART_CHUNK + threadIdx.x;
+  if (gid < n) {
+    uint32_t z[4], zk[8];
+    load_scalars(z, zk, scal, gid);
+    bv_for_digits(z, zk, [&](int w, int d, int) { atomicAdd(&hist[bv_key(w, d) >> BV_FINE_BITS], 1u); });
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < BV_NPART; i += PART_CHUNK) pcount[(size_t)blockIdx.x * BV_NPART + i] = hist[i];
+}
+// block b: partitions [64b, 64b + 64), 4 chunk groups; row reads are 256-B coalesced.
+// poff[c][p] = entries of partition p in chunks < c; ptot[p] = partition size.
 __global__ void __launch_bounds__(256) k_part_scan(const uint32_t* __restrict__ pcount, uint32_t nchunk,
                                                    uint32_t* __restrict__ poff, uint32_t* __restrict__ ptot) {
-  __shared__ uint32_t sm[256];
-  const uint32_t p = blockIdx.x;
-  const uint32_t per = (nchunk + 255) / 256;
-  const uint32_t c0 = threadIdx.x * per, c1 = min(nchunk, c0 + per);
+  __shared__ uint32_t gsum[4][64];
+  const uint32_t pl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const uint32_t p = blockIdx.x * 64 + pl;
+  const uint32_t per = (nchunk + 3) / 4;
+  const uint32_t c0 = g * per, c1 = min(nchunk, c0 + per);
   uint32_t sum = 0;
   for (uint32_t c = c0; c < c1; c++) sum += pcount[(size_t)c * BV_NPART + p];
-  uint32_t total;
-  uint32_t run = block_excl_scan256(sum, sm, total);
+  gsum[g][pl] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t k = 0; k < g; k++) run += gsum[k][pl];
   for (uint32_t c = c0; c < c1; c++) {
     const uint32_t v = pcount[(size_t)c * BV_NPART + p];
     poff[(size_t)c * BV_NPART + p] = run;
     run += v;
   }
-  if (threadIdx.x == 0) ptot[p] = total;
+  if (g == 3) ptot[p] = run;
 }
-// exclusive scan of the 512 partition totals -> pstart[0..512]
+// exclusive scan of the partition totals -> pstart[0..NPART]
 __global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ ptot, uint32_t* __restrict__ pstart) {
+  constexpr int PER = BV_NPART / 256;
   __shared__ uint32_t sm[256];
-  const uint32_t a = ptot[2 * threadIdx.x], b = ptot[2 * threadIdx.x + 1];
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    v[i] = ptot[PER * threadIdx.x + i];
+    sum += v[i];
+  }
   uint32_t total;
-  const uint32_t ex = block_excl_scan256(a + b, sm, total);
-  pstart[2 * threadIdx.x] = ex;
-  pstart[2 * threadIdx.x + 1] = ex + a;
+  uint32_t run = block_excl_scan256(sum, sm, total);
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    pstart[PER * threadIdx.x + i] = run;
+    run += v[i];
+  }
   if (threadIdx.x == 0) pstart[BV_NPART] = total;
 }
-__global__ void __launch_bounds__(256) k_part_scatter(const uint4* __restrict__ scal, uint32_t n,
-                                                      const uint32_t* __restrict__ poff,
-                                                      const uint32_t* __restrict__ pstart,
-                                                      unsigned long long* __restrict__ tmp) {
+__global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __restrict__ scal, uint32_t n,
+                                                             const uint32_t* __restrict__ poff,
+                                                             const uint32_t* __restrict__ pstart,
+                                                             unsigned long long* __restrict__ tmp) {
   __shared__ uint32_t rank[BV_NPART];
-  for (int i = threadIdx.x; i < BV_NPART; i += blockDim.x) rank[i] = 0;
+  for (int i = threadIdx.x; i < BV_NPART; i += PART_CHUNK) rank[i] = 0;
   __syncthreads();
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gid = blockIdx.x * PART_CHUNK + threadIdx.x;
   if (gid < n) {
-    const uint4* sc = scal + (size_t)gid * SC_QUADS;
-    const uint4 q0 = sc[0], q1 = sc[1], q2 = sc[2];
-    const uint32_t z[4] = {q0.x, q0.y, q0.z, q0.w};
-    const uint32_t zk[8] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    uint32_t z[4], zk[8];
+    load_scalars(z, zk, scal, gid);
     const uint32_t* po = poff + (size_t)blockIdx.x * BV_NPART;
     bv_for_digits(z, zk, [&](int w, int d, int isA) {
       const uint32_t key = bv_key(w, d);
@@ -327,10 +356,11 @@ __global__ void __launch_bounds__(256) k_part_scatter(const uint4* __restrict__ 
     });
   }
 }
-// block p: the partition's entries sorted by bucket into ents; offs[key] for its 1024
-// keys. 1024 threads, one bin each; the biggest partitions (window 15's, whose digits
-// stop at 2^13) are scheduled first.
-__global__ void __launch_bounds__(1024) k_fine_sort(const unsigned long long* __restrict__ tmp,
+// block p: the partition's entries sorted by bucket into ents; offs[key] for its 256
+// keys. One thread per bin; a partition's output window is ~64 KB, so the ranked
+// stores of the blocks in flight merge in L2. The biggest partitions (window 15's,
+// whose digits stop at 2^13) are scheduled first.
+__global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned long long* __restrict__ tmp,
                                                     const uint32_t* __restrict__ pstart, uint32_t* __restrict__ ents,
                                                     uint32_t* __restrict__ offs) {
   constexpr int NF = 1 << BV_FINE_BITS;
@@ -403,8 +433,9 @@ __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts
       p3_add_precomp(t, T, pc);
       p1p1_to_p3(T, t);
     }
-    p3_acc(S, T);
+    if (BV_G > 1) p3_acc(S, T);
   }
+  if (BV_G == 1) S = T;  // one bucket: V = T (weight 1)
   p3_store(segV, sidx, S);
   p3_store(segT, sidx, T);
 }
@@ -529,8 +560,9 @@ struct BatchLayout {
     auto take = [&](size_t bytes) { size_t r = o; o += align256(bytes); return r; };
     pts = take((size_t)2 * n * PT_QUADS * 16);
     scal = take((size_t)n * SC_QUADS * 16);
-    pcount = take(nblk * BV_NPART * 4);
-    poff = take(nblk * BV_NPART * 4);
+    const size_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
+    pcount = take(nchunk * BV_NPART * 4);
+    poff = take(nchunk * BV_NPART * 4);
     ptot = take((size_t)BV_NPART * 4);
     pstart = take((size_t)(BV_NPART + 1) * 4);
     tmp = take((size_t)(BV_NWR + BV_NW) * n * 8);
@@ -576,17 +608,19 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   hipError_t e;
   BvKey k;
   for (int i = 0; i < 10; i++) k.w[i] = key[i];
-  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, pcount, bsum,
-                     status);
-  hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART), dim3(256), 0, s, pcount, nblk, poff, ptot);
+  const uint32_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
+  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, bsum, status);
+  hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, pcount);
+  hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART / 64), dim3(256), 0, s, pcount, nchunk, poff, ptot);
   hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, pstart);
-  hipLaunchKernelGGL(k_part_scatter, dim3(nblk), dim3(256), 0, s, scal, n, poff, pstart, tmp);
-  hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(1024), 0, s, tmp, pstart, ents, offs);
+  hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, tmp);
+  hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, ents, offs);
   hipLaunchKernelGGL(k_bv_bucket, dim3(BV_NSEG / 256), dim3(256), 0, s, pts, offs, ents, segV, segT);
   const uint4* inV = segV;
   const uint4* inT = segT;
   uint32_t cnt = BV_SEGW;
   int shift = BV_G == 4 ? 2 : (BV_G == 2 ? 1 : 0);  // log2(BV_G)
+  static_assert(BV_G == 1 || BV_G == 2 || BV_G == 4, "segment size");
   int pp = 0;
   while (cnt > 1) {
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
