@@ -31,16 +31,45 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "verified StatementBlock sigs/sec (1/2/4/8 MI355X) vs host-core ed25519-consensus"
-# Algorithmic work per signature: 3,200 field multiplications x 64
-# 32x32->64 multiply-accumulates, plus one SHA-512 compression (~6,000 32-bit ops).
-W_VERIFY_MACS = 3200 * 64
+# Work accounting. Unit: one field multiplication or squaring = 64
+# 32x32->64 multiply-accumulates (SURVEY.md §8d convention), each MAC 2 full-rate issue
+# slots; hashes in 32-bit ops (SHA-512 compression ~6,000, BLAKE2b compression 2,688).
+#   reference algorithm (dalek single verify, §8d): 3,200 field ops + 1 SHA-512
+#   k_bv_prep (batch path): ZIP-215 decode of A and R = 2 x (255 sq + 23 mul), the
+#       precomp conversion included, + SHA-512 (k) + BLAKE2b (z)
+#   whole batch step: prep + 24 bucket additions x 7 field ops (+ ~2 for the tree)
+#   k_verify (single path): decode 2 x 278 + tables 126 + 32-window ladder 1,632 + 21
+FIELD_MACS = 64
 W_SHA512_OPS = 6000
+W_BLAKE2B_OPS = 2688
+F_REFERENCE = 3200
+F_PREP = 2 * (255 + 23)
+F_BATCH_STEP = F_PREP + 24 * 7 + 2
+F_SINGLE = 2 * 278 + 126 + 1632 + 21
 # Peaks: full-rate 32-bit VALU = 256 CU x 128 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md:
 # FP32 vector 157.3 TFLOPS = 2 x 78.6 T lane-ops/s); v_mad_u64_u32 issues at half that
 # rate on gfx950 (tools/microbench_valu.hip, profiles/r01_microbench_valu*.jsonl), so one
 # MAC costs 2 full-rate issue slots.
 PEAK_VALU_OPS = 256 * 128 * 2.4e9
 MAC_SLOTS = 2
+
+
+def slots(field_ops: int, hash_ops: int) -> int:
+    """Full-rate VALU issue slots for `field_ops` field multiplications plus hash ops."""
+    return field_ops * FIELD_MACS * MAC_SLOTS + hash_ops
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/), if any."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_{kernel}*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+        except (OSError, ValueError):
+            continue
+    return None, None
 
 
 def corpus_host(lo: int, n: int):
@@ -155,6 +184,9 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    if args.path == "batch":
+        eng.stage_times(reset=True)
+        eng.set_stage_timing(True)  # HIP events around every stage, on the launch streams
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev_side = [torch.cuda.Event() for _ in range(nstreams)]
 
@@ -175,6 +207,11 @@ def main():
 
     elapsed = timed_region(timed_step, args.steps, close_and_sync, dist)
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # device time per step on the launch streams
+    stage_ms = {}
+    if args.path == "batch":
+        tot, calls = eng.stage_times()
+        eng.set_stage_timing(False)
+        stage_ms = {k: v / max(calls, 1) for k, v in tot.items()}
     batch_ok = all(int(x.item()) == 1 for x in d_ok) if args.path == "batch" else None
 
     status = d_status[(args.warmup + args.steps - 1) % nstreams].cpu().numpy()
@@ -189,9 +226,18 @@ def main():
 
     total = n * world * args.steps
     value = total / elapsed
-    rate_kernel = n / (kernel_ms * 1e-3)
-    ops_per_sig = MAC_SLOTS * W_VERIFY_MACS + W_SHA512_OPS
-    achieved = rate_kernel * ops_per_sig
+    if args.path == "batch":
+        kern, kern_ms = "k_bv_prep", stage_ms["prep"]
+        w_kern = slots(F_PREP, W_SHA512_OPS + W_BLAKE2B_OPS)
+        w_step = slots(F_BATCH_STEP, W_SHA512_OPS + W_BLAKE2B_OPS)
+        kdesc = (f"{F_PREP} field ops x {FIELD_MACS} MACs x {MAC_SLOTS} slots + SHA-512 {W_SHA512_OPS} + "
+                 f"BLAKE2b {W_BLAKE2B_OPS} ops per signature")
+    else:
+        kern, kern_ms = "k_verify", kernel_ms
+        w_kern = w_step = slots(F_SINGLE, W_SHA512_OPS)
+        kdesc = f"{F_SINGLE} field ops x {FIELD_MACS} MACs x {MAC_SLOTS} slots + SHA-512 {W_SHA512_OPS} ops"
+    achieved = n / (kern_ms * 1e-3) * w_kern
+    traffic, traffic_src = pmc_traffic(kern)
 
     out = None
     if rank == 0:
@@ -226,9 +272,17 @@ def main():
                                    "block digests per GPU", "batch_per_gpu": n, "global_batch": n * world,
                        "parallelism": f"shard-per-gpu x{world}, no collective"},
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2),
-                         "unit": "TOP/s", "frac": round(achieved / PEAK_VALU_OPS, 4), "traffic": None,
-                         "kernel": "k_verify", "kernel_ms": round(kernel_ms, 4),
-                         "work_per_sig": f"{W_VERIFY_MACS} MACs x {MAC_SLOTS} slots + {W_SHA512_OPS} SHA-512 ops"},
+                         "unit": "TOP/s", "frac": round(achieved / PEAK_VALU_OPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel": kern, "kernel_ms": round(kern_ms, 4),
+                         "work_per_sig": kdesc},
+            "pipeline": {"device_ms_per_step": round(kernel_ms, 4),
+                         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()} if stage_ms else None,
+                         "achieved_TOPs": round(value / world * w_step / 1e12, 3),
+                         "frac": round(value / world * w_step / PEAK_VALU_OPS, 4),
+                         "work_per_sig_field_ops": F_BATCH_STEP if args.path == "batch" else F_SINGLE,
+                         "reference_equivalent_TOPs": round(value / world * slots(F_REFERENCE, W_SHA512_OPS) / 1e12, 3),
+                         "note": "reference_equivalent counts the dalek single-verify work (3,200 field ops, "
+                                 "SURVEY.md 8d) per verified signature; it is not a roofline fraction"},
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "correct": bool(ok),

@@ -141,6 +141,13 @@ mv_status mv_dev_ed25519_sign(mv_ctx* ctx, int device, const uint8_t* d_seed, co
 /* Host-buffer batch-path counters since mv_create: batches tried, batches whose combined
  * equation failed (and were re-verified signature by signature). */
 mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks);
+/* Batch-path stage timing: when enabled, every batch call records HIP events on its stream
+ * around its MV_NSTAGES stages (prep, sort, bucket, reduce, final, fallback).
+ * mv_stage_times waits for the recorded calls and returns the summed device ms per stage and
+ * the number of calls measured; reset != 0 clears the sums. */
+#define MV_NSTAGES 6
+mv_status mv_set_stage_timing(mv_ctx* ctx, int enable);
+mv_status mv_stage_times(mv_ctx* ctx, double* ms /* MV_NSTAGES or NULL */, uint64_t* calls, int reset);
 /* Runs field/scalar primitive `op` on n lane inputs (16 words each) -> 16 words each (host buffers). */
 mv_status mv_selftest(mv_ctx* ctx, int op, const uint32_t* in, uint32_t n, uint32_t* out);
 

@@ -39,7 +39,9 @@ EXPORTS = [
     "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
+    "mv_set_stage_timing", "mv_stage_times",
 ]
+STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback"]
 FLAG_NO_BATCH = 1
 BATCH_MIN = 4096
 
@@ -78,6 +80,8 @@ def load_library(path: str = LIB_PATH):
     lib.mv_dev_ed25519_verify.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
     lib.mv_dev_ed25519_verify_batch.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, u32, vp, vp, vp]
     lib.mv_batch_stats.argtypes = [vp, vp, vp]
+    lib.mv_set_stage_timing.argtypes = [vp, ctypes.c_int]
+    lib.mv_stage_times.argtypes = [vp, vp, vp, ctypes.c_int]
     lib.mv_dev_ed25519_sign.argtypes = [vp, ctypes.c_int, vp, vp, u32, vp, vp, vp]
     lib.mv_selftest.argtypes = [vp, ctypes.c_int, vp, u32, vp]
     lib.mv_block_preimage.argtypes = [vp, u64, vp, u64]
@@ -223,6 +227,17 @@ class Engine:
         b, f = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.lib.mv_batch_stats(self.ctx, ctypes.byref(b), ctypes.byref(f)), "mv_batch_stats")
         return b.value, f.value
+
+    def set_stage_timing(self, enable: bool = True):
+        self._check(self.lib.mv_set_stage_timing(self.ctx, 1 if enable else 0), "mv_set_stage_timing")
+
+    def stage_times(self, reset: bool = False):
+        """({stage: summed device ms}, calls) of the batch calls made with stage timing on."""
+        ms = np.zeros(len(STAGES), dtype=np.float64)
+        calls = ctypes.c_uint64()
+        self._check(self.lib.mv_stage_times(self.ctx, _p(ms), ctypes.byref(calls), 1 if reset else 0),
+                    "mv_stage_times")
+        return dict(zip(STAGES, ms.tolist())), calls.value
 
     def dev_sign(self, device: int, d_seed, d_msg, d_pk, d_sig, stream_handle: int = 0):
         n = d_seed.shape[0]

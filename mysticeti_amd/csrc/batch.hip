@@ -583,8 +583,11 @@ size_t batch_scratch_bytes(uint32_t n) { return BatchLayout(n).total; }
 
 hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                                uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
-                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out) {
+                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out,
+                               hipEvent_t* ev) {
   using namespace mv;
+  // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
+  auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
   if (n == 0) return hipSuccess;
   const BatchLayout L(n);
   char* base = static_cast<char*>(bscratch);
@@ -609,13 +612,17 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   BvKey k;
   for (int i = 0; i < 10; i++) k.w[i] = key[i];
   const uint32_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
+  mark(0);
   hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, bsum, status);
+  mark(1);
   hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, pcount);
   hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART / 64), dim3(256), 0, s, pcount, nchunk, poff, ptot);
   hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, pstart);
   hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, tmp);
   hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, ents, offs);
+  mark(2);
   hipLaunchKernelGGL(k_bv_bucket, dim3(BV_NSEG / 256), dim3(256), 0, s, pts, offs, ents, segV, segT);
+  mark(3);
   const uint4* inV = segV;
   const uint4* inT = segT;
   uint32_t cnt = BV_SEGW;
@@ -634,11 +641,15 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     shift += fan == 8 ? 3 : (fan == 4 ? 2 : 1);
     cnt = out;
   }
+  mark(4);
   hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, bsum, nblk, (const uint4*)btab, flag);
+  mark(5);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // exact fallback: re-verifies every signature iff the combination failed
-  return launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag);
+  e = launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag);
+  mark(6);
+  return e;
 }
 
 }  // namespace mvk

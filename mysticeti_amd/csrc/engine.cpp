@@ -97,6 +97,12 @@ struct mv_ctx {
   uint32_t secret[8] = {0};         // batch-path z_i PRF key (from /dev/urandom)
   std::atomic<uint64_t> calls{0};   // batch calls, the PRF's per-call input
   std::atomic<uint64_t> batches{0}, fallbacks{0};
+  // batch-path stage timing (mv_set_stage_timing): event sets of calls not yet read back
+  bool stage_timing = false;
+  std::mutex tmu;
+  std::vector<std::pair<int, std::vector<hipEvent_t>>> pending;  // (device, events)
+  double stage_ms[mvk::BATCH_STAGES] = {0};
+  uint64_t stage_calls = 0;
   bool has_committee = false;
   mvh::Committee committee;
 };
@@ -156,8 +162,17 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   key[8] = (uint32_t)call;
   key[9] = (uint32_t)(call >> 32);
   uint32_t* flag = nullptr;
+  std::vector<hipEvent_t> evs;
+  if (ctx->stage_timing) {
+    evs.assign(mvk::BATCH_STAGES + 1, nullptr);
+    for (auto& ev : evs) HIPCHK(ctx, hipEventCreate(&ev));
+  }
   HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscr[slot].p,
-                                       dev.vscr[slot].p, d_status, s, &flag));
+                                       dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data()));
+  if (!evs.empty()) {
+    std::lock_guard<std::mutex> lk(ctx->tmu);
+    ctx->pending.emplace_back(dev.id, std::move(evs));
+  }
   if (flag_dst)
     HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, flag_dst_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, s));
   HIPCHK(ctx, hipEventRecord(dev.slot_done[slot], s));
@@ -223,6 +238,7 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
 
 void mv_destroy(mv_ctx* ctx) {
   if (!ctx) return;
+  (void)mv_stage_times(ctx, nullptr, nullptr, 1);  // drain pending stage events
   for (auto& dev : ctx->devs) {
     (void)hipSetDevice(dev.id);
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
@@ -503,6 +519,39 @@ mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_
   HIPCHK(ctx, hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
   return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok, false);
+}
+
+mv_status mv_set_stage_timing(mv_ctx* ctx, int enable) {
+  if (!ctx) return MV_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->stage_timing = enable != 0;
+  return MV_OK;
+}
+
+mv_status mv_stage_times(mv_ctx* ctx, double* ms, uint64_t* calls, int reset) {
+  if (!ctx) return MV_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(ctx->tmu);
+  for (auto& pe : ctx->pending) {
+    HIPCHK(ctx, hipSetDevice(pe.first));
+    std::vector<hipEvent_t>& ev = pe.second;
+    HIPCHK(ctx, hipEventSynchronize(ev.back()));
+    for (int i = 0; i < mvk::BATCH_STAGES; i++) {
+      float t = 0;
+      HIPCHK(ctx, hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      ctx->stage_ms[i] += t;
+    }
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    ctx->stage_calls++;
+  }
+  ctx->pending.clear();
+  if (ms)
+    for (int i = 0; i < mvk::BATCH_STAGES; i++) ms[i] = ctx->stage_ms[i];
+  if (calls) *calls = ctx->stage_calls;
+  if (reset) {
+    for (double& x : ctx->stage_ms) x = 0;
+    ctx->stage_calls = 0;
+  }
+  return MV_OK;
 }
 
 mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks) {

@@ -20,9 +20,12 @@ hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint
 hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s);
 // batch.hip: random-linear-combination batch verify with exact on-device fallback.
 // key = 32-byte secret + 64-bit call counter (the z_i PRF key); *flag_out receives the
-// device address of the batch flag (1 = the combined equation held).
+// device address of the batch flag (1 = the combined equation held). ev (optional):
+// BATCH_STAGES + 1 events, recorded before the first stage and after each stage.
+constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
 size_t batch_scratch_bytes(uint32_t n);
 hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                                uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
-                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out);
+                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out,
+                               hipEvent_t* ev = nullptr);
 }  // namespace mvk

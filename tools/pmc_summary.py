@@ -1,14 +1,25 @@
 """Summarise rocprofv3 --pmc CSVs for one kernel: per-dispatch averages + derived metrics.
 
-    python tools/pmc_summary.py gpurun_out/prof_<tag> [kernel-substring]
+    python tools/pmc_summary.py gpurun_out/prof_<tag> [kernel-substring] [--json out.json]
+
+--json writes {"kernel", "hbm_bytes_per_launch", "fetch_bytes", "write_bytes", counters...}:
+HBM bytes per launch = 2 x FETCH_SIZE (gfx950 tallies 128-B requests at 64 B,
+MI355X_MICROARCH.md HBM section; Infinity-Cache hits are counted too) + WRITE_SIZE, KiB -> B.
+bench.py reads it for roofline.traffic.
 """
 import collections
 import csv
 import glob
 import sys
 
-d = sys.argv[1]
-kname = sys.argv[2] if len(sys.argv) > 2 else "k_verify"
+args = [a for a in sys.argv[1:]]
+jout = None
+if "--json" in args:
+    i = args.index("--json")
+    jout = args[i + 1]
+    del args[i:i + 2]
+d = args[0]
+kname = args[1] if len(args) > 1 else "k_verify"
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 meta = {}
 for f in sorted(glob.glob(f"{d}/pmc*/run_counter_collection.csv")):
@@ -24,7 +35,7 @@ print("#", meta)
 for c in sorted(avg):
     print(f"{c:28s} {avg[c]:.4e}")
 dur = None
-for f in glob.glob(f"{d}/trace/*kernel_stats.csv"):
+for f in glob.glob(f"{d}/trace1/*kernel_stats.csv") or glob.glob(f"{d}/trace/*kernel_stats.csv"):
     for r in csv.DictReader(open(f)):
         if kname in r["Name"]:
             dur = float(r["AverageNs"]) * 1e-9
@@ -48,3 +59,12 @@ if dur:
         print(f"{'fetch_GBps (x2 gfx950 corr)':28s} {2 * avg['FETCH_SIZE'] * 1024 / dur / 1e9:.1f}")
     if "WRITE_SIZE" in avg:
         print(f"{'write_GBps':28s} {avg['WRITE_SIZE'] * 1024 / dur / 1e9:.1f}")
+
+if jout:
+    import json
+
+    fetch = 2 * avg["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in avg else None
+    write = avg["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in avg else None
+    out = {"kernel": kname, "source": d, "hbm_bytes_per_launch": (fetch or 0) + (write or 0) if fetch is not None else None,
+           "fetch_bytes": fetch, "write_bytes": write, "meta": meta, "counters": avg}
+    json.dump(out, open(jout, "w"), indent=1)
