@@ -154,7 +154,15 @@ struct BvKey {
   uint32_t w[10];  // 32-byte secret, 64-bit call counter
 };
 
-__global__ void __launch_bounds__(256, 2)
+// one decode at a time at 3 waves/SIMD beat two decodes in lock-step at 2 (seq3 vs
+// x2 A/B on MI355X: 241 vs 220 M verifies/s for the whole batch path)
+#ifndef MV_PREP_X2
+#define MV_PREP_SEQ
+#endif
+#ifndef MV_PREP_OCC
+#define MV_PREP_OCC 3
+#endif
+__global__ void __launch_bounds__(256, MV_PREP_OCC)
     k_bv_prep(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
               const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, uint4* __restrict__ pts,
               uint4* __restrict__ scal, unsigned long long* __restrict__ bsum_part, uint8_t* __restrict__ status) {
@@ -171,26 +179,22 @@ __global__ void __launch_bounds__(256, 2)
   load8(sw, sig + 64 * (size_t)idx + 32);
   load8(mw, msg + 32 * (size_t)idx);
   const bool s_ok = sc_is_canonical(sw);
-  uint32_t k[8];
+  // scalars first (cheap, and their inputs die before the long decode):
+  // k = SHA-512(R || A || M) mod l, z = BLAKE2b(secret || call || i) < 2^127, z k mod l
+  uint32_t z[4], zk[8];
   {
-    uint32_t kin[24], h[16];
+    uint32_t k[8];
+    {
+      uint32_t kin[24], h[16];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      kin[i] = rw[i];
-      kin[8 + i] = aw[i];
-      kin[16 + i] = mw[i];
+      for (int i = 0; i < 8; i++) {
+        kin[i] = rw[i];
+        kin[8 + i] = aw[i];
+        kin[16 + i] = mw[i];
+      }
+      sha512_short(h, kin, 96);
+      sc_reduce512(k, h);
     }
-    sha512_short(h, kin, 96);
-    sc_reduce512(k, h);
-  }
-  p3 A, R;
-  bool okA, okR;
-  decompress_x2(A, okA, aw, R, okR, rw);
-  const bool ok = live && okA && okR && s_ok;
-
-  // z = first 128 bits of BLAKE2b-256(secret || call || i)
-  uint32_t z[4];
-  {
     uint64_t m[16], h[8];
 #pragma unroll
     for (int i = 0; i < 5; i++) m[i] = (uint64_t)key.w[2 * i] | ((uint64_t)key.w[2 * i + 1] << 32);
@@ -203,28 +207,60 @@ __global__ void __launch_bounds__(256, 2)
     z[1] = (uint32_t)(h[0] >> 32);
     z[2] = (uint32_t)h[1];
     z[3] = (uint32_t)(h[1] >> 32) & 0x7fffffffu;  // z < 2^127
-  }
+    uint32_t z8[8], zero[8];
 #pragma unroll
-  for (int i = 0; i < 4; i++) z[i] = ok ? z[i] : 0u;
-  uint32_t zk[8], z8[8], zero[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    z8[i] = i < 4 ? z[i] : 0u;
-    zero[i] = 0;
+    for (int i = 0; i < 8; i++) {
+      z8[i] = i < 4 ? z[i] : 0u;
+      zero[i] = 0;
+    }
+    sc_muladd(zk, z8, k, zero);
   }
-  sc_muladd(zk, z8, k, zero);  // z * k mod l (0 when !ok)
-
+  uint4* sc = scal + (size_t)idx * SC_QUADS;
   if (live) {
-    precomp pc;
-    precomp_from_affine(pc, R);
-    pt_store(pts, gid, pc);
-    precomp_from_affine(pc, A);
-    pt_store(pts, (size_t)n + gid, pc);
-    uint4* sc = scal + (size_t)gid * SC_QUADS;
     sc[0] = make_uint4(z[0], z[1], z[2], z[3]);
     sc[1] = make_uint4(zk[0], zk[1], zk[2], zk[3]);
     sc[2] = make_uint4(zk[4], zk[5], zk[6], zk[7]);
+  }
+
+  bool okA, okR;
+  {
+    precomp pc;
+#ifdef MV_PREP_SEQ  // experiment: one decode at a time (fewer registers, more waves)
+    p3 P;
+    decompress1(P, okR, rw);
+    precomp_from_affine(pc, P);
+    if (live) pt_store(pts, gid, pc);
+    decompress1(P, okA, aw);
+    precomp_from_affine(pc, P);
+    if (live) pt_store(pts, (size_t)n + gid, pc);
+#else
+    p3 A, R;
+    decompress_x2(A, okA, aw, R, okR, rw);
+    precomp_from_affine(pc, R);
+    if (live) pt_store(pts, gid, pc);
+    precomp_from_affine(pc, A);
+    if (live) pt_store(pts, (size_t)n + gid, pc);
+#endif
+  }
+  const bool ok = live && okA && okR && s_ok;
+  if (live) {
+    if (!ok) {  // excluded from the combination: no bucket entries
+      const uint4 zq = make_uint4(0, 0, 0, 0);
+      sc[0] = zq;
+      sc[1] = zq;
+      sc[2] = zq;
+    }
     status[gid] = !okA ? 2 : (ok ? 0 : 1);
+  }
+  // z and s were stored / are in HBM: reload them rather than hold 12 registers
+  // across the decode
+  {
+    const uint4 q = sc[0];
+    z[0] = ok ? q.x : 0u;
+    z[1] = ok ? q.y : 0u;
+    z[2] = ok ? q.z : 0u;
+    z[3] = ok ? q.w : 0u;
+    load8(sw, sig + 64 * (size_t)idx + 32);
   }
   // z * s (12 words, not reduced), summed per workgroup
   {

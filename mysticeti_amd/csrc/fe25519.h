@@ -90,7 +90,10 @@ MV_DEV void fe_reduce_scan(fe& r, Col col) {
   for (int k = 0; k < 9; k++) lo[k] = col(k);
 #pragma unroll
   for (int k = 9; k < 17; k++) {
-    const uint64_t c = col(k);
+    uint64_t c = col(k);
+    // opaque: keeps the column one 64-bit MAD chain (otherwise the compiler may also
+    // rebuild its low half from v_mul_lo_u32 products for the L * 1216 term)
+    asm("" : "+v"(c));
     lo[k - 9] += (uint64_t)(uint32_t)c * R261;
     lo[k - 8] += (uint64_t)(uint32_t)(c >> 32) * (8 * R261);
   }

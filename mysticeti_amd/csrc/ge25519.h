@@ -211,4 +211,25 @@ MV_DEV void decompress_x2(p3& A, bool& okA, const uint32_t ea[8], p3& R, bool& o
   R.X = xr; R.Y = yr; fe_set(R.Z, 1); fe_mul(R.T, xr, yr);
 }
 
+// One ZIP-215 decompression (single exponentiation chain: about half the registers of
+// decompress_x2, for kernels that trade its ILP for occupancy).
+MV_DEV void decompress1(p3& A, bool& okA, const uint32_t ea[8]) {
+  fe d, one, ya, ua, va, t, v3a, ea7, pa, xa, n;
+  fe_const(d, K_D);
+  fe_set(one, 1);
+  fe_from_words(ya, ea);
+  fe_sq(t, ya);
+  fe_sub(ua, t, one);
+  fe_mul(va, t, d);
+  fe_add(va, va, one);
+  fe_sq(t, va); fe_mul(v3a, t, va);
+  fe_sq(t, v3a); fe_mul(ea7, t, va); fe_mul(ea7, ea7, ua);
+  fe_pow_p58(pa, ea7);
+  fe_mul(pa, pa, v3a); fe_mul(pa, pa, ua);
+  okA = sqrt_ratio_finish(xa, ua, va, pa);
+  fe_neg(n, xa);
+  fe_cmov(xa, n, (ea[7] >> 31) != 0);
+  A.X = xa; A.Y = ya; fe_set(A.Z, 1); fe_mul(A.T, xa, ya);
+}
+
 }  // namespace mv
