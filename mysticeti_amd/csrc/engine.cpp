@@ -455,9 +455,16 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
       HIPCHK(ctx, dev.sig.ensure(64 * (size_t)m));
       HIPCHK(ctx, dev.keyidx.ensure(4 * (size_t)m));
       HIPCHK(ctx, dev.status.ensure(m));
-      HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
       std::vector<uint8_t> sigs(64 * (size_t)m);
-      for (uint32_t k = 0; k < m; k++) memcpy(&sigs[64 * (size_t)k], facts[k].signature, 64);
+      for (uint32_t k = 0; k < m; k++) {
+        const mvh::BlockFacts& f = facts[k];
+        memcpy(&sigs[64 * (size_t)k], f.signature, 64);
+        // the verdict of a block that fails a check ahead of the signature one does not
+        // depend on its signature: s = 2^256 - 1 (>= l) takes it out of the batch
+        // equation (rejected up front) instead of failing the whole batch
+        if (!f.parsed || f.epoch != com.epoch || f.author >= com.size() || f.round == 0)
+          memset(&sigs[64 * (size_t)k + 32], 0xff, 32);
+      }
       HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, st, pos, hipMemcpyHostToDevice, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(dev.off.p, soff.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(dev.len.p, slen.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
@@ -466,14 +473,29 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
       // msg digests stay on the device and feed the verify kernel directly
       HIPCHK(ctx, mvk::launch_block_hash(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
                                          dev.msg.as<uint8_t>(), dev.out2.as<uint8_t>(), dev.stream));
-      HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dev.committee_pk.as<uint8_t>(),
-                                     dev.keyidx.as<uint32_t>(), m, dev.btab.p, dev.scratch.p,
-                                     dev.status.as<uint8_t>(), dev.stream));
+      bool batched = false;
+      uint32_t h_flag = 1;
+      if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
+        mv_status st = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
+                                     dev.committee_pk.as<uint8_t>(), dev.keyidx.as<uint32_t>(), m,
+                                     dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
+        if (st != MV_OK) return st;
+        batched = true;
+      } else {
+        HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
+        HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dev.committee_pk.as<uint8_t>(),
+                                       dev.keyidx.as<uint32_t>(), m, dev.btab.p, dev.scratch.p,
+                                       dev.status.as<uint8_t>(), dev.stream));
+      }
       std::vector<uint8_t> md(32 * (size_t)m), bd(32 * (size_t)m), ss(m);
       HIPCHK(ctx, hipMemcpyAsync(md.data(), dev.msg.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(bd.data(), dev.out2.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(ss.data(), dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
+      if (batched) {
+        ctx->batches++;
+        if (!h_flag) ctx->fallbacks++;
+      }
       for (uint32_t k = 0; k < m; k++) {
         status[i + k] = mvh::block_verdict(facts[k], com, &bd[32 * (size_t)k], ss[k]);
         if (msg_digest) memcpy(msg_digest + 32 * (i + k), &md[32 * (size_t)k], 32);

@@ -83,3 +83,25 @@ def test_mixed_lengths_and_failures(engine):
         if ost != 1:
             assert md[i].tobytes() == omd and bd[i].tobytes() == obd, i
     assert len({int(s) for s in st}) >= 3
+
+
+def test_edge_blocks_through_batch_path(engine, golden):
+    """>= MV_BATCH_MIN blocks take the batch path: the edge cases tiled 200x keep their
+    statuses. Blocks rejected ahead of the signature check (parse error, epoch, unknown
+    author, genesis) are taken out of the combined equation, so without the one bad
+    signature the batch passes with no fallback; with it, the fallback is exact."""
+    import mysticeti_amd as M
+
+    e = golden("block_edge.json")
+    pks, stakes, epoch = committee_arrays(e["committee"])
+    engine.set_committee(pks, stakes, epoch)
+    for drop_bad_sig in (True, False):
+        cases = [c for c in e["cases"] if not (drop_bad_sig and c["note"].startswith("bad signature"))]
+        reps = M.BATCH_MIN // len(cases) + 1
+        blocks = [bytes.fromhex(c["bincode"]) for c in cases] * reps
+        b0, f0 = engine.batch_stats()
+        st, md, bd = engine.verify_blocks(blocks)
+        b1, f1 = engine.batch_stats()
+        assert [int(x) for x in st] == [c["status"] for c in cases] * reps
+        assert b1 - b0 == 1
+        assert f1 - f0 == (0 if drop_bad_sig else 1)
