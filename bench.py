@@ -131,7 +131,16 @@ def main():
     ap.add_argument("--path", choices=["batch", "single"], default="batch",
                     help="batch: one combined equation per step (batch.hip) with exact fallback; "
                          "single: every signature verified alone (k_verify)")
+    ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
+                    help="config2 (default, the headline line): 1M independent signatures per GPU; "
+                         "config4: HBM-resident 100-validator blocks through the device block pipeline; "
+                         "config5: p50/p99 latency of 64-block batches, GPU vs host cores")
+    ap.add_argument("--batches", type=int, default=10000, help="config5: GPU batches timed per shape")
     args = ap.parse_args()
+    if args.workload != "config2":
+        import bench_blocks
+
+        return bench_blocks.run(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,7 +220,7 @@ def main():
     if args.path == "batch":
         tot, calls = eng.stage_times()
         eng.set_stage_timing(False)
-        stage_ms = {k: v / max(calls, 1) for k, v in tot.items()}
+        stage_ms = {k: v / calls[k] for k, v in tot.items() if calls[k]}
     batch_ok = all(int(x.item()) == 1 for x in d_ok) if args.path == "batch" else None
 
     status = d_status[(args.warmup + args.steps - 1) % nstreams].cpu().numpy()

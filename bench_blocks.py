@@ -1,0 +1,263 @@
+"""Block-path benchmarks behind `bench.py --workload config4|config5` (BASELINE.json configs 4, 5).
+
+config4  Throughput of whole-block verification (StatementBlock::verify, types.rs:315-376) on
+         config-4-shaped blocks: 100-validator committee, 67 includes, one 512-B Share tx,
+         66 VoteRanges (pre-image ~8,060 B, bincode ~9.5 KB). The bincode of `--batch` blocks
+         per GPU is resident in HBM (a 4,100-block corpus signed on the GPU, replicated on the
+         device); one step = one mv_dev_verify_blocks pass over it: device bincode parse ->
+         pre-image -> 2 x BLAKE2b-256 (shared prefix) -> SHA-512 -> batch ZIP-215 verify ->
+         verdicts. N > 1: one process per GPU, each with its own shard (weak scaling, no
+         collective on the data path), as bench.py.
+config5  Latency of 64-block batches (the online path: one message of blocks from the block
+         handler, net_sync.rs:314-386): submit -> verdicts through mv_verify_blocks on host
+         buffers (PCIe both ways), p50/p99 over --batches batches, for config-1 and config-4
+         shaped blocks; beside the oracle's StatementBlock::verify on 1 host core (the
+         reference's sequential loop) and on 16 host threads.
+The CPU legs time oracle/block.c (the checker; -O3 -march=native on the box), the only use
+of oracle/ here.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+METRIC = "verified StatementBlock sigs/sec (1/2/4/8 MI355X) vs host-core ed25519-consensus"
+PEAK_VALU_OPS = 256 * 128 * 2.4e9  # full-rate 32-bit VALU lane-ops/s (bench.py)
+W_BLAKE2B_OPS = 2688               # 32-bit ops per BLAKE2b compression
+CPU_THREADS = 16                   # the box's CPU share
+
+
+def _oracle_native():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-s", "native"], check=True)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libmv_oracle_native.so"))
+    vp = ctypes.c_void_p
+    lib.orc_block_verify_batch.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_uint32, ctypes.c_uint64,
+                                           vp, vp, vp, ctypes.c_int]
+    return lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _cpu_blocks(lib, buf, off, ln, pks, stakes, threads):
+    st = np.zeros(off.shape[0], dtype=np.uint8)
+    lib.orc_block_verify_batch(_p(buf), _p(off), _p(ln), off.shape[0], _p(pks), _p(stakes), pks.shape[0], 0,
+                               _p(st), None, None, threads)
+    return st
+
+
+def _host_cpu():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def _pct(lat, q):
+    return round(float(np.percentile(np.asarray(lat) * 1e6, q)), 1)
+
+
+def _lat_summary(lat):
+    return {"p50_us": _pct(lat, 50), "p99_us": _pct(lat, 99), "mean_us": round(float(np.mean(lat)) * 1e6, 1),
+            "batches": len(lat)}
+
+
+def run(args) -> int:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+    sys.path.insert(0, ROOT)
+    import mysticeti_amd as M
+
+    eng = M.Engine(devices=(local_rank,))
+    try:
+        if args.workload == "config5":
+            return config5(args, eng, rank)
+        return config4(args, eng, torch, local_rank, rank, world, dist)
+    finally:
+        eng.close()
+        if dist:
+            dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ config 5 (latency)
+def config5(args, eng, rank) -> int:
+    import mysticeti_amd.blocks as MB
+
+    lib = _oracle_native() if args.cpu_sample > 0 else None
+    out = {"metric": "config5: 64-block batch verify latency, submit -> verdicts (mv_verify_blocks, host buffers)",
+           "unit": "us", "higher_is_better": False, "n_gpus": 1, "data": "synthetic (blocks signed on the GPU)",
+           "host_cpu": _host_cpu(), "shapes": {}}
+    ok = True
+    for shape in ("config1", "config4"):
+        if shape == "config1":
+            blocks = MB.config1(eng, rounds=64)
+            pks, stakes = MB.committee(eng, 4, distinct=False)
+        else:
+            blocks = MB.config4(eng, rounds=4)
+            pks, stakes = MB.committee(eng, 100, distinct=True)
+        eng.set_committee(pks, stakes, 0)
+        batches = [MB.pack(blocks[i:i + 64]) for i in range(0, len(blocks) - 63, 64)]
+        for b in batches:  # warm-up + correctness
+            st, _, _ = eng.verify_blocks_packed(*b)
+            ok &= bool((st == 0).all())
+        lat = []
+        for it in range(args.batches):
+            b = batches[it % len(batches)]
+            t0 = time.perf_counter()
+            eng.verify_blocks_packed(*b)
+            lat.append(time.perf_counter() - t0)
+        res = {"gpu": _lat_summary(lat), "bincode_bytes_per_block": int(batches[0][2].mean())}
+        if lib is not None:
+            for threads, nb in ((1, 100 if shape == "config4" else 300), (CPU_THREADS, 1500)):
+                clat = []
+                for it in range(nb):
+                    buf, off, ln = batches[it % len(batches)]
+                    t0 = time.perf_counter()
+                    st = _cpu_blocks(lib, buf, off, ln, pks, stakes, threads)
+                    clat.append(time.perf_counter() - t0)
+                    ok &= bool((st == 0).all())
+                res[f"cpu_{threads}t"] = _lat_summary(clat)
+            res["gpu_vs_cpu_p50"] = {k: round(res[k]["p50_us"] / res["gpu"]["p50_us"], 2)
+                                     for k in res if k.startswith("cpu_")}
+        out["shapes"][shape] = res
+    out["correct"] = ok
+    out["note"] = ("GPU: host parse-free path (raw bincode H2D, device parse/hash/verify, verdicts D2H), "
+                   "64 blocks < MV_BATCH_MIN so signatures take the committee comb tables (comb.hip); "
+                   "CPU: oracle/block.c StatementBlock::verify (threads spawned per batch)")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    return 0 if ok else 1
+
+
+# ------------------------------------------------------------------ config 4 (throughput)
+def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
+    import mysticeti_amd.blocks as MB
+    from mysticeti_amd.dist import all_ranks_ok, timed_region
+
+    dev = torch.device("cuda", local_rank)
+    rounds = 41
+    base = MB.config4(eng, rounds=rounds)  # 4,100 distinct blocks
+    pks, stakes = MB.committee(eng, 100, distinct=True)
+    eng.set_committee(pks, stakes, 0)
+    buf, off, ln = MB.pack(base)
+    nb = len(base)
+    base_bytes = int(off[-1] + ln[-1])
+    span = (base_bytes + 7) & ~7
+    n = args.batch
+    reps = (n + nb - 1) // nb
+    host = np.zeros(span, dtype=np.uint8)
+    host[:base_bytes] = buf[:base_bytes]
+    d_base = torch.from_numpy(host).to(dev)
+    d_buf = torch.zeros(reps * span + 64, dtype=torch.uint8, device=dev)
+    d_buf[: reps * span].view(reps, span).copy_(d_base.unsqueeze(0).expand(reps, span))
+    off_all = (np.arange(reps, dtype=np.int64)[:, None] * span + off.astype(np.int64)[None, :]).reshape(-1)[:n]
+    len_all = np.tile(ln.astype(np.int64), reps)[:n]
+    d_off = torch.from_numpy(off_all).to(dev)
+    d_len = torch.from_numpy(len_all).to(dev)
+    buf_bytes = reps * span
+    nstreams = max(1, args.streams)
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    d_st = [torch.full((n,), 255, dtype=torch.uint8, device=dev) for _ in range(nstreams)]
+    d_md = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(nstreams)]
+    d_bd = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(nstreams)]
+    torch.cuda.synchronize(dev)
+    state = {"i": 0}
+
+    def step():
+        j = state["i"] % nstreams
+        state["i"] += 1
+        eng.dev_verify_blocks(local_rank, d_buf, buf_bytes, d_off, d_len, d_st[j], d_md[j], d_bd[j],
+                              streams[j].cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.stage_times(reset=True)
+    eng.set_stage_timing(True)
+    elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
+    tot, calls = eng.stage_times()
+    eng.set_stage_timing(False)
+    stage_ms = {k: round(v / calls[k], 4) for k, v in tot.items() if calls[k]}
+    ok = all(bool((x.cpu().numpy() == 0).all()) for x in d_st)
+    # block digests = the digests the blocks claim (bincode bytes 24..56), bit-exact
+    bd = d_bd[0][:nb].cpu().numpy()
+    claimed = np.stack([np.frombuffer(b[24:56], dtype=np.uint8) for b in base])
+    ok &= bool((bd == claimed).all())
+    msg_ok = hashlib.sha256(d_md[0][:nb].cpu().numpy().tobytes()).hexdigest()
+    ok = all_ranks_ok(ok, dist)
+    value = n * world * args.steps / elapsed
+    L = int(np.mean([len(b) for b in base]))  # bincode length
+    import mysticeti_amd as M
+
+    pre_len = len(M.block_preimage(base[0]))  # the host codec (block_codec.cpp)
+    # shared prefix: (L-1)//128 compressions, then 1 final for B2(P) and the rest of B2(P || sig)
+    comp_exec = (pre_len + 64 - 1) // 128 + 2
+    comp_alg = -(-pre_len // 128) + -(-(pre_len + 64) // 128)
+    hash_ms = stage_ms.get("hash")
+    out = None
+    if rank == 0:
+        cpu = None
+        if args.cpu_sample > 0:
+            lib = _oracle_native()
+            res = {}
+            for threads, seconds in ((1, 4.0), (CPU_THREADS, 8.0)):
+                done, t0 = 0, time.perf_counter()
+                sub = nb if threads > 1 else 400
+                o2, l2 = off[:sub].copy(), ln[:sub].copy()
+                while time.perf_counter() - t0 < seconds:
+                    st = _cpu_blocks(lib, buf, o2, l2, pks, stakes, threads)
+                    ok &= bool((st == 0).all())
+                    done += sub
+                res[threads] = (done / (time.perf_counter() - t0), done)
+            cpu = {"value": round(res[CPU_THREADS][0], 1), "unit": "blocks/s", "cores": CPU_THREADS, "kind": "port",
+                   "sample": f"{res[CPU_THREADS][1]} config-4 blocks on {CPU_THREADS} threads; single core: "
+                             f"{res[1][1]} blocks", "single_core_value": round(res[1][0], 1),
+                   "host_cpu": _host_cpu(), "nproc": os.cpu_count(),
+                   "impl": "oracle/block.c StatementBlock::verify (parse, 2 x BLAKE2b, ZIP-215 verify), gcc -O3 "
+                           "-march=native"}
+        roof = None
+        if hash_ms:
+            ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
+            roof = {"bound": "valu", "kernel": "k_block_hash", "kernel_ms": hash_ms,
+                    "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
+                    "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": None,
+                    "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
+                                      f"algorithmic) x {W_BLAKE2B_OPS} ops"}
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "blocks/s (= verified block signatures/s)",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "u32",
+               "data": f"synthetic config-4 blocks ({nb} distinct, signed on the GPU, replicated in HBM)",
+               "config": {"workload": "config4: 100-validator blocks, 67 includes, 512-B tx, 66 VoteRanges, "
+                                      "HBM-resident bincode, device parse + verify", "blocks_per_gpu": n,
+                          "bincode_bytes_per_block": L, "preimage_bytes": pre_len,
+                          "parallelism": f"shard-per-gpu x{world}, no collective"},
+               "roofline": roof, "pipeline": {"stage_ms": stage_ms,
+                                              "hbm_bincode_GBps": round(n * L / (elapsed / args.steps) / 1e9, 1)},
+               "cpu_baseline": cpu, "correct": bool(ok), "sha256_msg_digests_first_corpus": msg_ok}
+        if cpu:
+            out["speedup_vs_cpu"] = {"all_cores": round(value / world / cpu["value"], 1),
+                                     "single_core": round(value / world / cpu["single_core_value"], 1)}
+        print(json.dumps(out), flush=True)
+    return 0 if ok else 1

@@ -71,6 +71,8 @@ typedef int32_t mv_status;
 
 /* mv_config.flags */
 #define MV_FLAG_NO_BATCH 1u /* host-buffer verify: never use the batch (random linear combination) path */
+#define MV_FLAG_NO_COMB 2u  /* committee-key verifies: never use the per-key comb tables (ladder per signature) */
+#define MV_FLAG_HOST_PARSE 4u /* mv_verify_blocks: parse the bincode on the host (block_codec.cpp), not on the GPU */
 
 /* Host-buffer verify calls of at least this many signatures per device take the batch path
  * (one combined equation + exact fallback); smaller ones verify every signature alone. */
@@ -136,18 +138,30 @@ mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_
                                       uint8_t* d_status, uint32_t* d_batch_ok, void* stream);
 mv_status mv_dev_ed25519_sign(mv_ctx* ctx, int device, const uint8_t* d_seed, const uint8_t* d_msg, uint32_t n,
                               uint8_t* d_pk, uint8_t* d_sig, void* stream);
+/* StatementBlock::verify on n bincode blocks already in HBM (Data::from_bytes + verify,
+ * data.rs:43-52, types.rs:315-376): block i is d_buf[d_off[i] .. d_off[i] + d_len[i]). The
+ * parse, the pre-image, both digests, the signature and the committee checks all run on the
+ * device; verdicts as mv_verify_blocks. d_buf is 8-byte aligned, blocks do not overlap, and
+ * 16 bytes past the end of every block are readable (pad the buffer); buf_bytes bounds the
+ * blocks' extent in d_buf. d_msg_digest / d_block_digest (n x 32, 16-byte aligned) may be NULL.
+ * Requires mv_set_committee. Enqueue only. */
+mv_status mv_dev_verify_blocks(mv_ctx* ctx, int device, const uint8_t* d_buf, uint64_t buf_bytes,
+                               const uint64_t* d_off, const uint64_t* d_len, uint32_t n, uint8_t* d_status,
+                               uint8_t* d_msg_digest, uint8_t* d_block_digest, void* stream);
 
 /* ---- diagnostics (used by the test-suite) ---- */
 /* Host-buffer batch-path counters since mv_create: batches tried, batches whose combined
  * equation failed (and were re-verified signature by signature). */
 mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks);
-/* Batch-path stage timing: when enabled, every batch call records HIP events on its stream
- * around its MV_NSTAGES stages (prep, sort, bucket, reduce, final, fallback).
+/* Stage timing: when enabled, every call records HIP events on its stream around its
+ * stages: batch path 0..5 (prep, sort, bucket, reduce, final, fallback), block pipeline
+ * 6..9 (parse, hash, verify = comb/ladder verify when the batch path is not taken, verdict).
  * mv_stage_times waits for the recorded calls and returns the summed device ms per stage and
- * the number of calls measured; reset != 0 clears the sums. */
-#define MV_NSTAGES 6
+ * the number of calls measured per stage; reset != 0 clears the sums. */
+#define MV_NSTAGES 10
 mv_status mv_set_stage_timing(mv_ctx* ctx, int enable);
-mv_status mv_stage_times(mv_ctx* ctx, double* ms /* MV_NSTAGES or NULL */, uint64_t* calls, int reset);
+mv_status mv_stage_times(mv_ctx* ctx, double* ms /* MV_NSTAGES or NULL */, uint64_t* calls /* MV_NSTAGES or NULL */,
+                         int reset);
 /* Runs field/scalar primitive `op` on n lane inputs (16 words each) -> 16 words each (host buffers). */
 mv_status mv_selftest(mv_ctx* ctx, int op, const uint32_t* in, uint32_t n, uint32_t* out);
 

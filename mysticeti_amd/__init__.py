@@ -39,10 +39,11 @@ EXPORTS = [
     "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
-    "mv_set_stage_timing", "mv_stage_times",
+    "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks",
 ]
-STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback"]
-FLAG_NO_BATCH = 1
+# batch path stages, then the block pipeline's (mv_stage_times order, MV_NSTAGES)
+STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback", "parse", "hash", "verify", "verdict"]
+FLAG_NO_BATCH, FLAG_NO_COMB, FLAG_HOST_PARSE = 1, 2, 4
 BATCH_MIN = 4096
 
 
@@ -82,6 +83,7 @@ def load_library(path: str = LIB_PATH):
     lib.mv_batch_stats.argtypes = [vp, vp, vp]
     lib.mv_set_stage_timing.argtypes = [vp, ctypes.c_int]
     lib.mv_stage_times.argtypes = [vp, vp, vp, ctypes.c_int]
+    lib.mv_dev_verify_blocks.argtypes = [vp, ctypes.c_int, vp, u64, vp, vp, u32, vp, vp, vp, vp]
     lib.mv_dev_ed25519_sign.argtypes = [vp, ctypes.c_int, vp, vp, u32, vp, vp, vp]
     lib.mv_selftest.argtypes = [vp, ctypes.c_int, vp, u32, vp]
     lib.mv_block_preimage.argtypes = [vp, u64, vp, u64]
@@ -104,13 +106,18 @@ def _u8(a, shape_tail: int) -> np.ndarray:
 class Engine:
     """One mv_ctx: the devices it shards over, their streams and buffers."""
 
-    def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0, batch: bool = True):
-        """batch=False sets MV_FLAG_NO_BATCH: host-buffer verifies check every signature alone."""
+    def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0, batch: bool = True, comb: bool = True,
+                 host_parse: bool = False):
+        """batch=False sets MV_FLAG_NO_BATCH: host-buffer verifies check every signature alone.
+        comb=False sets MV_FLAG_NO_COMB: committee keys go through the per-signature ladder,
+        not the per-key comb tables. host_parse=True sets MV_FLAG_HOST_PARSE: verify_blocks
+        parses the bincode on the host instead of on the GPU."""
         self.lib = load_library()
         mask = 0
         for d in devices:
             mask |= 1 << int(d)
-        cfg = _Config(mask, max_batch, 0 if batch else FLAG_NO_BATCH)
+        flags = (0 if batch else FLAG_NO_BATCH) | (0 if comb else FLAG_NO_COMB) | (FLAG_HOST_PARSE if host_parse else 0)
+        cfg = _Config(mask, max_batch, flags)
         h = ctypes.c_void_p()
         rc = self.lib.mv_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != MV_OK:
@@ -232,12 +239,22 @@ class Engine:
         self._check(self.lib.mv_set_stage_timing(self.ctx, 1 if enable else 0), "mv_set_stage_timing")
 
     def stage_times(self, reset: bool = False):
-        """({stage: summed device ms}, calls) of the batch calls made with stage timing on."""
+        """({stage: summed device ms}, {stage: calls measured}) since the last reset."""
         ms = np.zeros(len(STAGES), dtype=np.float64)
-        calls = ctypes.c_uint64()
-        self._check(self.lib.mv_stage_times(self.ctx, _p(ms), ctypes.byref(calls), 1 if reset else 0),
-                    "mv_stage_times")
-        return dict(zip(STAGES, ms.tolist())), calls.value
+        calls = np.zeros(len(STAGES), dtype=np.uint64)
+        self._check(self.lib.mv_stage_times(self.ctx, _p(ms), _p(calls), 1 if reset else 0), "mv_stage_times")
+        return dict(zip(STAGES, ms.tolist())), dict(zip(STAGES, (int(c) for c in calls)))
+
+    def dev_verify_blocks(self, device: int, d_buf, buf_bytes: int, d_off, d_len, d_status, d_md=None, d_bd=None,
+                          stream_handle: int = 0):
+        """StatementBlock::verify on HBM-resident bincode (torch uint8 buffer, int64 offsets and
+        lengths); parse, digests, signatures and checks on the GPU. Enqueue only."""
+        n = d_off.shape[0]
+        vp = ctypes.c_void_p
+        self._check(self.lib.mv_dev_verify_blocks(
+            self.ctx, device, vp(d_buf.data_ptr()), int(buf_bytes), vp(d_off.data_ptr()), vp(d_len.data_ptr()), n,
+            vp(d_status.data_ptr()), vp(d_md.data_ptr()) if d_md is not None else None,
+            vp(d_bd.data_ptr()) if d_bd is not None else None, vp(stream_handle or None)), "mv_dev_verify_blocks")
 
     def dev_sign(self, device: int, d_seed, d_msg, d_pk, d_sig, stream_handle: int = 0):
         n = d_seed.shape[0]

@@ -1,9 +1,10 @@
 // libmysti_verify.so: contexts, device sharding and the C ABI of include/mysti_verify.h.
 //
-// One mv_ctx owns, per HIP device: a stream, the fixed-base table [0..128]B, and
-// growable device / pinned-host buffers. Host-buffer calls split their items into
-// one contiguous shard per device and run each shard on its own host thread
-// (one stream per device, no collective: only per-item verdicts come back), in
+// One mv_ctx owns, per HIP device: a stream; the fixed-base tables ([0..128]B and
+// [0..128](2^124 B) for the ladders, the comb table C_B); the committee (keys, stakes, the
+// per-key comb tables C_A); growable device / pinned-host buffers. Host-buffer calls split
+// their items into one contiguous shard per device and run each shard on its own host
+// thread (one stream per device, no collective: only per-item verdicts come back), in
 // chunks of at most cfg.max_batch items. Calls on one ctx are serialised by a mutex.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -21,6 +22,10 @@
 #include "kernels.h"
 
 namespace {
+
+constexpr int kBlockStage0 = mvk::BATCH_STAGES;  // parse, hash, verify, verdict
+constexpr int kBlockStages = 4;
+static_assert(kBlockStage0 + kBlockStages == MV_NSTAGES, "stage count");
 
 struct DevBuf {
   void* p = nullptr;
@@ -73,17 +78,29 @@ struct HostBuf {
 struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
-  DevBuf btab, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2, committee_pk;
-  // batch-path scratch ring: consecutive batch calls alternate between two slots, so a
-  // batch on one stream can run while the previous one (on another stream) finishes its
-  // latency-bound tail; an event per slot orders reuse across streams
+  DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
+  // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
+  DevBuf committee_pk, stakes, combA, keyok;
+  // scratch rings: consecutive calls alternate between two slots, so a call on one stream
+  // can run while the previous one (on another stream) finishes its latency-bound tail; an
+  // event per slot orders reuse across streams. Batch path: bscr/vscr; blocks: blk.
   static constexpr int kSlots = 2;
   DevBuf bscr[kSlots], vscr[kSlots];
   hipEvent_t slot_done[kSlots] = {nullptr, nullptr};
   bool slot_used[kSlots] = {false, false};
   int next_slot = 0;
+  DevBuf blk[kSlots];
+  hipEvent_t blk_done[kSlots] = {nullptr, nullptr};
+  bool blk_used[kSlots] = {false, false};
+  int blk_next = 0;
   HostBuf h_in, h_out;
   bool committee_loaded = false;
+};
+
+struct PendingEvents {
+  int device;
+  int first_stage;  // stage index of events[0] -> events[1]
+  std::vector<hipEvent_t> events;
 };
 
 }  // namespace
@@ -97,12 +114,12 @@ struct mv_ctx {
   uint32_t secret[8] = {0};         // batch-path z_i PRF key (from /dev/urandom)
   std::atomic<uint64_t> calls{0};   // batch calls, the PRF's per-call input
   std::atomic<uint64_t> batches{0}, fallbacks{0};
-  // batch-path stage timing (mv_set_stage_timing): event sets of calls not yet read back
+  // stage timing (mv_set_stage_timing): event sets of calls not yet read back
   bool stage_timing = false;
   std::mutex tmu;
-  std::vector<std::pair<int, std::vector<hipEvent_t>>> pending;  // (device, events)
-  double stage_ms[mvk::BATCH_STAGES] = {0};
-  uint64_t stage_calls = 0;
+  std::vector<PendingEvents> pending;
+  double stage_ms[MV_NSTAGES] = {0};
+  uint64_t stage_calls[MV_NSTAGES] = {0};
   bool has_committee = false;
   mvh::Committee committee;
 };
@@ -131,7 +148,6 @@ mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
     return fn(ctx->devs[0], 0, n);
   }
   std::vector<mv_status> rc(nd, MV_OK);
-  std::vector<std::string> errs(nd);
   std::vector<std::thread> th;
   for (size_t d = 0; d < nd; d++) {
     uint64_t lo = n * d / nd, hi = n * (d + 1) / nd;
@@ -144,6 +160,20 @@ mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
   for (size_t d = 0; d < nd; d++)
     if (rc[d] != MV_OK) return rc[d];
   return MV_OK;
+}
+
+// count + 1 timing events (empty when stage timing is off)
+mv_status make_events(mv_ctx* ctx, int count, std::vector<hipEvent_t>& evs) {
+  evs.clear();
+  if (!ctx->stage_timing) return MV_OK;
+  evs.assign(count + 1, nullptr);
+  for (auto& ev : evs) HIPCHK(ctx, hipEventCreate(&ev));
+  return MV_OK;
+}
+void keep_events(mv_ctx* ctx, int device, int first_stage, std::vector<hipEvent_t>& evs) {
+  if (evs.empty()) return;
+  std::lock_guard<std::mutex> lk(ctx->tmu);
+  ctx->pending.push_back(PendingEvents{device, first_stage, std::move(evs)});
 }
 
 // Enqueues the batch path (batch.hip) for n signatures on stream s.
@@ -163,16 +193,11 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   key[9] = (uint32_t)(call >> 32);
   uint32_t* flag = nullptr;
   std::vector<hipEvent_t> evs;
-  if (ctx->stage_timing) {
-    evs.assign(mvk::BATCH_STAGES + 1, nullptr);
-    for (auto& ev : evs) HIPCHK(ctx, hipEventCreate(&ev));
-  }
+  mv_status st = make_events(ctx, mvk::BATCH_STAGES, evs);
+  if (st != MV_OK) return st;
   HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data()));
-  if (!evs.empty()) {
-    std::lock_guard<std::mutex> lk(ctx->tmu);
-    ctx->pending.emplace_back(dev.id, std::move(evs));
-  }
+  keep_events(ctx, dev.id, 0, evs);
   if (flag_dst)
     HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, flag_dst_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, s));
   HIPCHK(ctx, hipEventRecord(dev.slot_done[slot], s));
@@ -180,11 +205,195 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   return MV_OK;
 }
 
+// Committee-key signatures one by one: comb tables (comb.hip) or, with MV_FLAG_NO_COMB,
+// the per-signature ladder (k_verify).
+mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig,
+                                   const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s) {
+  if (!(ctx->flags & MV_FLAG_NO_COMB)) {
+    HIPCHK(ctx, mvk::launch_verify_comb(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
+                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s));
+  } else {
+    HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(n)));
+    HIPCHK(ctx, mvk::launch_verify(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.btab.p,
+                                   dev.scratch.p, d_status, s));
+  }
+  return MV_OK;
+}
+
+// The device block pipeline on stream s (enqueue only): k_block_parse -> k_block_hash ->
+// signatures (batch path for >= MV_BATCH_MIN blocks, else committee verify) ->
+// k_block_verdict. d_md / d_bd may be null (scratch then). h_flag (optional, host) receives
+// the batch flag; *batched says whether the batch path ran.
+mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
+                         const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
+                         hipStream_t s, uint32_t* h_flag, bool* batched) {
+  *batched = false;
+  if (n == 0) return MV_OK;
+  const mvh::Committee& com = ctx->committee;
+  const int slot = dev.blk_next;
+  dev.blk_next = (slot + 1) % Device::kSlots;
+  if (!dev.blk_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.blk_done[slot], hipEventDisableTiming));
+  if (dev.blk_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.blk_done[slot], 0));
+  // scratch: stage | pre_off | pre_len | sig | key_idx | facts | claimed | sig status | md | bd
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t nn = n;
+  size_t o = 0;
+  const size_t o_stage = o;
+  o += al(buf_bytes + 256);
+  const size_t o_poff = o;
+  o += al(8 * nn);
+  const size_t o_plen = o;
+  o += al(8 * nn);
+  const size_t o_sig = o;
+  o += al(64 * nn);
+  const size_t o_kidx = o;
+  o += al(4 * nn);
+  const size_t o_facts = o;
+  o += al(4 * nn);
+  const size_t o_claim = o;
+  o += al(32 * nn);
+  const size_t o_sst = o;
+  o += al(nn);
+  const size_t o_md = o;
+  o += al(32 * nn);
+  const size_t o_bd = o;
+  o += al(32 * nn);
+  HIPCHK(ctx, dev.blk[slot].ensure(o));
+  char* b = dev.blk[slot].as<char>();
+  uint8_t* stage = (uint8_t*)(b + o_stage);
+  uint64_t* poff = (uint64_t*)(b + o_poff);
+  uint64_t* plen = (uint64_t*)(b + o_plen);
+  uint8_t* sig = (uint8_t*)(b + o_sig);
+  uint32_t* kidx = (uint32_t*)(b + o_kidx);
+  uint32_t* facts = (uint32_t*)(b + o_facts);
+  uint8_t* claimed = (uint8_t*)(b + o_claim);
+  uint8_t* sst = (uint8_t*)(b + o_sst);
+  uint8_t* md = d_md ? d_md : (uint8_t*)(b + o_md);
+  uint8_t* bd = d_bd ? d_bd : (uint8_t*)(b + o_bd);
+  std::vector<hipEvent_t> evs;
+  mv_status st = make_events(ctx, kBlockStages, evs);
+  if (st != MV_OK) return st;
+  auto mark = [&](int i) -> hipError_t { return evs.empty() ? hipSuccess : hipEventRecord(evs[i], s); };
+  HIPCHK(ctx, mark(0));
+  HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
+                                      com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
+  HIPCHK(ctx, mark(1));
+  HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
+  HIPCHK(ctx, mark(2));
+  if (!(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN) {
+    st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, h_flag, h_flag != nullptr);
+    *batched = true;
+  } else {
+    st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s);
+  }
+  if (st != MV_OK) return st;
+  HIPCHK(ctx, mark(3));
+  HIPCHK(ctx, mvk::launch_block_verdict(facts, claimed, bd, sst, n, d_status, s));
+  HIPCHK(ctx, mark(4));
+  keep_events(ctx, dev.id, kBlockStage0, evs);
+  HIPCHK(ctx, hipEventRecord(dev.blk_done[slot], s));
+  dev.blk_used[slot] = true;
+  return MV_OK;
+}
+
+// mv_verify_blocks with MV_FLAG_HOST_PARSE: bincode parsed on the host (block_codec.cpp),
+// staged pre-images to the device. Kept as the cross-check of the device ingest path.
+mv_status verify_blocks_host_parse(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len,
+                                   uint32_t n, uint8_t* status, uint8_t* msg_digest, uint8_t* block_digest) {
+  const mvh::Committee& com = ctx->committee;
+  return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
+    HIPCHK(ctx, hipSetDevice(dev.id));
+    uint64_t i = lo;
+    std::vector<mvh::BlockFacts> facts;
+    while (i < hi) {
+      // chunk: <= max_batch blocks and <= 1 GiB of staged pre-images
+      uint64_t j = i, bytes = 0;
+      while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += len[j++] + 64 + 16;
+      uint32_t m = (uint32_t)(j - i);
+      facts.assign(m, mvh::BlockFacts());
+      HIPCHK(ctx, dev.h_in.ensure(bytes + 64));
+      uint8_t* st = dev.h_in.as<uint8_t>();
+      std::vector<uint64_t> soff(m), slen(m);
+      std::vector<uint32_t> kidx(m);
+      uint64_t pos = 0;
+      for (uint32_t k = 0; k < m; k++) {
+        mvh::BlockFacts& f = facts[k];
+        soff[k] = pos;
+        // pre-image is never longer than the bincode (only fields are dropped or re-encoded)
+        bool ok = mvh::parse_block(buf + off[i + k], len[i + k], &com, st + pos, len[i + k], f);
+        if (!ok) f.parsed = false;
+        uint64_t L = ok ? f.preimage_len : 0;
+        if (ok) memcpy(st + pos + L, f.signature, 64);
+        else memset(st + pos, 0, 64);
+        memset(st + pos + L + 64, 0, 8);
+        slen[k] = L;
+        kidx[k] = (ok && f.author < com.size()) ? (uint32_t)f.author : 0u;
+        pos += (L + 64 + 15) & ~7ull;
+      }
+      HIPCHK(ctx, dev.bytes.ensure(pos + 64));
+      HIPCHK(ctx, dev.off.ensure(8 * (size_t)m));
+      HIPCHK(ctx, dev.len.ensure(8 * (size_t)m));
+      HIPCHK(ctx, dev.msg.ensure(32 * (size_t)m));
+      HIPCHK(ctx, dev.out2.ensure(32 * (size_t)m));
+      HIPCHK(ctx, dev.sig.ensure(64 * (size_t)m));
+      HIPCHK(ctx, dev.keyidx.ensure(4 * (size_t)m));
+      HIPCHK(ctx, dev.status.ensure(m));
+      std::vector<uint8_t> sigs(64 * (size_t)m);
+      for (uint32_t k = 0; k < m; k++) {
+        const mvh::BlockFacts& f = facts[k];
+        memcpy(&sigs[64 * (size_t)k], f.signature, 64);
+        // the verdict of a block that fails a check ahead of the signature one does not
+        // depend on its signature: s = 2^256 - 1 (>= l) takes it out of the batch
+        // equation (rejected up front) instead of failing the whole batch
+        if (!f.parsed || f.epoch != com.epoch || f.author >= com.size() || f.round == 0)
+          memset(&sigs[64 * (size_t)k + 32], 0xff, 32);
+      }
+      HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, st, pos, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(dev.off.p, soff.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(dev.len.p, slen.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(dev.sig.p, sigs.data(), 64 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(dev.keyidx.p, kidx.data(), 4 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
+      // msg digests stay on the device and feed the verify kernel directly
+      HIPCHK(ctx, mvk::launch_block_hash(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
+                                         dev.msg.as<uint8_t>(), dev.out2.as<uint8_t>(), dev.stream));
+      bool batched = false;
+      uint32_t h_flag = 1;
+      if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
+        mv_status st2 = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
+                                      dev.committee_pk.as<uint8_t>(), dev.keyidx.as<uint32_t>(), m,
+                                      dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
+        if (st2 != MV_OK) return st2;
+        batched = true;
+      } else {
+        mv_status st2 = enqueue_committee_verify(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
+                                                 dev.keyidx.as<uint32_t>(), m, dev.status.as<uint8_t>(), dev.stream);
+        if (st2 != MV_OK) return st2;
+      }
+      std::vector<uint8_t> md(32 * (size_t)m), bd(32 * (size_t)m), ss(m);
+      HIPCHK(ctx, hipMemcpyAsync(md.data(), dev.msg.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(bd.data(), dev.out2.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(ss.data(), dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
+      HIPCHK(ctx, hipStreamSynchronize(dev.stream));
+      if (batched) {
+        ctx->batches++;
+        if (!h_flag) ctx->fallbacks++;
+      }
+      for (uint32_t k = 0; k < m; k++) {
+        status[i + k] = mvh::block_verdict(facts[k], com, &bd[32 * (size_t)k], ss[k]);
+        if (msg_digest) memcpy(msg_digest + 32 * (i + k), &md[32 * (size_t)k], 32);
+        if (block_digest) memcpy(block_digest + 32 * (i + k), &bd[32 * (size_t)k], 32);
+      }
+      i = j;
+    }
+    return MV_OK;
+  });
+}
+
 }  // namespace
 
 extern "C" {
 
-const char* mv_version(void) { return "mysti_verify 0.1 gfx950"; }
+const char* mv_version(void) { return "mysti_verify 0.2 gfx950"; }
 
 int64_t mv_block_preimage(const uint8_t* bincode, uint64_t len, uint8_t* out, uint64_t cap) {
   if (!bincode && len) return -1;
@@ -226,6 +435,8 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = dev.btab.ensure(mvk::btable_bytes());
     if (e == hipSuccess) e = mvk::launch_btable_init(dev.btab.p, dev.stream);
+    if (e == hipSuccess) e = dev.combB.ensure(mvk::comb_table_bytes(1));
+    if (e == hipSuccess) e = mvk::launch_comb_init(nullptr, 1, 0, dev.combB.p, nullptr, dev.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(dev.stream);
     if (e != hipSuccess) {
       mv_destroy(ctx);
@@ -242,11 +453,14 @@ void mv_destroy(mv_ctx* ctx) {
   for (auto& dev : ctx->devs) {
     (void)hipSetDevice(dev.id);
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
-    for (DevBuf* b : {&dev.btab, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status, &dev.bytes,
-                      &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0],
-                      &dev.vscr[1]})
+    (void)hipDeviceSynchronize();  // device-API calls may have run on the caller's streams
+    for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
+                      &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
+                      &dev.keyok, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0], &dev.vscr[1], &dev.blk[0], &dev.blk[1]})
       b->release();
     for (hipEvent_t ev : dev.slot_done)
+      if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
     dev.h_in.release();
     dev.h_out.release();
@@ -272,24 +486,23 @@ mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks, const uint64_t* stak
   ctx->has_committee = true;
   for (auto& dev : ctx->devs) {
     HIPCHK(ctx, hipSetDevice(dev.id));
+    HIPCHK(ctx, hipDeviceSynchronize());  // earlier device-API work may still read the old tables
     HIPCHK(ctx, dev.committee_pk.ensure(32 * (size_t)n));
+    HIPCHK(ctx, dev.stakes.ensure(8 * (size_t)n));
+    HIPCHK(ctx, dev.combA.ensure(mvk::comb_table_bytes(n)));
+    HIPCHK(ctx, dev.keyok.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(dev.committee_pk.p, pks, 32 * (size_t)n, hipMemcpyHostToDevice, dev.stream));
+    HIPCHK(ctx, hipMemcpyAsync(dev.stakes.p, stakes, 8 * (size_t)n, hipMemcpyHostToDevice, dev.stream));
+    // VerificationKey::try_from once per key (ZIP-215 decode) and its comb table of -A
+    HIPCHK(ctx, mvk::launch_comb_init(dev.committee_pk.as<uint8_t>(), n, 1, dev.combA.p, dev.keyok.as<uint8_t>(),
+                                      dev.stream));
     HIPCHK(ctx, hipStreamSynchronize(dev.stream));
     dev.committee_loaded = true;
   }
   if (key_ok) {
-    // VerificationKey::try_from: ZIP-215 decode of each key (selftest op 7 on device 0)
-    std::vector<uint32_t> in(16 * (size_t)n, 0), outw(16 * (size_t)n, 0);
-    for (uint32_t i = 0; i < n; i++) memcpy(&in[16 * (size_t)i], pks + 32 * (size_t)i, 32);
     Device& dev = ctx->devs[0];
     HIPCHK(ctx, hipSetDevice(dev.id));
-    HIPCHK(ctx, dev.bytes.ensure(in.size() * 4));
-    HIPCHK(ctx, dev.out2.ensure(outw.size() * 4));
-    HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, in.data(), in.size() * 4, hipMemcpyHostToDevice, dev.stream));
-    HIPCHK(ctx, mvk::launch_selftest(7, dev.bytes.as<uint32_t>(), n, dev.btab.p, dev.out2.as<uint32_t>(), dev.stream));
-    HIPCHK(ctx, hipMemcpyAsync(outw.data(), dev.out2.p, outw.size() * 4, hipMemcpyDeviceToHost, dev.stream));
-    HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-    for (uint32_t i = 0; i < n; i++) key_ok[i] = outw[16 * (size_t)i + 8] ? 1 : 0;
+    HIPCHK(ctx, hipMemcpy(key_ok, dev.keyok.p, n, hipMemcpyDeviceToHost));
   }
   return MV_OK;
 }
@@ -372,9 +585,13 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
                                      dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
         if (st != MV_OK) return st;
         batched = true;
+      } else if (dki) {
+        mv_status st = enqueue_committee_verify(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dki, m,
+                                                dev.status.as<uint8_t>(), dev.stream);
+        if (st != MV_OK) return st;
       } else {
         HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
-        HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m, dev.btab.p,
+        HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, nullptr, m, dev.btab.p,
                                        dev.scratch.p, dev.status.as<uint8_t>(), dev.stream));
       }
       HIPCHK(ctx, hipMemcpyAsync(status + i, dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
@@ -417,90 +634,57 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
   if (!ctx || (n && (!buf || !off || !len || !status))) return set_err(ctx, MV_E_INVALID_ARG, "bad block args");
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (!ctx->has_committee) return set_err(ctx, MV_E_NO_COMMITTEE, "mv_set_committee first");
-  const mvh::Committee& com = ctx->committee;
+  if (ctx->flags & MV_FLAG_HOST_PARSE) return verify_blocks_host_parse(ctx, buf, off, len, n, status, msg_digest,
+                                                                       block_digest);
+  // Device ingest: the host only packs the raw bincode (8-aligned, 16 pad bytes after the
+  // last block) with the offset and length arrays into pinned staging, one H2D; parse,
+  // hashes, signatures and checks run on the GPU; one D2H of [digests | digests | status].
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
     uint64_t i = lo;
-    std::vector<mvh::BlockFacts> facts;
     while (i < hi) {
-      // chunk: <= max_batch blocks and <= 1 GiB of staged pre-images
       uint64_t j = i, bytes = 0;
-      while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += len[j++] + 64 + 16;
-      uint32_t m = (uint32_t)(j - i);
-      facts.assign(m, mvh::BlockFacts());
-      HIPCHK(ctx, dev.h_in.ensure(bytes + 64));
-      uint8_t* st = dev.h_in.as<uint8_t>();
-      std::vector<uint64_t> soff(m), slen(m);
-      std::vector<uint32_t> kidx(m);
+      while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += (len[j++] + 7) & ~7ull;
+      const uint32_t m = (uint32_t)(j - i);
+      const size_t buf_bytes = (bytes + 16 + 15) & ~(size_t)15;
+      const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
+      HIPCHK(ctx, dev.h_in.ensure(total));
+      uint8_t* h = dev.h_in.as<uint8_t>();
+      uint64_t* hoff = (uint64_t*)(h + o_off);
+      uint64_t* hlen = (uint64_t*)(h + o_len);
       uint64_t pos = 0;
       for (uint32_t k = 0; k < m; k++) {
-        mvh::BlockFacts& f = facts[k];
-        soff[k] = pos;
-        // pre-image is never longer than the bincode (only fields are dropped or re-encoded)
-        bool ok = mvh::parse_block(buf + off[i + k], len[i + k], &com, st + pos, len[i + k], f);
-        if (!ok) f.parsed = false;
-        uint64_t L = ok ? f.preimage_len : 0;
-        if (ok) memcpy(st + pos + L, f.signature, 64);
-        else memset(st + pos, 0, 64);
-        memset(st + pos + L + 64, 0, 8);
-        slen[k] = L;
-        kidx[k] = (ok && f.author < com.size()) ? (uint32_t)f.author : 0u;
-        pos += (L + 64 + 15) & ~7ull;
+        const uint64_t l = len[i + k];
+        memcpy(h + pos, buf + off[i + k], l);
+        hoff[k] = pos;
+        hlen[k] = l;
+        const uint64_t next = (pos + l + 7) & ~7ull;
+        memset(h + pos + l, 0, next - pos - l);
+        pos = next;
       }
-      HIPCHK(ctx, dev.bytes.ensure(pos + 64));
-      HIPCHK(ctx, dev.off.ensure(8 * (size_t)m));
-      HIPCHK(ctx, dev.len.ensure(8 * (size_t)m));
-      HIPCHK(ctx, dev.msg.ensure(32 * (size_t)m));
-      HIPCHK(ctx, dev.out2.ensure(32 * (size_t)m));
-      HIPCHK(ctx, dev.sig.ensure(64 * (size_t)m));
-      HIPCHK(ctx, dev.keyidx.ensure(4 * (size_t)m));
-      HIPCHK(ctx, dev.status.ensure(m));
-      std::vector<uint8_t> sigs(64 * (size_t)m);
-      for (uint32_t k = 0; k < m; k++) {
-        const mvh::BlockFacts& f = facts[k];
-        memcpy(&sigs[64 * (size_t)k], f.signature, 64);
-        // the verdict of a block that fails a check ahead of the signature one does not
-        // depend on its signature: s = 2^256 - 1 (>= l) takes it out of the batch
-        // equation (rejected up front) instead of failing the whole batch
-        if (!f.parsed || f.epoch != com.epoch || f.author >= com.size() || f.round == 0)
-          memset(&sigs[64 * (size_t)k + 32], 0xff, 32);
-      }
-      HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, st, pos, hipMemcpyHostToDevice, dev.stream));
-      HIPCHK(ctx, hipMemcpyAsync(dev.off.p, soff.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
-      HIPCHK(ctx, hipMemcpyAsync(dev.len.p, slen.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
-      HIPCHK(ctx, hipMemcpyAsync(dev.sig.p, sigs.data(), 64 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
-      HIPCHK(ctx, hipMemcpyAsync(dev.keyidx.p, kidx.data(), 4 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
-      // msg digests stay on the device and feed the verify kernel directly
-      HIPCHK(ctx, mvk::launch_block_hash(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
-                                         dev.msg.as<uint8_t>(), dev.out2.as<uint8_t>(), dev.stream));
+      memset(h + pos, 0, buf_bytes - pos);
+      HIPCHK(ctx, dev.bytes.ensure(total));
+      HIPCHK(ctx, dev.out2.ensure(65 * (size_t)m + 256));
+      HIPCHK(ctx, dev.h_out.ensure(65 * (size_t)m));
+      HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
+      uint8_t* dout = dev.out2.as<uint8_t>();
+      const uint8_t* dbuf = dev.bytes.as<uint8_t>();
       bool batched = false;
       uint32_t h_flag = 1;
-      if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
-        mv_status st = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
-                                     dev.committee_pk.as<uint8_t>(), dev.keyidx.as<uint32_t>(), m,
-                                     dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
-        if (st != MV_OK) return st;
-        batched = true;
-      } else {
-        HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
-        HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dev.committee_pk.as<uint8_t>(),
-                                       dev.keyidx.as<uint32_t>(), m, dev.btab.p, dev.scratch.p,
-                                       dev.status.as<uint8_t>(), dev.stream));
-      }
-      std::vector<uint8_t> md(32 * (size_t)m), bd(32 * (size_t)m), ss(m);
-      HIPCHK(ctx, hipMemcpyAsync(md.data(), dev.msg.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
-      HIPCHK(ctx, hipMemcpyAsync(bd.data(), dev.out2.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
-      HIPCHK(ctx, hipMemcpyAsync(ss.data(), dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
+      mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
+                                    (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
+                                    dout + 32 * (size_t)m, dev.stream, &h_flag, &batched);
+      if (st != MV_OK) return st;
+      HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
       if (batched) {
         ctx->batches++;
         if (!h_flag) ctx->fallbacks++;
       }
-      for (uint32_t k = 0; k < m; k++) {
-        status[i + k] = mvh::block_verdict(facts[k], com, &bd[32 * (size_t)k], ss[k]);
-        if (msg_digest) memcpy(msg_digest + 32 * (i + k), &md[32 * (size_t)k], 32);
-        if (block_digest) memcpy(block_digest + 32 * (i + k), &bd[32 * (size_t)k], 32);
-      }
+      const uint8_t* ho = dev.h_out.as<uint8_t>();
+      memcpy(status + i, ho + 64 * (size_t)m, m);
+      if (msg_digest) memcpy(msg_digest + 32 * i, ho, 32 * (size_t)m);
+      if (block_digest) memcpy(block_digest + 32 * i, ho + 32 * (size_t)m, 32 * (size_t)m);
       i = j;
     }
     return MV_OK;
@@ -511,6 +695,24 @@ static Device* find_dev(mv_ctx* ctx, int device) {
   for (auto& d : ctx->devs)
     if (d.id == device) return &d;
   return nullptr;
+}
+
+mv_status mv_dev_verify_blocks(mv_ctx* ctx, int device, const uint8_t* d_buf, uint64_t buf_bytes,
+                               const uint64_t* d_off, const uint64_t* d_len, uint32_t n, uint8_t* d_status,
+                               uint8_t* d_msg_digest, uint8_t* d_block_digest, void* stream) {
+  if (!ctx || (n && (!d_buf || !d_off || !d_len || !d_status))) return set_err(ctx, MV_E_INVALID_ARG, "bad args");
+  if (((uintptr_t)d_buf) & 7) return set_err(ctx, MV_E_INVALID_ARG, "d_buf must be 8-byte aligned");
+  if ((((uintptr_t)d_msg_digest) | ((uintptr_t)d_block_digest)) & 15)
+    return set_err(ctx, MV_E_INVALID_ARG, "digest arrays must be 16-byte aligned");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!ctx->has_committee) return set_err(ctx, MV_E_NO_COMMITTEE, "mv_set_committee first");
+  Device* dev = find_dev(ctx, device);
+  if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
+  HIPCHK(ctx, hipSetDevice(dev->id));
+  hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
+  bool batched = false;
+  return enqueue_blocks(ctx, *dev, d_buf, buf_bytes, d_off, d_len, n, d_status, d_msg_digest, d_block_digest, s,
+                        nullptr, &batched);
 }
 
 mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
@@ -554,24 +756,25 @@ mv_status mv_stage_times(mv_ctx* ctx, double* ms, uint64_t* calls, int reset) {
   if (!ctx) return MV_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(ctx->tmu);
   for (auto& pe : ctx->pending) {
-    HIPCHK(ctx, hipSetDevice(pe.first));
-    std::vector<hipEvent_t>& ev = pe.second;
+    HIPCHK(ctx, hipSetDevice(pe.device));
+    std::vector<hipEvent_t>& ev = pe.events;
     HIPCHK(ctx, hipEventSynchronize(ev.back()));
-    for (int i = 0; i < mvk::BATCH_STAGES; i++) {
+    for (size_t i = 0; i + 1 < ev.size(); i++) {
       float t = 0;
       HIPCHK(ctx, hipEventElapsedTime(&t, ev[i], ev[i + 1]));
-      ctx->stage_ms[i] += t;
+      ctx->stage_ms[pe.first_stage + i] += t;
+      ctx->stage_calls[pe.first_stage + i]++;
     }
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-    ctx->stage_calls++;
   }
   ctx->pending.clear();
-  if (ms)
-    for (int i = 0; i < mvk::BATCH_STAGES; i++) ms[i] = ctx->stage_ms[i];
-  if (calls) *calls = ctx->stage_calls;
+  for (int i = 0; i < MV_NSTAGES; i++) {
+    if (ms) ms[i] = ctx->stage_ms[i];
+    if (calls) calls[i] = ctx->stage_calls[i];
+  }
   if (reset) {
     for (double& x : ctx->stage_ms) x = 0;
-    ctx->stage_calls = 0;
+    for (uint64_t& x : ctx->stage_calls) x = 0;
   }
   return MV_OK;
 }

@@ -28,4 +28,18 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
                                void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out,
                                hipEvent_t* ev = nullptr);
+// comb.hip: per-key comb tables C[i][j] = [j 256^i](+-P) and the committee-key verify.
+// enc == nullptr builds the table of B; negate = 1 stores -P (committee keys).
+size_t comb_table_bytes(uint32_t nbases);
+hipError_t launch_comb_init(const uint8_t* enc, uint32_t nb, int negate, void* tab, uint8_t* ok, hipStream_t s);
+hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                              uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
+                              uint8_t* status, hipStream_t s);
+// ingest.hip: device-side bincode parse + pre-image staging, and the final block verdict
+hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                              const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
+                              uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
+                              uint32_t* facts, uint8_t* claimed, hipStream_t s);
+hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, const uint8_t* digest,
+                                const uint8_t* sig_status, uint32_t n, uint8_t* status, hipStream_t s);
 }  // namespace mvk
