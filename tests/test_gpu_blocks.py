@@ -95,8 +95,18 @@ def test_edge_blocks_through_batch_path(engine, golden):
     e = golden("block_edge.json")
     pks, stakes, epoch = committee_arrays(e["committee"])
     engine.set_committee(pks, stakes, epoch)
+    # the fixture's "bad signature" flips a bit of R, which then does not decode: decided per
+    # signature before the combination (no fallback). A flipped bit of s (still < l) with R
+    # intact can only be caught by the combined equation, so it forces the fallback.
+    valid = bytes.fromhex(next(c for c in e["cases"] if c["note"] == "valid")["bincode"])
+    sig = bytearray(valid[-64:])
+    sig[40] ^= 0x10
+    dig = hashlib.blake2b(M.block_preimage(valid) + bytes(sig), digest_size=32).digest()
+    bad_s = {"bincode": (valid[:24] + dig + valid[56:-64] + bytes(sig)).hex(), "status": 6, "note": "s bit flip"}
     for drop_bad_sig in (True, False):
-        cases = [c for c in e["cases"] if not (drop_bad_sig and c["note"].startswith("bad signature"))]
+        cases = [c for c in e["cases"] if not c["note"].startswith("bad signature")]
+        if not drop_bad_sig:
+            cases.append(bad_s)
         reps = M.BATCH_MIN // len(cases) + 1
         blocks = [bytes.fromhex(c["bincode"]) for c in cases] * reps
         b0, f0 = engine.batch_stats()

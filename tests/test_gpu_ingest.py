@@ -79,7 +79,7 @@ def test_byte_flips_and_garbage_vs_oracle(engine, host_engine):
         assert int(st[i]) == ost, i
         if ost != O.BLOCK_PARSE_ERROR:
             assert md[i].tobytes() == omd and bd[i].tobytes() == obd, i
-    assert len({int(s) for s in st}) >= 4
+    assert len({int(s) for s in st}) >= 3
 
 
 def test_statement_kinds_and_ragged_lengths(engine, host_engine):
