@@ -176,7 +176,8 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     d_off = torch.from_numpy(off_all).to(dev)
     d_len = torch.from_numpy(len_all).to(dev)
     buf_bytes = reps * span
-    nstreams = max(1, args.streams)
+    # one stream: the stage events then time each stage alone (they match rocprofv3)
+    nstreams = 1
     streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
     d_st = [torch.full((n,), 255, dtype=torch.uint8, device=dev) for _ in range(nstreams)]
     d_md = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(nstreams)]

@@ -17,6 +17,7 @@
 // both paths and the oracle to the same verdicts and digests, malformed input included.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/mysti_verify.h"
 #include "hash_dev.h"
@@ -112,25 +113,33 @@ struct PreWriter {
   }
 };
 
-// Lane per block. Block i = buf[off[i] .. off[i] + len[i]); P || sig (then 8 zero bytes) is
-// written at stage + round_up(off[i], 8), which stays inside the block's own span because
-// the bincode is at least |P| + 128 bytes long. Writes happen only after the bytes they
-// come from were read, so a malformed block never writes outside its span either.
-__global__ void __launch_bounds__(256) k_block_parse(
-    const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint32_t n,
-    const uint64_t* __restrict__ stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
-    uint8_t* __restrict__ stage, uint64_t* __restrict__ pre_off, uint64_t* __restrict__ pre_len,
-    uint8_t* __restrict__ sig_out, uint32_t* __restrict__ key_idx, uint32_t* __restrict__ facts,
-    uint8_t* __restrict__ claimed) {
-  __shared__ uint32_t seen[16][256];  // per-lane authority bitmap (<= 512 authorities), [word][lane]
-  const uint32_t t = threadIdx.x;
-  const uint32_t i = blockIdx.x * 256 + t;
-#pragma unroll
-  for (int k = 0; k < 16; k++) seen[k][t] = 0;
-  if (i >= n) return;
-  const uint64_t o = off[i];
+// Outputs of the ingest of one block (all indexed by block).
+struct IngestOut {
+  uint8_t* stage;
+  uint64_t* pre_off;
+  uint64_t* pre_len;
+  uint8_t* sig_out;
+  uint32_t* key_idx;
+  uint32_t* facts;
+  uint8_t* claimed;
+};
+struct CommitteeView {
+  const uint64_t* stakes;
+  uint32_t n_auth;
+  uint64_t epoch, quorum_thr;
+};
+
+// Block i = buf[o .. o + L), one lane, straight from global memory. P || sig (then 8 zero
+// bytes) is written at stage + round_up(o, 8), which stays inside the block's own span
+// because the bincode is at least |P| + 128 bytes long; writes happen only after the bytes
+// they come from were read, so a malformed block never writes outside its span either.
+// seen[k * stride], k < 16: a zeroed authority bitmap (<= 512 authorities) for this lane.
+MV_DEV void ingest_lane(const uint8_t* buf, uint64_t o, uint64_t L, uint32_t i, const CommitteeView& cv,
+                        const IngestOut& io, uint32_t* seen, int stride) {
+  const uint32_t n_auth = cv.n_auth;
   const uint64_t so = (o + 7) & ~7ull;
-  BcReader r{buf + o, len[i], 0, true};
+  uint8_t* const stage = io.stage;
+  BcReader r{buf + o, L, 0, true};
   PreWriter w{reinterpret_cast<uint64_t*>(stage + so), 0, 0, 0};
 
   uint64_t me_a, me_r;
@@ -159,12 +168,12 @@ __global__ void __launch_bounds__(256) k_block_parse(
     }
     if (me_r > 0 && rd == me_r - 1 && a < n_auth) {
       const uint32_t wd = static_cast<uint32_t>(a) >> 5, bit = 1u << (a & 31);
-      const uint32_t s = seen[wd][t];
+      const uint32_t s = seen[wd * stride];
       if (!(s & bit)) {
-        seen[wd][t] = s | bit;
-        stake += stakes[a];
+        seen[wd * stride] = s | bit;
+        stake += cv.stakes[a];
       }
-      quorum = stake > quorum_thr;
+      quorum = stake > cv.quorum_thr;
     }
   }
   // statements
@@ -255,20 +264,20 @@ __global__ void __launch_bounds__(256) k_block_parse(
     }
     w.put(0, 8);  // a zero word after P || sig
     w.flush();
-    pre_len[i] = plen;
-    f = BF_PARSED | (ep == epoch ? BF_EPOCH_OK : 0u) | (me_a < n_auth ? BF_AUTHOR_OK : 0u) |
+    io.pre_len[i] = plen;
+    f = BF_PARSED | (ep == cv.epoch ? BF_EPOCH_OK : 0u) | (me_a < n_auth ? BF_AUTHOR_OK : 0u) |
         (me_r == 0 ? BF_GENESIS : 0u) | (vr_bad ? BF_VR_BAD : 0u) | (quorum ? BF_QUORUM : 0u) |
         (inc_err << BF_INC_SHIFT);
     const uint64_t d0 = peek8(me_d), d1 = peek8(me_d + 8), d2 = peek8(me_d + 16), d3 = peek8(me_d + 24);
-    uint4* cd = reinterpret_cast<uint4*>(claimed + 32 * (size_t)i);
+    uint4* cd = reinterpret_cast<uint4*>(io.claimed + 32 * (size_t)i);
     cd[0] = make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32));
     cd[1] = make_uint4((uint32_t)d2, (uint32_t)(d2 >> 32), (uint32_t)d3, (uint32_t)(d3 >> 32));
   } else {
-    pre_len[i] = 0;
+    io.pre_len[i] = 0;
 #pragma unroll
     for (int q = 0; q < 16; q++) sw[q] = 0;
   }
-  pre_off[i] = so;
+  io.pre_off[i] = so;
   // a block rejected ahead of the signature check gets s = 2^256 - 1 (>= l): its verdict
   // does not depend on the signature, and s >= l keeps it out of the batch equation
   const bool sig_decides = parsed && (f & BF_EPOCH_OK) && (f & BF_AUTHOR_OK) && !(f & BF_GENESIS);
@@ -276,11 +285,352 @@ __global__ void __launch_bounds__(256) k_block_parse(
 #pragma unroll
     for (int q = 8; q < 16; q++) sw[q] = 0xffffffffu;
   }
-  uint4* so4 = reinterpret_cast<uint4*>(sig_out + 64 * (size_t)i);
+  uint4* so4 = reinterpret_cast<uint4*>(io.sig_out + 64 * (size_t)i);
 #pragma unroll
   for (int q = 0; q < 4; q++) so4[q] = make_uint4(sw[4 * q], sw[4 * q + 1], sw[4 * q + 2], sw[4 * q + 3]);
-  key_idx[i] = (parsed && me_a < n_auth) ? static_cast<uint32_t>(me_a) : 0u;
-  facts[i] = f;
+  io.key_idx[i] = (parsed && me_a < n_auth) ? static_cast<uint32_t>(me_a) : 0u;
+  io.facts[i] = f;
+}
+
+// Lane per block over global memory (the reference implementation of the ingest; the
+// product launches k_block_ingest, which falls back to ingest_lane for oversize blocks).
+__global__ void __launch_bounds__(256) k_block_parse(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                                                     const uint64_t* __restrict__ len, uint32_t n, CommitteeView cv,
+                                                     IngestOut io) {
+  __shared__ uint32_t seen[16][256];  // per-lane authority bitmap, [word][lane]
+  const uint32_t t = threadIdx.x;
+  const uint32_t i = blockIdx.x * 256 + t;
+#pragma unroll
+  for (int k = 0; k < 16; k++) seen[k][t] = 0;
+  if (i >= n) return;
+  ingest_lane(buf, off[i], len[i], i, cv, io, &seen[0][t], 256);
+}
+
+// ---------------------------------------------------------------- wave per block
+// k_block_ingest: one 64-lane workgroup per block. The block's bincode is staged in LDS with
+// coalesced 8-byte loads; the fixed-size includes are transcoded one per lane; the
+// variable-size statements are located 64 at a time by lane 0 walking their headers, then
+// transcoded one per lane (Share payloads copied by the whole wave); the pre-image is built
+// in LDS and written to the stage with coalesced stores. Blocks that do not fit the LDS
+// window take ingest_lane on lane 0. The rules are ingest_lane's (and block_codec.cpp's);
+// tests/test_gpu_ingest.py holds the two kernels and the host codec to identical results.
+constexpr uint32_t IG_WIN = 10240;  // LDS window per block, bytes
+constexpr uint32_t IG_CHUNK = 64;   // statements located per walk
+
+MV_DEV uint32_t lds_u8(const uint32_t* w, uint32_t p) { return (w[p >> 2] >> (8 * (p & 3))) & 0xffu; }
+MV_DEV uint32_t lds_u32(const uint32_t* w, uint32_t p) {
+  const uint32_t i = p >> 2, sh = (p & 3) * 8;
+  return __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+}
+MV_DEV uint64_t lds_u64(const uint32_t* w, uint32_t p) {
+  const uint32_t i = p >> 2, sh = (p & 3) * 8;
+  const uint32_t x0 = w[i], x1 = w[i + 1], x2 = w[i + 2];
+  return ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32) | __builtin_amdgcn_alignbit(x1, x0, sh);
+}
+MV_DEV void pre_be64(uint8_t* pre, uint32_t p, uint64_t x) {
+#pragma unroll
+  for (int b = 0; b < 8; b++) pre[p + b] = (uint8_t)(x >> (56 - 8 * b));
+}
+// 32 bytes from the window (any alignment) into the pre-image: 9 word reads issued together
+MV_DEV void pre_copy32(uint8_t* pre, uint32_t p, const uint32_t* win, uint32_t q) {
+  const uint32_t i = q >> 2, sh = (q & 3) * 8;
+  uint32_t w[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) w[k] = win[i + k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t x = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh);
+#pragma unroll
+    for (int b = 0; b < 4; b++) pre[p + 4 * k + b] = (uint8_t)(x >> (8 * b));
+  }
+}
+MV_DEV uint32_t wave_min(uint32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, m));
+  return x;
+}
+MV_DEV uint32_t wave_or(uint32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x |= (uint32_t)__shfl_xor((int)x, m);
+  return x;
+}
+MV_DEV uint64_t wave_sum64(uint64_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), m);
+    x += ((uint64_t)hi << 32) | lo;
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                                                     const uint64_t* __restrict__ len, uint32_t n, CommitteeView cv,
+                                                     IngestOut io) {
+  __shared__ uint32_t win[IG_WIN / 4 + 8];      // the block's bincode (from its aligned start)
+  __shared__ uint64_t pre64[IG_WIN / 8];        // its pre-image || signature
+  __shared__ uint32_t st_pos[IG_CHUNK], st_pre[IG_CHUNK];
+  __shared__ uint32_t seen[16];                 // authorities of round r-1 among the includes
+  uint8_t* pre = reinterpret_cast<uint8_t*>(pre64);
+  const uint32_t lane = threadIdx.x;
+  const uint32_t i = blockIdx.x;
+  const uint64_t o = off[i], L = len[i];
+  const uint32_t d = (uint32_t)(o & 7);
+  if (lane < 16) seen[lane] = 0;
+  if (d + L + 16 > IG_WIN) {  // does not fit the window: one lane from global memory
+    __syncthreads();
+    if (lane == 0) ingest_lane(buf, o, L, i, cv, io, seen, 1);
+    return;
+  }
+  {
+    // 16 loads in flight per lane before their LDS stores (a store right behind each load
+    // would serialise the HBM latency 19 times for a 9.5-KB block)
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(buf + (o - d));
+    uint64_t* w64 = reinterpret_cast<uint64_t*>(win);
+    const uint32_t nw = (uint32_t)((d + L + 15) >> 3);
+    for (uint32_t k0 = lane; k0 < nw; k0 += 64 * 16) {
+      uint64_t t[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) t[j] = k0 + 64 * j < nw ? src[k0 + 64 * j] : 0ull;
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (k0 + 64 * j < nw) w64[k0 + 64 * j] = t[j];
+    }
+  }
+  __syncthreads();
+  const uint32_t Lb = (uint32_t)L;
+  auto rd64 = [&](uint32_t p) { return lds_u64(win, d + p); };
+  auto rd32 = [&](uint32_t p) { return lds_u32(win, d + p); };
+  auto rd8 = [&](uint32_t p) { return lds_u8(win, d + p); };
+  const uint32_t n_auth = cv.n_auth;
+
+  // reference (56 B) and the include count
+  bool ok = Lb >= 64;
+  uint64_t me_a = 0, me_r = 0;
+  if (ok) {
+    me_a = rd64(0);
+    me_r = rd64(8);
+    ok = rd64(16) == 32;
+  }
+  const uint64_t n_inc = ok ? rd64(56) : 0;
+  if (ok && n_inc > (uint64_t)((Lb - 64) / 56)) ok = false;
+  uint32_t bad = 0, inc_first = 0xffffffffu;
+  if (ok) {
+    if (lane < 8) {
+      pre[lane] = (uint8_t)(me_a >> (56 - 8 * lane));
+      pre[8 + lane] = (uint8_t)(me_r >> (56 - 8 * lane));
+    }
+    // includes: lane per include (pre-image at 16 + 48 k), checks (types.rs:349-362),
+    // the threshold clock's authorities of round r-1 (threshold_clock.rs:12-35)
+    for (uint32_t k = lane; k < (uint32_t)n_inc; k += 64) {
+      const uint32_t p = 64 + 56 * k;
+      const uint64_t a = rd64(p), r = rd64(p + 8);
+      bad |= rd64(p + 16) != 32;
+      const uint32_t q = 16 + 48 * k;
+      pre_be64(pre, q, a);
+      pre_be64(pre, q + 8, r);
+      pre_copy32(pre, q + 16, win, d + p + 24);
+      const uint32_t code = a >= n_auth ? MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY : (r >= me_r ? MV_BLOCK_INCLUDE_ROUND : 0u);
+      if (code && inc_first == 0xffffffffu) inc_first = (k << 4) | code;
+      if (me_r > 0 && r == me_r - 1 && a < n_auth) atomicOr(&seen[(uint32_t)a >> 5], 1u << (a & 31));
+    }
+  }
+  inc_first = wave_min(inc_first);
+  // statements: located by lane 0 (headers only), 64 at a time, then transcoded per lane
+  uint32_t pos = 64 + 56 * (uint32_t)n_inc, ppos = 16 + 48 * (uint32_t)n_inc;
+  uint64_t n_st = 0;
+  if (ok) {
+    if (pos + 8 > Lb) ok = false;
+    else n_st = rd64(pos);
+    pos += 8;
+  }
+  uint32_t vr_bad = 0;
+  for (uint64_t k0 = 0; ok && k0 < n_st; k0 += IG_CHUNK) {
+    // Locate up to IG_CHUNK statements. Speculation: lane j assumes the j statements
+    // before it are VoteRanges (76 B in bincode, 65 in the pre-image) and checks its own
+    // tag; the run of confirmed VoteRanges is taken at once, anything else takes one
+    // scalar step (the whole wave computes it identically).
+    uint32_t c = 0, p = pos, pp = ppos;
+    bool lok = true;
+    while (c < IG_CHUNK && k0 + c < n_st) {
+      const uint32_t j = c + lane;
+      const uint32_t q = p + 76 * lane;
+      const bool rng = j < IG_CHUNK && k0 + j < n_st && q + 76 <= Lb && rd32(q) == 2;
+      const uint64_t brk = __ballot(!rng);
+      const uint32_t run = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;
+      if (lane < run) {
+        st_pos[j] = q;
+        st_pre[j] = pp + 65 * lane;
+      }
+      c += run;
+      p += 76 * run;
+      pp += 65 * run;
+      if (c >= IG_CHUNK || k0 + c >= n_st) break;
+      uint32_t size = 0, psize = 0;
+      if (p + 4 > Lb) { lok = false; break; }
+      const uint32_t tag = rd32(p);
+      if (tag == 0) {  // Share: u32 tag, u64 length, bytes
+        if (p + 12 > Lb) { lok = false; break; }
+        const uint64_t l = rd64(p + 4);
+        if (l > (uint64_t)(Lb - p - 12)) { lok = false; break; }
+        size = 12 + (uint32_t)l;
+        psize = 1 + (uint32_t)l;
+      } else if (tag == 1) {  // Vote: locator (64 B), u32 vote, [u8 option, [locator]]
+        if (p + 72 > Lb) { lok = false; break; }
+        const uint32_t vote = rd32(p + 68);
+        if (vote == 0) {
+          size = 72;
+          psize = 57;
+        } else if (vote == 1 && p + 73 <= Lb) {
+          const uint32_t some = rd8(p + 72);
+          if (some == 0) {
+            size = 73;
+            psize = 57;
+          } else if (some == 1 && p + 137 <= Lb) {
+            size = 137;
+            psize = 113;
+          } else {
+            lok = false;
+            break;
+          }
+        } else {
+          lok = false;
+          break;
+        }
+      } else {  // tag 2 here means a truncated VoteRange; others are invalid
+        lok = false;
+        break;
+      }
+      if (lane == 0) {
+        st_pos[c] = p;
+        st_pre[c] = pp;
+      }
+      c++;
+      p += size;
+      pp += psize;
+    }
+    __syncthreads();
+    const uint32_t cnt = c;
+    ok = lok;
+    bool is_share = false;
+    if (lane < cnt) {
+      const uint32_t p = st_pos[lane], q = st_pre[lane];
+      const uint32_t tag = rd32(p);
+      if (tag == 0) {
+        pre[q] = 0;
+        is_share = true;
+      } else if (tag == 1) {
+        const uint64_t a = rd64(p + 4), r = rd64(p + 12), off1 = rd64(p + 60);
+        bad |= rd64(p + 20) != 32;
+        const uint32_t vote = rd32(p + 68);
+        const uint32_t some = vote == 1 ? rd8(p + 72) : 0u;
+        pre[q] = (uint8_t)(vote == 0 ? 1 : (some == 0 ? 2 : 3));
+        pre_be64(pre, q + 1, a);
+        pre_be64(pre, q + 9, r);
+        pre_copy32(pre, q + 17, win, d + p + 28);
+        pre_be64(pre, q + 49, off1);
+        if (vote == 1 && some == 1) {
+          const uint64_t a2 = rd64(p + 73), r2 = rd64(p + 81), off2 = rd64(p + 129);
+          bad |= rd64(p + 89) != 32;
+          pre_be64(pre, q + 57, a2);
+          pre_be64(pre, q + 65, r2);
+          pre_copy32(pre, q + 73, win, d + p + 97);
+          pre_be64(pre, q + 105, off2);
+        }
+      } else {  // tag 2
+        const uint64_t a = rd64(p + 4), r = rd64(p + 12), s0 = rd64(p + 60), s1 = rd64(p + 68);
+        bad |= rd64(p + 20) != 32;
+        pre[q] = 4;
+        pre_be64(pre, q + 1, a);
+        pre_be64(pre, q + 9, r);
+        pre_copy32(pre, q + 17, win, d + p + 28);
+        pre_be64(pre, q + 49, s0);
+        pre_be64(pre, q + 57, s1);
+        vr_bad |= (s1 < s0 || s1 - s0 >= VR_MAX_LEN || s1 >= VR_MAX_LEN) ? 1u : 0u;
+      }
+    }
+    // Share payloads, copied by the whole wave
+    uint64_t shares = __ballot(is_share);
+    while (shares) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(shares);
+      shares &= shares - 1;
+      const uint32_t p = st_pos[j], q = st_pre[j];
+      const uint32_t l = (uint32_t)rd64(p + 4);
+      for (uint32_t t = lane; t < l; t += 64) pre[q + 1 + t] = (uint8_t)rd8(p + 12 + t);
+    }
+    pos = p;
+    ppos = pp;
+    __syncthreads();  // st_* are rewritten by the next chunk
+  }
+  // meta_creation_time_ns (u128 LE), epoch_marker (bool), epoch, signature (u64 64 + 64 B)
+  uint64_t tlo = 0, thi = 0, ep = 0;
+  uint32_t marker = 0;
+  if (ok) {
+    if (pos + 97 > Lb) {
+      ok = false;
+    } else {
+      tlo = rd64(pos);
+      thi = rd64(pos + 8);
+      marker = rd8(pos + 16);
+      ep = rd64(pos + 17);
+      ok = marker <= 1 && rd64(pos + 25) == 64;
+    }
+  }
+  ok = ok && wave_or(bad) == 0;
+  const uint32_t spos = pos + 33;  // signature
+  uint32_t f = 0;
+  if (ok) {
+    if (lane == 0) {
+      pre_be64(pre, ppos, thi);
+      pre_be64(pre, ppos + 8, tlo);
+      pre[ppos + 16] = (uint8_t)marker;
+      pre_be64(pre, ppos + 17, ep);
+    }
+    pre[ppos + 25 + lane] = (uint8_t)rd8(spos + lane);  // P || sig
+    // threshold clock: stake of the distinct round r-1 authorities among the includes
+    // (lane j sums authorities j, j + 64, ...: independent loads, one latency)
+    uint64_t stake = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+      const uint32_t a = lane + 64 * q;
+      if (a < n_auth && ((seen[a >> 5] >> (a & 31)) & 1u)) stake += cv.stakes[a];
+    }
+    stake = wave_sum64(stake);
+    const uint32_t inc_code = inc_first == 0xffffffffu ? 0u : (inc_first & 15u);
+    vr_bad = wave_or(vr_bad);
+    f = BF_PARSED | (ep == cv.epoch ? BF_EPOCH_OK : 0u) | (me_a < n_auth ? BF_AUTHOR_OK : 0u) |
+        (me_r == 0 ? BF_GENESIS : 0u) | (vr_bad ? BF_VR_BAD : 0u) | (stake > cv.quorum_thr ? BF_QUORUM : 0u) |
+        (inc_code << BF_INC_SHIFT);
+  }
+  __syncthreads();
+  const uint64_t so = (o + 7) & ~7ull;
+  const uint32_t plen = ppos + 25;
+  if (ok) {  // P || sig to the stage (it stays inside the block's own span, see ingest_lane)
+    uint64_t* dst = reinterpret_cast<uint64_t*>(io.stage + so);
+    const uint32_t nw = (plen + 64 + 7) >> 3;
+    for (uint32_t k = lane; k < nw; k += 64) dst[k] = pre64[k];
+  }
+  if (lane == 0) {
+    io.pre_off[i] = so;
+    io.pre_len[i] = ok ? plen : 0;
+    uint32_t sw[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) sw[q] = ok ? rd32(spos + 4 * q) : 0u;
+    if (ok) {
+      uint4* cd = reinterpret_cast<uint4*>(io.claimed + 32 * (size_t)i);
+      cd[0] = make_uint4(rd32(24), rd32(28), rd32(32), rd32(36));
+      cd[1] = make_uint4(rd32(40), rd32(44), rd32(48), rd32(52));
+    }
+    const bool sig_decides = ok && (f & BF_EPOCH_OK) && (f & BF_AUTHOR_OK) && !(f & BF_GENESIS);
+    if (!sig_decides) {
+#pragma unroll
+      for (int q = 8; q < 16; q++) sw[q] = 0xffffffffu;
+    }
+    uint4* so4 = reinterpret_cast<uint4*>(io.sig_out + 64 * (size_t)i);
+#pragma unroll
+    for (int q = 0; q < 4; q++) so4[q] = make_uint4(sw[4 * q], sw[4 * q + 1], sw[4 * q + 2], sw[4 * q + 3]);
+    io.key_idx[i] = (ok && me_a < n_auth) ? (uint32_t)me_a : 0u;
+    io.facts[i] = f;
+  }
 }
 
 // status[i] in the order of StatementBlock::verify (types.rs:315-376)
@@ -325,8 +675,16 @@ hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uin
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mv::k_block_parse, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, stakes, n_auth,
-                     epoch, quorum_thr, stage, pre_off, pre_len, sig, key_idx, facts, claimed);
+  const mv::CommitteeView cv{stakes, n_auth, epoch, quorum_thr};
+  const mv::IngestOut io{stage, pre_off, pre_len, sig, key_idx, facts, claimed};
+  static const bool lane_kernel = [] {
+    const char* e = getenv("MV_INGEST_LANE");  // A/B: the lane-per-block kernel
+    return e && e[0] == '1';
+  }();
+  if (lane_kernel)
+    hipLaunchKernelGGL(mv::k_block_parse, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, cv, io);
+  else
+    hipLaunchKernelGGL(mv::k_block_ingest, dim3(n), dim3(64), 0, s, buf, off, len, n, cv, io);
   return hipGetLastError();
 }
 

@@ -391,6 +391,11 @@ __global__ void __launch_bounds__(256) k_blake2b(const uint8_t* __restrict__ buf
 }
 
 // Staged P || sig (8-aligned, len[i] = |P|): msg = B2(P), digest = B2(P || sig).
+// The compressions common to both hashes are done once. All compressions go through ONE
+// b2_compress call site (a step loop that picks the block, the length limit, the counter
+// and the final flag), so the unrolled compression (~20 KB of code) is instantiated once:
+// with a call site per phase the kernel overflowed the instruction cache. The next step's
+// message block is loaded during the current compression.
 __global__ void __launch_bounds__(256) k_block_hash(const uint8_t* __restrict__ buf,
                                                     const uint64_t* __restrict__ off,
                                                     const uint64_t* __restrict__ len, uint32_t n,
@@ -398,28 +403,44 @@ __global__ void __launch_bounds__(256) k_block_hash(const uint8_t* __restrict__ 
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n) return;
   const uint8_t* p = buf + off[gid];
-  const uint64_t L = len[gid];
-  uint64_t h[8], m[16];
-  b2_init256(h);
+  const uint64_t L = len[gid], LD = L + 64;
   const uint64_t common = L == 0 ? 0 : (L - 1) / 128;  // non-final in both hashes
-  for (uint64_t b = 0; b < common; b++) {
-    b2_load_block(m, p, b, L + 64);
-    b2_compress(h, m, 128 * (b + 1), false);
-  }
-  uint64_t hm[8];
+  const uint64_t last = (LD - 1) / 128;                 // final block of B2(P || sig)
+  // steps: [0, common) shared; common: final of B2(P); common+1 ..: rest of B2(P || sig)
+  const uint64_t nsteps = last + 2;
+  auto blk = [&](uint64_t s, uint64_t& lim) -> uint64_t {
+    if (s == common) {
+      lim = L;
+      return common;
+    }
+    lim = LD;
+    return s < common ? s : s - 1;
+  };
+  uint64_t h[8], hs[8], m[16], mn[16];
+  b2_init256(h);
+  uint64_t lim;
+  b2_load_block(m, p, blk(0, lim), lim);
+  for (uint64_t s = 0; s < nsteps; s++) {
+    uint64_t lim_n;
+    const uint64_t bn = blk(s + 1 < nsteps ? s + 1 : s, lim_n);
+    b2_load_block(mn, p, bn, lim_n);
+    const bool msg_final = s == common;
+    const uint64_t b = s < common ? s : (msg_final ? common : s - 1);
+    const bool fin = msg_final || b == last;
+    const uint64_t t = msg_final ? L : (b == last ? LD : 128 * (b + 1));
+    if (msg_final) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) hm[i] = h[i];
-  b2_load_block(m, p, common, L);
-  b2_compress(hm, m, L, true);
-  b2_store256(msg_out + 32 * (size_t)gid, hm);
-  const uint64_t LD = L + 64;
-  const uint64_t last = (LD - 1) / 128;
-  for (uint64_t b = common; b < last; b++) {
-    b2_load_block(m, p, b, LD);
-    b2_compress(h, m, 128 * (b + 1), false);
+      for (int i = 0; i < 8; i++) hs[i] = h[i];
+    }
+    b2_compress(h, m, t, fin);
+    if (msg_final) {
+      b2_store256(msg_out + 32 * (size_t)gid, h);
+#pragma unroll
+      for (int i = 0; i < 8; i++) h[i] = hs[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = mn[j];
   }
-  b2_load_block(m, p, last, LD);
-  b2_compress(h, m, LD, true);
   b2_store256(dig_out + 32 * (size_t)gid, h);
 }
 
