@@ -1,0 +1,253 @@
+// BLAKE2b-256 for gfx950 with FOUR lanes per string (blake2 0.10.6
+// Blake2b<U32> as crypto.rs:34-61 and :174-189 use it; RFC 7693 with nn = 32, kk = 0).
+//
+// Lane q of a quad holds column q of the 4x4 working matrix, (v[q], v[4+q], v[8+q], v[12+q]),
+// and runs one G per half-round: the column step as is, the diagonal step after rotating the
+// b, c, d rows across the quad by 1, 2, 3 lanes (DPP quad_perm, full rate) and back. The
+// message block sits in LDS (128 B per string, double-buffered, each lane loads a quarter of
+// the next block from HBM during the current compression); each lane reads the four words
+// its G's add in a round at SIGMA-derived indices.
+//
+// Why four lanes: a compression is a chain of 12 rounds, so a lane-per-string kernel runs
+// each string's 96 G's back to back. Four lanes cut that chain 4x (the latency path, 64
+// blocks per call, is bound by it) and shrink the state to 8 VGPRs + 4 for h, so the
+// throughput kernel runs at full occupancy instead of ~160 VGPRs per lane.
+//
+// 64-bit adds are v_lshl_add_u64 (one half-rate instruction, not an add/addc pair); the 24-
+// and 16-bit rotations are byte permutes (v_perm_b32); 32 is a register swap.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+#ifndef MV_DEV
+#define MV_DEV __device__ __forceinline__
+#endif
+
+namespace mv {
+namespace b2q {
+
+// RFC 7693 §2.7 message schedule (rounds 10 and 11 reuse rows 0 and 1)
+constexpr uint8_t SIGMA[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+// The message word lane q adds in round r, slot k (0/1: column step x/y, 2/3: diagonal step
+// x/y) is SIGMA[r][8 (k >> 1) + 2q + (k & 1)]; packed 4 bits per lane.
+constexpr uint32_t msel(int r, int k) {
+  uint32_t c = 0;
+  for (int q = 0; q < 4; q++) c |= (uint32_t)SIGMA[r][8 * (k >> 1) + 2 * q + (k & 1)] << (4 * q);
+  return c;
+}
+struct Sel {
+  uint32_t v[12][4];
+};
+constexpr Sel make_sel() {
+  Sel s{};
+  for (int r = 0; r < 12; r++)
+    for (int k = 0; k < 4; k++) s.v[r][k] = msel(r, k);
+  return s;
+}
+constexpr Sel SEL = make_sel();
+
+constexpr uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                            0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                            0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+MV_DEV uint64_t add64(uint64_t a, uint64_t b) {
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+MV_DEV uint64_t pack(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+MV_DEV uint64_t ror32(uint64_t x) { return (x >> 32) | (x << 32); }
+MV_DEV uint64_t ror24(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_perm(hi, lo, 0x06050403u), __builtin_amdgcn_perm(lo, hi, 0x06050403u));
+}
+MV_DEV uint64_t ror16(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_perm(hi, lo, 0x05040302u), __builtin_amdgcn_perm(lo, hi, 0x05040302u));
+}
+MV_DEV uint64_t ror63(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_alignbit(lo, hi, 31), __builtin_amdgcn_alignbit(hi, lo, 31));
+}
+// lane q of each quad takes x from lane (q + K) & 3
+template <int K>
+MV_DEV uint64_t qrot(uint64_t x) {
+  constexpr int ctrl = ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, ctrl, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), ctrl, 0xf, 0xf, false);
+  return pack(lo, hi);
+}
+
+#define MV_QG(x, y)         \
+  a = add64(add64(a, b), x); \
+  d = ror32(d ^ a);          \
+  c = add64(c, d);           \
+  b = ror24(b ^ c);          \
+  a = add64(add64(a, b), y); \
+  d = ror16(d ^ a);          \
+  c = add64(c, d);           \
+  b = ror63(b ^ c);
+
+// One compression of the quad's block m[16] (LDS). (h0, h1) = (h[q], h[4 + q]); (iv0, iv1) =
+// (IV[q], IV[4 + q]); t = byte counter (< 2^64), fin = final block.
+MV_DEV void compress(uint64_t& h0, uint64_t& h1, const uint64_t* m, uint32_t q, uint64_t iv0, uint64_t iv1,
+                     uint64_t t, bool fin) {
+  uint64_t a = h0, b = h1, c = iv0, d = iv1;
+  d ^= q == 0 ? t : 0ull;            // v[12] ^= t (t_hi = 0: v[13] unchanged)
+  d = (q == 2 && fin) ? ~d : d;      // v[14] = ~v[14] on the final block
+  const uint32_t sh = 4 * q;
+#pragma unroll
+  for (int r = 0; r < 12; r++) {
+    const uint64_t x0 = m[(SEL.v[r][0] >> sh) & 15u], y0 = m[(SEL.v[r][1] >> sh) & 15u];
+    const uint64_t x1 = m[(SEL.v[r][2] >> sh) & 15u], y1 = m[(SEL.v[r][3] >> sh) & 15u];
+    MV_QG(x0, y0)
+    b = qrot<1>(b);
+    c = qrot<2>(c);
+    d = qrot<3>(d);
+    MV_QG(x1, y1)
+    b = qrot<3>(b);
+    c = qrot<2>(c);
+    d = qrot<1>(d);
+  }
+  h0 ^= a ^ c;
+  h1 ^= b ^ d;
+}
+#undef MV_QG
+
+MV_DEV uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, m));
+  return x;
+}
+
+// What step s of a string hashes. DUAL (the block path, staged P || sig with L = |P|):
+// steps [0, common) are the compressions B2(P) and B2(P || sig) share, step `common` is the
+// final block of B2(P) (msg), steps after it finish B2(P || sig) (digest). Otherwise one
+// hash of L bytes. Steps at or past the string's count load nothing (lim = 0).
+template <bool DUAL>
+struct Plan {
+  uint64_t L, common, last;
+  uint32_t nsteps;
+  MV_DEV void init(uint64_t len, bool live) {
+    L = len;
+    if (DUAL) {
+      common = L == 0 ? 0 : (L - 1) / 128;
+      last = (L + 63) / 128;
+      nsteps = live ? (uint32_t)(last + 2) : 0u;
+    } else {
+      common = ~0ull;
+      last = L == 0 ? 0 : (L - 1) / 128;
+      nsteps = live ? (uint32_t)(last + 1) : 0u;
+    }
+  }
+  // block index, length limit, counter, final flag, msg-final flag
+  MV_DEV void at(uint32_t s, uint64_t& b, uint64_t& lim, uint64_t& t, bool& fin, bool& mfin) const {
+    if (DUAL) {
+      mfin = s == common;
+      b = s < common ? s : (mfin ? common : s - 1);
+      lim = mfin ? L : L + 64;
+      fin = mfin || b == last;
+      t = mfin ? L : (b == last ? L + 64 : 128 * (b + 1));
+    } else {
+      mfin = false;
+      b = s;
+      lim = L;
+      fin = b == last;
+      t = fin ? L : 128 * (b + 1);
+    }
+    if (s >= nsteps) lim = 0;
+  }
+};
+
+// Lane q's quarter (words 4q .. 4q+3) of block b, zero past lim; a word is read only when it
+// starts below lim (the strings are 8-aligned and readable up to round-up(lim, 8)).
+MV_DEV void load_quarter(uint64_t w[4], const uint8_t* p, uint64_t b, uint64_t lim, uint32_t q) {
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + b * 16 + 4 * q;
+  const uint64_t base = b * 128 + 32 * q;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint64_t pos = base + 8 * j;
+    uint64_t v = 0;
+    if (pos < lim) {
+      v = src[j];
+      const uint64_t rem = lim - pos;
+      if (rem < 8) v &= (1ull << (8 * rem)) - 1;
+    }
+    w[j] = v;
+  }
+}
+
+// 16 strings per 64-lane workgroup. DUAL: out0 = B2(P) (msg), out1 = B2(P || sig) (digest);
+// otherwise out0 = B2(string).
+template <bool DUAL>
+__global__ void __launch_bounds__(64) k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                                                const uint64_t* __restrict__ len, uint32_t n,
+                                                uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
+  __shared__ uint64_t mbuf[2][16][16];  // [buffer][string][word]
+  const uint32_t lane = threadIdx.x, q = lane & 3, qd = lane >> 2;
+  const uint32_t i = blockIdx.x * 16 + qd;
+  const bool live = i < n;
+  const uint8_t* p = buf + (live ? off[i] : 0);
+  Plan<DUAL> pl;
+  pl.init(live ? len[i] : 0, live);
+  const uint32_t nmax = wave_max(pl.nsteps);
+  const uint64_t iv0 = IV[q], iv1 = IV[4 + q];
+  uint64_t h0 = iv0 ^ (q == 0 ? 0x01010020ull : 0ull), h1 = iv1;  // depth 1, fanout 1, nn = 32
+
+  uint64_t b, lim, t;
+  bool fin, mfin;
+  uint64_t w[4];
+  pl.at(0, b, lim, t, fin, mfin);
+  load_quarter(w, p, b, lim, q);
+#pragma unroll
+  for (int j = 0; j < 4; j++) mbuf[0][qd][4 * q + j] = w[j];
+  for (uint32_t s = 0; s < nmax; s++) {
+    __syncthreads();
+    uint64_t bn, limn, tn;
+    bool finn, mfinn;
+    pl.at(s + 1, bn, limn, tn, finn, mfinn);
+    load_quarter(w, p, bn, limn, q);  // next block, in flight during this compression
+    pl.at(s, b, lim, t, fin, mfin);
+    const uint64_t s0 = h0, s1 = h1;
+    compress(h0, h1, mbuf[s & 1][qd], q, iv0, iv1, t, fin);
+    if (DUAL && mfin && s < pl.nsteps) reinterpret_cast<uint64_t*>(out0 + 32 * (size_t)i)[q] = h0;
+    if ((DUAL && mfin) || s >= pl.nsteps) {  // msg stored / string already done: keep h
+      h0 = s0;
+      h1 = s1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][qd][4 * q + j] = w[j];
+  }
+  if (live) reinterpret_cast<uint64_t*>((DUAL ? out1 : out0) + 32 * (size_t)i)[q] = h0;
+}
+
+}  // namespace b2q
+}  // namespace mv
+
+namespace mvk {
+
+hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::b2q::k_b2_quad<false>, dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, out,
+                     (uint8_t*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                                  uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::b2q::k_b2_quad<true>, dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, msg_out,
+                     dig_out);
+  return hipGetLastError();
+}
+
+}  // namespace mvk

@@ -594,15 +594,25 @@ hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, cons
   hipLaunchKernelGGL(mv::k_sign, dim3((n + 255) / 256), dim3(256), 0, s, seed, msg, n, (const uint4*)btab, pk, sig);
   return hipGetLastError();
 }
+// A/B switch: MV_HASH_LANE=1 runs the lane-per-string hash kernels instead of blake2b_quad.hip
+static bool hash_lane_kernels() {
+  static const bool v = [] {
+    const char* e = getenv("MV_HASH_LANE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                           hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (!hash_lane_kernels()) return launch_blake2b_quad(buf, off, len, n, out, s);
   hipLaunchKernelGGL(mv::k_blake2b, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, out);
   return hipGetLastError();
 }
 hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                              uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (!hash_lane_kernels()) return launch_block_hash_quad(buf, off, len, n, msg_out, dig_out, s);
   hipLaunchKernelGGL(mv::k_block_hash, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, msg_out, dig_out);
   return hipGetLastError();
 }

@@ -145,3 +145,35 @@ def test_device_resident_api(engine, golden):
     assert (d_st.cpu().numpy() == 0).all()
     assert hashlib.sha256(d_md.cpu().numpy().tobytes()).hexdigest() == g["sha256_msg_digests"]
     assert hashlib.sha256(d_bd.cpu().numpy().tobytes()).hexdigest() == g["sha256_block_digests"]
+
+
+def test_blocks_beyond_the_lds_window(engine, host_engine):
+    """Blocks whose bincode exceeds k_block_ingest's 10 KB LDS window take its one-lane
+    path over global memory; mixed with window-sized blocks, corrupted and truncated ones."""
+    pks, stakes = small_committee()
+    seeds = [B.authority_seed(a) for a in range(7)]
+    prev = [B.genesis(a) for a in range(7)]
+    rng = np.random.default_rng(77)
+    out = []
+    for r in range(1, 5):
+        cur = []
+        for a in range(7):
+            inc = [prev[a].reference()] + [prev[x].reference() for x in range(7) if x != a][:5]
+            big = int(rng.integers(9000, 40000)) if (a + r) % 2 else int(rng.integers(0, 3000))
+            sts = [("share", bytes(rng.integers(0, 256, size=big, dtype=np.uint8)))]
+            sts += [("range", prev[(a + 2) % 7].reference(), 0, 3)] * 4
+            cur.append(B.new_with_signer(a, r, inc, sts, r, False, 0, seeds[a], O.sign))
+        out += [b.bincode() for b in cur]
+        prev = cur
+    big = [b for b in out if len(b) > 10240]
+    assert len(big) >= 8
+    bad = bytearray(big[0])
+    bad[len(bad) // 2] ^= 4  # digest mismatch inside the share payload
+    out += [bytes(bad), big[1][:-1], big[2][: len(big[2]) // 2]]
+    st, md, bd = agree(engine, host_engine, out, pks, stakes, 0)
+    for i in range(len(out)):
+        ost, omd, obd = O.block_verify(out[i], pks, stakes, 0)
+        assert int(st[i]) == ost, i
+        if ost != O.BLOCK_PARSE_ERROR:
+            assert md[i].tobytes() == omd and bd[i].tobytes() == obd, i
+    assert int(st[-3]) == M.BLOCK_DIGEST_MISMATCH and int(st[-2]) == M.BLOCK_PARSE_ERROR

@@ -171,3 +171,17 @@ def test_second_fixed_base_table(engine):
     out = engine.selftest(14, w)
     for k, o in zip(ks, out):
         assert o[:8].astype("<u4").tobytes() == Z.compress(Z.scalarmult(Z.B_POINT, k * 2**124 % Z.L)), k
+
+
+def test_blake2b_ragged_lengths(engine):
+    """Every length 0..700 and some up to 40 KB in one call: the 16 strings of a quad-kernel
+    workgroup run different step counts (RFC 7693, checked with hashlib)."""
+    import hashlib
+
+    rng = np.random.default_rng(9)
+    lens = list(range(0, 701)) + [int(x) for x in rng.integers(700, 40000, size=60)]
+    rng.shuffle(lens)
+    items = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    out = engine.blake2b256(items)
+    for it, o in zip(items, out):
+        assert bytes(o) == hashlib.blake2b(it, digest_size=32).digest(), len(it)
