@@ -382,19 +382,21 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
     return;
   }
   {
-    // 16 loads in flight per lane before their LDS stores (a store right behind each load
-    // would serialise the HBM latency 19 times for a 9.5-KB block)
+    // every load of the window in flight at once (IG_LOADS per lane) before the LDS stores:
+    // a store right behind each load would serialise the HBM latency 19 times for a 9.5-KB
+    // block, and 16 per lane still took two rounds for it. The fit test above bounds nw by
+    // IG_WIN / 8 = 64 * IG_LOADS, so one round always covers the block.
+    constexpr int IG_LOADS = IG_WIN / 8 / 64;
+    static_assert(IG_WIN % 512 == 0, "the window is whole 64-lane rounds of 8-byte loads");
     const uint64_t* src = reinterpret_cast<const uint64_t*>(buf + (o - d));
     uint64_t* w64 = reinterpret_cast<uint64_t*>(win);
     const uint32_t nw = (uint32_t)((d + L + 15) >> 3);
-    for (uint32_t k0 = lane; k0 < nw; k0 += 64 * 16) {
-      uint64_t t[16];
+    uint64_t t[IG_LOADS];
 #pragma unroll
-      for (int j = 0; j < 16; j++) t[j] = k0 + 64 * j < nw ? src[k0 + 64 * j] : 0ull;
+    for (int j = 0; j < IG_LOADS; j++) t[j] = lane + 64 * j < nw ? src[lane + 64 * j] : 0ull;
 #pragma unroll
-      for (int j = 0; j < 16; j++)
-        if (k0 + 64 * j < nw) w64[k0 + 64 * j] = t[j];
-    }
+    for (int j = 0; j < IG_LOADS; j++)
+      if (lane + 64 * j < nw) w64[lane + 64 * j] = t[j];
   }
   __syncthreads();
   const uint32_t Lb = (uint32_t)L;
