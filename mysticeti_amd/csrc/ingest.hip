@@ -427,10 +427,12 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
       const uint32_t p = 64 + 56 * k;
       const uint64_t a = rd64(p), r = rd64(p + 8);
       bad |= rd64(p + 16) != 32;
-      const uint32_t q = 16 + 48 * k;
-      pre_be64(pre, q, a);
-      pre_be64(pre, q + 8, r);
-      pre_copy32(pre, q + 16, win, d + p + 24);
+      // pre-image offset 16 + 48 k is 8-byte aligned: six 64-bit LDS stores, not 48 byte stores
+      uint64_t* pq = pre64 + 2 + 6 * k;
+      pq[0] = __builtin_bswap64(a);  // big-endian u64 (pre_be64)
+      pq[1] = __builtin_bswap64(r);
+#pragma unroll
+      for (int m = 0; m < 4; m++) pq[2 + m] = rd64(p + 24 + 8 * m);  // digest bytes as they lie
       const uint32_t code = a >= n_auth ? MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY : (r >= me_r ? MV_BLOCK_INCLUDE_ROUND : 0u);
       if (code && inc_first == 0xffffffffu) inc_first = (k << 4) | code;
       if (me_r > 0 && r == me_r - 1 && a < n_auth) atomicOr(&seen[(uint32_t)a >> 5], 1u << (a & 31));
