@@ -154,6 +154,14 @@ struct BvKey {
   uint32_t w[10];  // 32-byte secret, 64-bit call counter
 };
 
+// Committee keys (block path): A of key b is entry [0][1] = [1](-A_b) of its comb table
+// (comb.hip, built by mv_set_committee with the same ZIP-215 decode), negated here.
+struct CommitteeA {
+  const uint4* tab;  // nullptr: decode A per signature
+  const uint8_t* ok;
+  uint32_t stride;   // uint4 per key table
+};
+
 // one decode at a time at 3 waves/SIMD beat two decodes in lock-step at 2 (seq3 vs
 // x2 A/B on MI355X: 241 vs 220 M verifies/s for the whole batch path)
 #ifndef MV_PREP_X2
@@ -164,7 +172,7 @@ struct BvKey {
 #endif
 __global__ void __launch_bounds__(256, MV_PREP_OCC)
     k_bv_prep(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
-              const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, uint4* __restrict__ pts,
+              const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, CommitteeA ca, uint4* __restrict__ pts,
               uint4* __restrict__ scal, unsigned long long* __restrict__ bsum_part, uint8_t* __restrict__ status) {
   __shared__ unsigned long long sbsum[BSUM_WORDS];
   if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
@@ -174,7 +182,8 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
   const uint32_t idx = live ? gid : n - 1;
 
   uint32_t aw[8], rw[8], sw[8], mw[8];
-  load8(aw, pk + 32 * (size_t)(key_idx ? key_idx[idx] : idx));
+  const uint32_t kid = key_idx ? key_idx[idx] : idx;
+  load8(aw, pk + 32 * (size_t)kid);
   load8(rw, sig + 64 * (size_t)idx);
   load8(sw, sig + 64 * (size_t)idx + 32);
   load8(mw, msg + 32 * (size_t)idx);
@@ -225,6 +234,21 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
   bool okA, okR;
   {
     precomp pc;
+    if (ca.tab) {  // committee key: R is the only decode
+      p3 P;
+      decompress1(P, okR, rw);
+      precomp_from_affine(pc, P);
+      if (live) pt_store(pts, gid, pc);
+      const uint4* e = ca.tab + (size_t)kid * ca.stride + 8;  // row 0, entry 1 (8 uint4 per entry)
+      uint4 q[7];
+#pragma unroll
+      for (int k = 0; k < 7; k++) q[k] = e[k];
+      quads_to_precomp(pc, q);
+      precomp_cneg(pc, true);  // -(-A) = A
+      fe_canon(pc.xy2d, pc.xy2d);
+      okA = ca.ok[kid] != 0;
+      if (live) pt_store(pts, (size_t)n + gid, pc);
+    } else {
 #ifdef MV_PREP_SEQ  // experiment: one decode at a time (fewer registers, more waves)
     p3 P;
     decompress1(P, okR, rw);
@@ -241,6 +265,7 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     precomp_from_affine(pc, A);
     if (live) pt_store(pts, (size_t)n + gid, pc);
 #endif
+    }
   }
   const bool ok = live && okA && okR && s_ok;
   if (live) {
@@ -620,7 +645,7 @@ size_t batch_scratch_bytes(uint32_t n) { return BatchLayout(n).total; }
 hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                                uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
                                void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out,
-                               hipEvent_t* ev) {
+                               hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
@@ -649,7 +674,10 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   for (int i = 0; i < 10; i++) k.w[i] = key[i];
   const uint32_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
   mark(0);
-  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, pts, scal, bsum, status);
+  CommitteeA ca{key_idx && key_ok ? static_cast<const uint4*>(comb_a) : nullptr, key_ok,
+                (uint32_t)(comb_table_bytes(1) / sizeof(uint4))};
+  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,
+                     status);
   mark(1);
   hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, pcount);
   hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART / 64), dim3(256), 0, s, pcount, nchunk, poff, ptot);

@@ -195,8 +195,12 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   std::vector<hipEvent_t> evs;
   mv_status st = make_events(ctx, mvk::BATCH_STAGES, evs);
   if (st != MV_OK) return st;
+  // committee keys: A comes from the comb tables built at mv_set_committee (no per-signature decode)
+  const bool com_a = d_key_idx && dev.committee_loaded && d_pk == dev.committee_pk.as<uint8_t>() &&
+                     !(ctx->flags & MV_FLAG_NO_COMB);
   HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscr[slot].p,
-                                       dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data()));
+                                       dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
+                                       com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr));
   keep_events(ctx, dev.id, 0, evs);
   if (flag_dst)
     HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, flag_dst_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, s));

@@ -162,3 +162,33 @@ def test_device_api_flag(engine):
     torch.cuda.synchronize()
     st = dst.cpu().numpy()
     assert int(ok.item()) == 0 and st[17] == 1 and (np.delete(st, 17) == 0).all()
+
+
+def test_committee_keys_batch_equation_uses_comb_a(engine, golden):
+    """With committee keys the batch path reads A from the comb tables of mv_set_committee
+    (no per-signature A decode). The combined equation must still hold for valid rows and
+    for the ZIP-215 edge-case keys (small-order, non-canonical), and a key that does not
+    decode must give MalformedPublicKey (status 2) without failing the combination."""
+    cases = [c for c in golden("zip215_corpus.json") if len(c["msg"]) == 64 and c["status"] in (0, 2)]
+    rng = np.random.default_rng(11)
+    seeds = rng.integers(0, 256, size=(7, 32), dtype=np.uint8)
+    n = 6000
+    ki = rng.integers(0, 7, size=n).astype(np.uint32)
+    msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    pk, sig = engine.ed25519_sign(seeds[ki], msg)
+    keys = [bytes(pk[int(np.nonzero(ki == a)[0][0])]) for a in range(7)]
+    for c in cases:
+        if bytes.fromhex(c["pk"]) not in keys:
+            keys.append(bytes.fromhex(c["pk"]))
+    assert len(keys) <= 512
+    com = np.frombuffer(b"".join(keys), dtype=np.uint8).reshape(-1, 32)
+    engine.set_committee(com, np.ones(len(keys), np.uint64))
+    cki = np.array([keys.index(bytes.fromhex(c["pk"])) for c in cases], np.uint32)
+    msg = np.concatenate([msg, arr([c["msg"] for c in cases], 32)])
+    sig = np.concatenate([sig, arr([c["sig"] for c in cases], 64)])
+    ki = np.concatenate([ki, cki])
+    want = np.concatenate([np.zeros(n, np.uint8), np.array([c["status"] for c in cases], np.uint8)])
+    st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, key_idx=ki))
+    assert nb == 1 and nf == 0
+    assert (st == want).all()
+    assert (want == 2).any()
