@@ -137,6 +137,8 @@ def main():
                          "config4: HBM-resident 100-validator blocks through the device block pipeline; "
                          "config5: p50/p99 latency of 64-block batches, GPU vs host cores")
     ap.add_argument("--batches", type=int, default=10000, help="config5: GPU batches timed per shape")
+    ap.add_argument("--corrupt", type=int, default=0, help="signatures per batch with a flipped s bit")
+    ap.add_argument("--groups", type=int, default=0, help="sub-batch equations per batch (0 = adaptive)")
     args = ap.parse_args()
     if args.workload != "config2":
         import bench_blocks
@@ -180,6 +182,13 @@ def main():
     torch.cuda.synchronize(dev)  # the H2D copies above ran on the default stream
     eng.dev_sign(local_rank, d_seed, d_msg, d_pk, d_sig, streams[0].cuda_stream)
     torch.cuda.synchronize(dev)
+    bad_idx = None
+    if args.corrupt:
+        bad_idx = torch.linspace(0, n - 1, args.corrupt, device=dev).long() if args.corrupt > 1 else \
+            torch.tensor([n // 3], device=dev)
+        d_sig[bad_idx, 40] ^= 0x10  # s bit: s stays < l, R decodes -> only the equation catches it
+    if args.groups:
+        eng.set_batch_groups(args.groups)
 
     state = {"i": 0}
 
@@ -240,9 +249,14 @@ def main():
 
     status = d_status[(args.warmup + args.steps - 1) % nstreams].cpu().numpy()
     accepted = int((status == 0).sum())
-    ok = accepted == n and all((x.cpu().numpy() == 0).all() for x in d_status)
+    if bad_idx is None:
+        ok = accepted == n and all((x.cpu().numpy() == 0).all() for x in d_status)
+    else:
+        want = np.zeros(n, np.uint8)
+        want[bad_idx.cpu().numpy()] = 1
+        ok = all((x.cpu().numpy() == want).all() for x in d_status)
     parity = None
-    if rank == 0 and n == (1 << 20):
+    if rank == 0 and n == (1 << 20) and bad_idx is None:
         gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_config2.json")))
         parity = hashlib.sha256(status.tobytes()).hexdigest() == gold["sha256_status"] and \
             hashlib.sha256(d_sig.cpu().numpy().tobytes()).hexdigest() == gold["sha256_sig"]

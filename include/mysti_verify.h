@@ -153,6 +153,15 @@ mv_status mv_dev_verify_blocks(mv_ctx* ctx, int device, const uint8_t* d_buf, ui
 /* Host-buffer batch-path counters since mv_create: batches tried, batches whose combined
  * equation failed (and were re-verified signature by signature). */
 mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks);
+/* batch counters: out[0] batches, out[1] batches whose combined equation failed in some
+ * sub-batch, out[2] sub-batch equations checked, out[3] sub-batch equations that failed
+ * (each re-verified signature by signature). Device-API calls are counted once complete. */
+mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out /* 4 */);
+/* Sub-batch equations per batch-path call. groups = 0 (default): adaptive -- one combined
+ * equation per batch; after a batch whose equation failed, the next 64 batches are cut into
+ * 8 sub-batches (whole 1024-signature chunks) with one equation each, so a bad signature
+ * re-verifies only its sub-batch. groups = 1..16 fixes the count. Verdicts never depend on it. */
+mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups);
 /* Stage timing: when enabled, every call records HIP events on its stream around its
  * stages: batch path 0..5 (prep, sort, bucket, reduce, final, fallback), block pipeline
  * 6..9 (parse, hash, verify = comb/ladder verify when the batch path is not taken, verdict).

@@ -39,7 +39,7 @@ EXPORTS = [
     "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
-    "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks",
+    "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
 ]
 # batch path stages, then the block pipeline's (mv_stage_times order, MV_NSTAGES)
 STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback", "parse", "hash", "verify", "verdict"]
@@ -81,6 +81,8 @@ def load_library(path: str = LIB_PATH):
     lib.mv_dev_ed25519_verify.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
     lib.mv_dev_ed25519_verify_batch.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, u32, vp, vp, vp]
     lib.mv_batch_stats.argtypes = [vp, vp, vp]
+    lib.mv_batch_counters.argtypes = [vp, vp]
+    lib.mv_set_batch_groups.argtypes = [vp, u32]
     lib.mv_set_stage_timing.argtypes = [vp, ctypes.c_int]
     lib.mv_stage_times.argtypes = [vp, vp, vp, ctypes.c_int]
     lib.mv_dev_verify_blocks.argtypes = [vp, ctypes.c_int, vp, u64, vp, vp, u32, vp, vp, vp, vp]
@@ -234,6 +236,16 @@ class Engine:
         b, f = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.lib.mv_batch_stats(self.ctx, ctypes.byref(b), ctypes.byref(f)), "mv_batch_stats")
         return b.value, f.value
+
+    def batch_counters(self) -> Tuple[int, int, int, int]:
+        """(batches, batches with a failed equation, sub-batch equations, failed sub-batch equations)."""
+        out = np.zeros(4, dtype=np.uint64)
+        self._check(self.lib.mv_batch_counters(self.ctx, _p(out)), "mv_batch_counters")
+        return tuple(int(x) for x in out)
+
+    def set_batch_groups(self, groups: int):
+        """Sub-batch equations per batch: 0 = adaptive (default), 1..16 fixed."""
+        self._check(self.lib.mv_set_batch_groups(self.ctx, int(groups)), "mv_set_batch_groups")
 
     def set_stage_timing(self, enable: bool = True):
         self._check(self.lib.mv_set_stage_timing(self.ctx, 1 if enable else 0), "mv_set_stage_timing")

@@ -21,10 +21,13 @@
 //                 affine points (y+x, y-x, 2dxy) to HBM, sum z_i s_i
 //   k_part_*, k_fine_sort   two-pass counting sort of the (bucket, point) entries
 //                 (LDS histograms and ranks; no global atomics)
-//   k_bv_bucket   lane per bucket (segment of BV_G buckets) of a window: bucket sums and the
-//                 segment's running sums (V = sum (b - b0) B_b, T = sum B_b)
-//   k_bv_reduce   tree over segments (fan-in 8) of the pairs (V, T) per window
+//   k_bv_bucket   lane per bucket: the bucket's sum T
+//   k_bv_reduce   tree over the buckets (fan-in 8) of the pairs (V, T) per window
 //   k_bv_final    Horner over the 16 window sums, -[sum z s]B, [8], identity test
+// Sub-batch equations: the batch may be cut into up to BV_MAXG groups of whole 1024-
+// signature chunks, each with its own buckets and its own combined equation (one flag per
+// group). The fallback then re-verifies only the groups whose equation failed, so k bad
+// signatures cost at most k groups of single verifies instead of the whole batch.
 // Windows: signed radix 2^16, |digit| <= 2^15; R scalars (z < 2^127) use windows 0..7,
 // A scalars (< l < 2^253) windows 0..15.
 #include <hip/hip_runtime.h>
@@ -43,13 +46,11 @@ constexpr int BV_C = 16;                    // window bits
 constexpr int BV_NB = 1 << (BV_C - 1);      // bucket magnitudes 1..2^15 per window
 constexpr int BV_NW = 16;                   // windows
 constexpr int BV_NWR = 8;                   // windows of the 127-bit R scalars
-constexpr int BV_NK = BV_NW * BV_NB;        // bucket keys, key = w * NB + |d| - 1
-constexpr int BV_G = 1;                     // buckets per segment lane
+constexpr uint32_t BV_NKG = BV_NW * BV_NB;  // bucket keys per group, key = w * NB + |d| - 1
 constexpr int BV_FINE_BITS = 8;             // bucket sort: partition = key >> 8 (window +
-constexpr int BV_NPART = BV_NK >> BV_FINE_BITS;  // 7 high magnitude bits), then 256 buckets
-constexpr int BV_SEGW = BV_NB / BV_G;       // segments per window
-constexpr int BV_NSEG = BV_NW * BV_SEGW;
+constexpr int BV_NPG = BV_NKG >> BV_FINE_BITS;  // 7 high magnitude bits), then 256 buckets
 constexpr int BV_FAN = 8;                   // reduction fan-in
+constexpr int BV_MAXG = mvk::BATCH_MAX_GROUPS;  // sub-batch equations per batch
 constexpr int PT_QUADS = 7;                 // precomp point, 27 words + pad
 constexpr int P3_QUADS = 9;
 constexpr int SC_QUADS = 3;                 // z (4 words), z*k mod l (8 words)
@@ -314,6 +315,10 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
 //                              partition, runs ordered by chunk, ranks from LDS atomics
 //   k_fine_sort                workgroup per partition: counting sort by the low 8 key
 //                              bits in LDS -> final bucket lists and bucket offsets
+// Sub-batches (groups): the batch's chunks are cut into `count` contiguous groups of `cpg`
+// chunks, and every group has its own buckets (key = g * BV_NKG + local key), so the
+// pipeline checks one combined equation per group. A chunk lies inside one group, so the
+// per-chunk counts stay group-local (BV_NPG partitions per chunk).
 template <int NT = 256>
 MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
   const int t = threadIdx.x;
@@ -333,6 +338,11 @@ MV_DEV uint32_t block_excl_scan256(uint32_t v, uint32_t* sm, uint32_t& total) {
 
 constexpr int PART_CHUNK = 1024;  // signatures per k_part_count / k_part_scatter block
 
+struct BvGroups {
+  uint32_t count;  // groups (sub-batch equations)
+  uint32_t cpg;    // chunks per group: signature i is in group i / (cpg * PART_CHUNK)
+};
+
 MV_DEV void load_scalars(uint32_t z[4], uint32_t zk[8], const uint4* scal, uint32_t i) {
   const uint4* sc = scal + (size_t)i * SC_QUADS;
   const uint4 q0 = sc[0], q1 = sc[1], q2 = sc[2];
@@ -340,11 +350,11 @@ MV_DEV void load_scalars(uint32_t z[4], uint32_t zk[8], const uint4* scal, uint3
   zk[0] = q1.x; zk[1] = q1.y; zk[2] = q1.z; zk[3] = q1.w;
   zk[4] = q2.x; zk[5] = q2.y; zk[6] = q2.z; zk[7] = q2.w;
 }
-// chunk c = 1024 signatures: entries per partition -> pcount[c][p] (LDS atomics only)
+// chunk c = 1024 signatures: entries per (group-local) partition -> pcount[c][p]
 __global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restrict__ scal, uint32_t n,
                                                            uint32_t* __restrict__ pcount) {
-  __shared__ uint32_t hist[BV_NPART];
-  for (int i = threadIdx.x; i < BV_NPART; i += PART_CHUNK) hist[i] = 0;
+  __shared__ uint32_t hist[BV_NPG];
+  for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) hist[i] = 0;
   __syncthreads();
   const uint32_t gid = blockIdx.x * PART_CHUNK + threadIdx.x;
   if (gid < n) {
@@ -353,81 +363,89 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restri
     bv_for_digits(z, zk, [&](int w, int d, int) { atomicAdd(&hist[bv_key(w, d) >> BV_FINE_BITS], 1u); });
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < BV_NPART; i += PART_CHUNK) pcount[(size_t)blockIdx.x * BV_NPART + i] = hist[i];
+  for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) pcount[(size_t)blockIdx.x * BV_NPG + i] = hist[i];
 }
-// block b: partitions [64b, 64b + 64), 4 chunk groups; row reads are 256-B coalesced.
-// poff[c][p] = entries of partition p in chunks < c; ptot[p] = partition size.
-__global__ void __launch_bounds__(256) k_part_scan(const uint32_t* __restrict__ pcount, uint32_t nchunk,
+// block b: group b / 32, its partitions [64 (b % 32), + 64), 4 chunk subgroups of the
+// group's chunks; row reads are 256-B coalesced. poff[c][p] = entries of partition (g, p)
+// in the group's chunks before c; ptot[g * BV_NPG + p] = partition size.
+__global__ void __launch_bounds__(256) k_part_scan(const uint32_t* __restrict__ pcount, uint32_t nchunk, BvGroups G,
                                                    uint32_t* __restrict__ poff, uint32_t* __restrict__ ptot) {
   __shared__ uint32_t gsum[4][64];
-  const uint32_t pl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const uint32_t p = blockIdx.x * 64 + pl;
-  const uint32_t per = (nchunk + 3) / 4;
-  const uint32_t c0 = g * per, c1 = min(nchunk, c0 + per);
+  constexpr uint32_t BPG = BV_NPG / 64;
+  const uint32_t pl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x / BPG;
+  const uint32_t p = (blockIdx.x % BPG) * 64 + pl;
+  const uint32_t cg0 = g * G.cpg, cg1 = min(nchunk, cg0 + G.cpg);
+  const uint32_t per = (cg1 - cg0 + 3) / 4;
+  const uint32_t c0 = min(cg1, cg0 + q * per), c1 = min(cg1, c0 + per);
   uint32_t sum = 0;
-  for (uint32_t c = c0; c < c1; c++) sum += pcount[(size_t)c * BV_NPART + p];
-  gsum[g][pl] = sum;
+  for (uint32_t c = c0; c < c1; c++) sum += pcount[(size_t)c * BV_NPG + p];
+  gsum[q][pl] = sum;
   __syncthreads();
   uint32_t run = 0;
-  for (uint32_t k = 0; k < g; k++) run += gsum[k][pl];
+  for (uint32_t k = 0; k < q; k++) run += gsum[k][pl];
   for (uint32_t c = c0; c < c1; c++) {
-    const uint32_t v = pcount[(size_t)c * BV_NPART + p];
-    poff[(size_t)c * BV_NPART + p] = run;
+    const uint32_t v = pcount[(size_t)c * BV_NPG + p];
+    poff[(size_t)c * BV_NPG + p] = run;
     run += v;
   }
-  if (g == 3) ptot[p] = run;
+  if (q == 3) ptot[g * BV_NPG + p] = run;
 }
-// exclusive scan of the partition totals -> pstart[0..NPART]
-__global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ ptot, uint32_t* __restrict__ pstart) {
-  constexpr int PER = BV_NPART / 256;
+// exclusive scan of the partition totals (all groups) -> pstart[0..total]
+__global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ ptot, uint32_t total,
+                                                  uint32_t* __restrict__ pstart) {
   __shared__ uint32_t sm[256];
-  uint32_t v[PER], sum = 0;
-#pragma unroll
-  for (int i = 0; i < PER; i++) {
-    v[i] = ptot[PER * threadIdx.x + i];
-    sum += v[i];
+  const uint32_t per = total / 256;  // total is a multiple of BV_NPG
+  const uint32_t* src = ptot + (size_t)per * threadIdx.x;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per; i++) sum += src[i];
+  uint32_t all;
+  uint32_t run = block_excl_scan256(sum, sm, all);
+  for (uint32_t i = 0; i < per; i++) {
+    const uint32_t v = src[i];
+    pstart[(size_t)per * threadIdx.x + i] = run;
+    run += v;
   }
-  uint32_t total;
-  uint32_t run = block_excl_scan256(sum, sm, total);
-#pragma unroll
-  for (int i = 0; i < PER; i++) {
-    pstart[PER * threadIdx.x + i] = run;
-    run += v[i];
-  }
-  if (threadIdx.x == 0) pstart[BV_NPART] = total;
+  if (threadIdx.x == 0) pstart[total] = all;
 }
 __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __restrict__ scal, uint32_t n,
                                                              const uint32_t* __restrict__ poff,
-                                                             const uint32_t* __restrict__ pstart,
+                                                             const uint32_t* __restrict__ pstart, BvGroups G,
                                                              unsigned long long* __restrict__ tmp) {
-  __shared__ uint32_t rank[BV_NPART];
-  for (int i = threadIdx.x; i < BV_NPART; i += PART_CHUNK) rank[i] = 0;
+  __shared__ uint32_t rank[BV_NPG];
+  for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) rank[i] = 0;
   __syncthreads();
   const uint32_t gid = blockIdx.x * PART_CHUNK + threadIdx.x;
   if (gid < n) {
+    const uint32_t g = blockIdx.x / G.cpg;
     uint32_t z[4], zk[8];
     load_scalars(z, zk, scal, gid);
-    const uint32_t* po = poff + (size_t)blockIdx.x * BV_NPART;
+    const uint32_t* po = poff + (size_t)blockIdx.x * BV_NPG;
+    const uint32_t* ps = pstart + (size_t)g * BV_NPG;
     bv_for_digits(z, zk, [&](int w, int d, int isA) {
       const uint32_t key = bv_key(w, d);
       const uint32_t p = key >> BV_FINE_BITS;
       const uint32_t r = atomicAdd(&rank[p], 1u);
       const uint32_t pt = isA ? n + gid : gid;
-      tmp[pstart[p] + po[p] + r] = ((unsigned long long)key << 32) | (pt << 1) | (d < 0 ? 1u : 0u);
+      tmp[ps[p] + po[p] + r] = ((unsigned long long)(g * BV_NKG + key) << 32) | (pt << 1) | (d < 0 ? 1u : 0u);
     });
   }
 }
-// block p: the partition's entries sorted by bucket into ents; offs[key] for its 256
-// keys. One thread per bin; a partition's output window is ~64 KB, so the ranked
-// stores of the blocks in flight merge in L2. The biggest partitions (window 15's,
-// whose digits stop at 2^13) are scheduled first.
+// block -> partition P: the partition's entries sorted by bucket into ents; offs[key] for
+// its 256 keys. One thread per bin; a partition's output window is ~64 KB, so the ranked
+// stores of the blocks in flight merge in L2. The biggest partitions (window 15's, whose
+// digits stop at 2^13) of every group are scheduled first.
+constexpr uint32_t BV_PPW = BV_NB >> BV_FINE_BITS;  // partitions per window (128)
 __global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned long long* __restrict__ tmp,
-                                                    const uint32_t* __restrict__ pstart, uint32_t* __restrict__ ents,
-                                                    uint32_t* __restrict__ offs) {
+                                                    const uint32_t* __restrict__ pstart, uint32_t ngroups,
+                                                    uint32_t* __restrict__ ents, uint32_t* __restrict__ offs) {
   constexpr int NF = 1 << BV_FINE_BITS;
   __shared__ uint32_t cnt[NF];
   __shared__ uint32_t sm[NF];
-  const uint32_t p = BV_NPART - 1 - blockIdx.x;
+  const uint32_t span = ngroups * BV_PPW;
+  const uint32_t w = BV_NW - 1 - blockIdx.x / span;
+  const uint32_t g = (blockIdx.x % span) / BV_PPW;
+  const uint32_t p = g * BV_NPG + w * BV_PPW + blockIdx.x % BV_PPW;
   const uint32_t s = pstart[p], e = pstart[p + 1];
   cnt[threadIdx.x] = 0;
   __syncthreads();
@@ -437,7 +455,7 @@ __global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned 
   uint32_t total;
   const uint32_t ex = block_excl_scan256<NF>(c, sm, total);
   offs[(size_t)p * NF + threadIdx.x] = s + ex;
-  if (p == BV_NPART - 1 && threadIdx.x == 0) offs[BV_NK] = e;
+  if (p == ngroups * BV_NPG - 1 && threadIdx.x == 0) offs[(size_t)ngroups * BV_NKG] = e;
   cnt[threadIdx.x] = ex;
   __syncthreads();
   for (uint32_t i = s + threadIdx.x; i < e; i += NF) {
@@ -448,24 +466,21 @@ __global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned 
 }
 
 // ---------------------------------------------------------------- buckets
-// Lane = segment (w, j): buckets of magnitude j*G + 1 .. j*G + G. Running sums from
-// the top bucket: T = sum of the segment's buckets, V = sum (m - j*G) * B_m.
-// The window's sum is then sum_j (V_j + j*G * T_j) (k_bv_reduce). Windows are laid
-// out high-first in the grid (window 15's buckets hold twice the entries), and each
-// point is loaded one add ahead.
+// Lane = bucket (g, w, |d|): T = the sum of the bucket's points. Windows are laid out
+// high-first in the grid (window 15's buckets hold four times the entries), every group's
+// windows side by side, and each point is loaded one add ahead.
 __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
-                                                   const uint32_t* __restrict__ ents, uint4* __restrict__ segV,
+                                                   const uint32_t* __restrict__ ents, uint32_t ngroups,
                                                    uint4* __restrict__ segT) {
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lin >= (uint32_t)BV_NSEG) return;
-  const uint32_t sidx = (uint32_t)(BV_NW - 1 - lin / BV_SEGW) * BV_SEGW + lin % BV_SEGW;
-  const uint32_t key0 = sidx * BV_G;  // == w * NB + j * G
-  p3 T, S;
+  if (lin >= ngroups * BV_NKG) return;
+  const uint32_t span = ngroups * BV_NB;
+  const uint32_t w = BV_NW - 1 - lin / span;
+  const uint32_t key = ((lin % span) / BV_NB) * BV_NKG + w * BV_NB + lin % BV_NB;
+  p3 T;
   p3_identity(T);
-  p3_identity(S);
-  // entries are consumed from the segment's end (top bucket) down, one load ahead
-  const uint32_t e_lo = offs[key0], e_hi = offs[key0 + BV_G];
-  uint32_t e = e_hi;
+  const uint32_t e_lo = offs[key];
+  uint32_t e = offs[key + 1];
   uint4 q[7];
   uint32_t ent = 0;
   if (e > e_lo) {
@@ -475,49 +490,56 @@ __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts
 #pragma unroll
     for (int i = 0; i < 7; i++) q[i] = p[i];
   }
-  for (int b = BV_G - 1; b >= 0; b--) {
-    const uint32_t b0 = offs[key0 + b];
-    const uint32_t b1 = b == BV_G - 1 ? e_hi : offs[key0 + b + 1];
-    for (uint32_t k = b1; k > b0; k--) {
-      precomp pc;
-      quads_to_precomp(pc, q);
-      const bool neg = ent & 1u;
-      if (e > e_lo) {  // next point in flight during this add
-        e--;
-        ent = ents[e];
-        const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+  for (uint32_t k = offs[key + 1]; k > e_lo; k--) {
+    precomp pc;
+    quads_to_precomp(pc, q);
+    const bool neg = ent & 1u;
+    if (e > e_lo) {  // next point in flight during this add
+      e--;
+      ent = ents[e];
+      const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
 #pragma unroll
-        for (int i = 0; i < 7; i++) q[i] = p[i];
-      }
-      precomp_cneg(pc, neg);
-      p1p1 t;
-      p3_add_precomp(t, T, pc);
-      p1p1_to_p3(T, t);
+      for (int i = 0; i < 7; i++) q[i] = p[i];
     }
-    if (BV_G > 1) p3_acc(S, T);
+    precomp_cneg(pc, neg);
+    p1p1 t;
+    p3_add_precomp(t, T, pc);
+    p1p1_to_p3(T, t);
   }
-  if (BV_G == 1) S = T;  // one bucket: V = T (weight 1)
-  p3_store(segV, sidx, S);
-  p3_store(segT, sidx, T);
+  p3_store(segT, key, T);
 }
 
 // ---------------------------------------------------------------- reduction
-// Elements (V, T) of one window with indices m = 0..cnt-1 stand for V + (m * scale) T.
-// Groups of FAN consecutive elements m = FAN*q + t become one element with index q:
+// Rows = (group, window); row r holds cnt_in elements. Elements (V, T) with indices
+// m = 0..cnt-1 stand for V + (m * scale) T. Groups of FAN consecutive elements m = FAN*q + t
+// become one element with index q:
 //   V' = sum V_t + scale * sum_t t T_t,   T' = sum T_t,   scale' = FAN * scale.
 // scale is a power of two (log2 = shift): the multiplication is `shift` doublings.
+// First level (inV == nullptr): the elements are the buckets, m = |d| - 1, so V_m = T_m
+// and scale = 1: V' = sum_t (t + 1) T_t, the sum of the running sums.
 __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV, const uint4* __restrict__ inT,
-                                                  uint32_t cnt_in, int fan, int shift, uint4* __restrict__ outV,
-                                                  uint4* __restrict__ outT) {
+                                                  uint32_t cnt_in, int fan, int shift, uint32_t rows,
+                                                  uint4* __restrict__ outV, uint4* __restrict__ outT) {
   const uint32_t cnt_out = (cnt_in + fan - 1) / fan;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= cnt_out * BV_NW) return;
-  const uint32_t w = gid / cnt_out, q = gid % cnt_out;
-  const size_t base = (size_t)w * cnt_in + (size_t)q * fan;
+  if (gid >= cnt_out * rows) return;
+  const uint32_t r = gid / cnt_out, q = gid % cnt_out;
+  const size_t base = (size_t)r * cnt_in + (size_t)q * fan;
   const int m = (int)min((uint32_t)fan, cnt_in - q * fan);
-  p3 U, Sx, Vs, X;
+  p3 U, Sx, X;
   p3_identity(U);
   p3_identity(Sx);
+  if (!inV) {
+    for (int t = m - 1; t >= 0; t--) {
+      p3_load(X, inT, base + t);
+      p3_acc(U, X);
+      p3_acc(Sx, U);
+    }
+    p3_store(outV, gid, Sx);
+    p3_store(outT, gid, U);
+    return;
+  }
+  p3 Vs;
   p3_identity(Vs);
   for (int t = m - 1; t >= 0; t--) {
     p3_load(X, inT, base + t);
@@ -533,75 +555,90 @@ __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV,
 }
 
 // ---------------------------------------------------------------- final check
-// One 128-thread block. Wave 0, lane 0: Horner over the window sums (V of the last
-// reduction level, one per window). Wave 1: -[sum z s mod l]B on the LDS B table.
+// One 128-thread block. Lane g of wave 0: Horner over group g's window sums (V of the last
+// reduction level, one per window). Lane g of wave 1: -[sum z s mod l]B of group g on the
+// LDS B table. flags[1 + g] = group g's equation held; flags[0] = all of them held.
 __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV,
                                                   const unsigned long long* __restrict__ bsum_part, uint32_t nparts,
-                                                  const uint4* __restrict__ btab_g, uint32_t* __restrict__ flag) {
+                                                  uint32_t parts_per_group, uint32_t ngroups,
+                                                  const uint4* __restrict__ btab_g, uint32_t* __restrict__ flags) {
   __shared__ uint4 btab[BT_TABLE];
-  __shared__ unsigned long long sb[BSUM_WORDS];
-  __shared__ uint4 sbp[P3_QUADS];
+  __shared__ unsigned long long sb[BV_MAXG][BSUM_WORDS];
+  __shared__ uint4 sbp[BV_MAXG][P3_QUADS];
+  __shared__ uint32_t sflag[BV_MAXG];
   lds_btab_load(btab, btab_g, BT_TABLE);
-  if (threadIdx.x < BSUM_WORDS) sb[threadIdx.x] = 0;
+  for (uint32_t i = threadIdx.x; i < BV_MAXG * BSUM_WORDS; i += blockDim.x) (&sb[0][0])[i] = 0;
   __syncthreads();
-  {
+  for (uint32_t g = 0; g < ngroups; g++) {
     unsigned long long acc[BSUM_WORDS];
 #pragma unroll
     for (int c = 0; c < BSUM_WORDS; c++) acc[c] = 0;
-    for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
+    const uint32_t i1 = min(nparts, (g + 1) * parts_per_group);
+    for (uint32_t i = g * parts_per_group + threadIdx.x; i < i1; i += blockDim.x) {
 #pragma unroll
       for (int c = 0; c < BSUM_WORDS; c++) acc[c] += bsum_part[(size_t)i * BSUM_WORDS + c];
     }
 #pragma unroll
-    for (int c = 0; c < BSUM_WORDS; c++) atomicAdd(&sb[c], acc[c]);
+    for (int c = 0; c < BSUM_WORDS; c++) atomicAdd(&sb[g][c], acc[c]);
   }
   __syncthreads();
   p3 acc;
+  const uint32_t lane = threadIdx.x & 63;
   if (threadIdx.x >= 64) {
-    // x = sum z s mod l from the 12 column sums (each < 2^64)
-    uint32_t x[16];
-    unsigned long long carry = 0;
+    if (lane < ngroups) {
+      // x = sum z s mod l from the group's 12 column sums (each < 2^64)
+      uint32_t x[16];
+      unsigned long long carry = 0;
 #pragma unroll
-    for (int c = 0; c < BSUM_WORDS; c++) {
-      const unsigned long long v = sb[c];
-      const unsigned long long lo = (v & 0xffffffffull) + (carry & 0xffffffffull);
-      x[c] = (uint32_t)lo;
-      carry = (v >> 32) + (carry >> 32) + (lo >> 32);
-    }
-    x[12] = (uint32_t)carry;
-    x[13] = (uint32_t)(carry >> 32);
-    x[14] = x[15] = 0;
-    uint32_t r[8], sd[8];
-    sc_reduce512(r, x);
-    sc_recode256(sd, r);
-    p3 P;
-    basemul(P, sd, btab);
-    p3_neg(P, P);
-    if (threadIdx.x == 64) {
+      for (int c = 0; c < BSUM_WORDS; c++) {
+        const unsigned long long v = sb[lane][c];
+        const unsigned long long lo = (v & 0xffffffffull) + (carry & 0xffffffffull);
+        x[c] = (uint32_t)lo;
+        carry = (v >> 32) + (carry >> 32) + (lo >> 32);
+      }
+      x[12] = (uint32_t)carry;
+      x[13] = (uint32_t)(carry >> 32);
+      x[14] = x[15] = 0;
+      uint32_t r[8], sd[8];
+      sc_reduce512(r, x);
+      sc_recode256(sd, r);
+      p3 P;
+      basemul(P, sd, btab);
+      p3_neg(P, P);
       uint4 q[9];
       p3_to_quads(q, P);
 #pragma unroll
-      for (int i = 0; i < 9; i++) sbp[i] = q[i];
+      for (int i = 0; i < 9; i++) sbp[lane][i] = q[i];
     }
-  } else if (threadIdx.x == 0) {
+  } else if (lane < ngroups) {
     p3 S;
-    p3_load(acc, winV, BV_NW - 1);
+    const size_t row0 = (size_t)lane * BV_NW;
+    p3_load(acc, winV, row0 + BV_NW - 1);
     for (int w = BV_NW - 2; w >= 0; w--) {
       p3_dbl_n(acc, BV_C);
-      p3_load(S, winV, w);
+      p3_load(S, winV, row0 + w);
       p3_acc(acc, S);
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < ngroups) {
     uint4 q[9];
 #pragma unroll
-    for (int i = 0; i < 9; i++) q[i] = sbp[i];
+    for (int i = 0; i < 9; i++) q[i] = sbp[threadIdx.x][i];
     p3 P;
     quads_to_p3(P, q);
     p3_acc(acc, P);
     p3_dbl_n(acc, 3);  // cofactor
-    *flag = p3_is_identity(acc) ? 1u : 0u;
+    sflag[threadIdx.x] = p3_is_identity(acc) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t all = 1;
+    for (uint32_t g = 0; g < ngroups; g++) {
+      flags[1 + g] = sflag[g];
+      all &= sflag[g];
+    }
+    flags[0] = all;
   }
 }
 
@@ -613,8 +650,8 @@ namespace mvk {
 namespace {
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BatchLayout {
-  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
-  explicit BatchLayout(uint32_t n) {
+  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
+  BatchLayout(uint32_t n, uint32_t groups) {
     using namespace mv;
     const size_t nblk = (n + 255) / 256;
     size_t o = 0;
@@ -622,35 +659,47 @@ struct BatchLayout {
     pts = take((size_t)2 * n * PT_QUADS * 16);
     scal = take((size_t)n * SC_QUADS * 16);
     const size_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
-    pcount = take(nchunk * BV_NPART * 4);
-    poff = take(nchunk * BV_NPART * 4);
-    ptot = take((size_t)BV_NPART * 4);
-    pstart = take((size_t)(BV_NPART + 1) * 4);
+    pcount = take(nchunk * BV_NPG * 4);
+    poff = take(nchunk * BV_NPG * 4);
+    ptot = take((size_t)groups * BV_NPG * 4);
+    pstart = take(((size_t)groups * BV_NPG + 1) * 4);
     tmp = take((size_t)(BV_NWR + BV_NW) * n * 8);
-    offs = take((size_t)(BV_NK + 1) * 4);
+    offs = take(((size_t)groups * BV_NKG + 1) * 4);
     ents = take((size_t)(BV_NWR + BV_NW) * n * 4);
-    segV = take((size_t)BV_NSEG * P3_QUADS * 16);
-    segT = take((size_t)BV_NSEG * P3_QUADS * 16);
-    const size_t lv = (size_t)(BV_NSEG / BV_FAN) * P3_QUADS * 16;
+    segT = take((size_t)groups * BV_NKG * P3_QUADS * 16);
+    const size_t lv = (size_t)groups * (BV_NKG / BV_FAN) * P3_QUADS * 16;
     rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
     bsum = take(nblk * BSUM_WORDS * 8);
-    flag = take(4);
+    flag = take((1 + BV_MAXG) * 4);
     total = o;
   }
 };
+// group geometry: `want` groups of whole 1024-signature chunks
+mv::BvGroups batch_groups(uint32_t n, uint32_t want) {
+  const uint32_t nchunk = (n + mv::PART_CHUNK - 1) / mv::PART_CHUNK;
+  uint32_t g = want < 1 ? 1 : (want > (uint32_t)mv::BV_MAXG ? (uint32_t)mv::BV_MAXG : want);
+  if (g > nchunk) g = nchunk;
+  const uint32_t cpg = (nchunk + g - 1) / g;
+  return mv::BvGroups{(nchunk + cpg - 1) / cpg, cpg};
+}
 }  // namespace
 
-size_t batch_scratch_bytes(uint32_t n) { return BatchLayout(n).total; }
+size_t batch_scratch_bytes(uint32_t n, uint32_t groups) { return BatchLayout(n, groups).total; }
+
+uint32_t batch_group_size(uint32_t n, uint32_t groups) {
+  return batch_groups(n, groups).cpg * mv::PART_CHUNK;
+}
 
 hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
-                               uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
-                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out,
-                               hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok) {
+                               uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
+                               void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
+                               uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
   if (n == 0) return hipSuccess;
-  const BatchLayout L(n);
+  const BvGroups G = batch_groups(n, groups);
+  const BatchLayout L(n, G.count);
   char* base = static_cast<char*>(bscratch);
   uint4* pts = (uint4*)(base + L.pts);
   uint4* scal = (uint4*)(base + L.scal);
@@ -661,7 +710,6 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   unsigned long long* tmp = (unsigned long long*)(base + L.tmp);
   uint32_t* offs = (uint32_t*)(base + L.offs);
   uint32_t* ents = (uint32_t*)(base + L.ents);
-  uint4* segV = (uint4*)(base + L.segV);
   uint4* segT = (uint4*)(base + L.segT);
   uint4* rv[2] = {(uint4*)(base + L.rV0), (uint4*)(base + L.rV1)};
   uint4* rt[2] = {(uint4*)(base + L.rT0), (uint4*)(base + L.rT1)};
@@ -673,6 +721,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   BvKey k;
   for (int i = 0; i < 10; i++) k.w[i] = key[i];
   const uint32_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
+  const uint32_t nparts = G.count * BV_NPG;
   mark(0);
   CommitteeA ca{key_idx && key_ok ? static_cast<const uint4*>(comb_a) : nullptr, key_ok,
                 (uint32_t)(comb_table_bytes(1) / sizeof(uint4))};
@@ -680,25 +729,25 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                      status);
   mark(1);
   hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, pcount);
-  hipLaunchKernelGGL(k_part_scan, dim3(BV_NPART / 64), dim3(256), 0, s, pcount, nchunk, poff, ptot);
-  hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, pstart);
-  hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, tmp);
-  hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPART), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, ents, offs);
+  hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(256), 0, s, pcount, nchunk, G, poff, ptot);
+  hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, nparts, pstart);
+  hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G, tmp);
+  hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, G.count, ents, offs);
   mark(2);
-  hipLaunchKernelGGL(k_bv_bucket, dim3(BV_NSEG / 256), dim3(256), 0, s, pts, offs, ents, segV, segT);
+  hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * BV_NKG / 256), dim3(256), 0, s, pts, offs, ents, G.count, segT);
   mark(3);
-  const uint4* inV = segV;
+  const uint4* inV = nullptr;  // first level: V = T (one bucket per element)
   const uint4* inT = segT;
-  uint32_t cnt = BV_SEGW;
-  int shift = BV_G == 4 ? 2 : (BV_G == 2 ? 1 : 0);  // log2(BV_G)
-  static_assert(BV_G == 1 || BV_G == 2 || BV_G == 4, "segment size");
+  const uint32_t rows = G.count * BV_NW;
+  uint32_t cnt = BV_NB;
+  int shift = 0;
   int pp = 0;
   while (cnt > 1) {
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
     const uint32_t out = (cnt + fan - 1) / fan;
-    const uint32_t lanes = out * BV_NW;
-    hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rv[pp],
-                       rt[pp]);
+    const uint32_t lanes = out * rows;
+    hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rows,
+                       rv[pp], rt[pp]);
     inV = rv[pp];
     inT = rt[pp];
     pp ^= 1;
@@ -706,12 +755,13 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     cnt = out;
   }
   mark(4);
-  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, bsum, nblk, (const uint4*)btab, flag);
+  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, bsum, nblk, G.cpg * (PART_CHUNK / 256), G.count,
+                     (const uint4*)btab, flag);
   mark(5);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // exact fallback: re-verifies every signature iff the combination failed
-  e = launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag);
+  // exact fallback: re-verifies the signatures of every group whose equation failed
+  e = launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag + 1, G.cpg * PART_CHUNK);
   mark(6);
   return e;
 }

@@ -8,6 +8,7 @@
 // chunks of at most cfg.max_batch items. Calls on one ctx are serialised by a mutex.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -24,6 +25,7 @@
 namespace {
 
 constexpr int kBlockStage0 = mvk::BATCH_STAGES;  // parse, hash, verify, verdict
+constexpr int kGuardBatches = 64;  // batches cut into sub-batch equations after a failure
 constexpr int kBlockStages = 4;
 static_assert(kBlockStage0 + kBlockStages == MV_NSTAGES, "stage count");
 
@@ -85,10 +87,20 @@ struct Device {
   // can run while the previous one (on another stream) finishes its latency-bound tail; an
   // event per slot orders reuse across streams. Batch path: bscr/vscr; blocks: blk.
   static constexpr int kSlots = 2;
+  static constexpr int kFlagWords = 1 + mvk::BATCH_MAX_GROUPS;
   DevBuf bscr[kSlots], vscr[kSlots];
   hipEvent_t slot_done[kSlots] = {nullptr, nullptr};
   bool slot_used[kSlots] = {false, false};
   int next_slot = 0;
+  // the batch flags of each slot's last call, copied to pinned host words behind it; read
+  // (without blocking) once slot_done has completed: flag_groups[slot] groups pending
+  uint32_t* h_flags = nullptr;  // kSlots x kFlagWords, pinned
+  uint32_t flag_groups[kSlots] = {0, 0};
+  // single-verify scratch (k_verify's per-wave tables), same two-slot ring
+  DevBuf sscr[kSlots];
+  hipEvent_t sscr_done[kSlots] = {nullptr, nullptr};
+  bool sscr_used[kSlots] = {false, false};
+  int sscr_next = 0;
   DevBuf blk[kSlots];
   hipEvent_t blk_done[kSlots] = {nullptr, nullptr};
   bool blk_used[kSlots] = {false, false};
@@ -113,7 +125,13 @@ struct mv_ctx {
   uint32_t flags = 0;
   uint32_t secret[8] = {0};         // batch-path z_i PRF key (from /dev/urandom)
   std::atomic<uint64_t> calls{0};   // batch calls, the PRF's per-call input
-  std::atomic<uint64_t> batches{0}, fallbacks{0};
+  std::atomic<uint64_t> batches{0}, fallbacks{0}, groups_run{0}, groups_failed{0};
+  // sub-batch equations per batch: groups_fixed != 0 forces that many; 0 = adaptive: one
+  // equation, and after a batch whose equation failed, the next kGuardBatches batches are
+  // cut into guard_groups sub-batch equations (a failure then re-verifies one group).
+  uint32_t groups_fixed = 0;
+  uint32_t guard_groups = 8;
+  std::atomic<int> guard_left{0};
   // stage timing (mv_set_stage_timing): event sets of calls not yet read back
   bool stage_timing = false;
   std::mutex tmu;
@@ -126,17 +144,26 @@ struct mv_ctx {
 
 namespace {
 
+// Errors are recorded in the calling thread's slot (shard threads of one call each own
+// one) and published to ctx->err by the thread that returns to the caller.
+thread_local std::string* t_err = nullptr;
+
+void record_err(mv_ctx* ctx, const std::string& msg) {
+  if (t_err) *t_err = msg;
+  else if (ctx) ctx->err = msg;
+}
+
 #define HIPCHK(ctx, expr)                                                                          \
   do {                                                                                             \
     hipError_t e_ = (expr);                                                                        \
     if (e_ != hipSuccess) {                                                                        \
-      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                             \
+      record_err((ctx), std::string(#expr) + ": " + hipGetErrorString(e_));                        \
       return MV_E_HIP;                                                                             \
     }                                                                                              \
   } while (0)
 
 mv_status set_err(mv_ctx* ctx, mv_status code, const std::string& msg) {
-  if (ctx) ctx->err = msg;
+  record_err(ctx, msg);
   return code;
 }
 
@@ -148,17 +175,22 @@ mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
     return fn(ctx->devs[0], 0, n);
   }
   std::vector<mv_status> rc(nd, MV_OK);
+  std::vector<std::string> errs(nd);
   std::vector<std::thread> th;
   for (size_t d = 0; d < nd; d++) {
     uint64_t lo = n * d / nd, hi = n * (d + 1) / nd;
     th.emplace_back([&, d, lo, hi] {
-      mv_status s = fn(ctx->devs[d], lo, hi);
-      rc[d] = s;
+      t_err = &errs[d];
+      rc[d] = fn(ctx->devs[d], lo, hi);
+      t_err = nullptr;
     });
   }
   for (auto& t : th) t.join();
   for (size_t d = 0; d < nd; d++)
-    if (rc[d] != MV_OK) return rc[d];
+    if (rc[d] != MV_OK) {
+      ctx->err = errs[d];
+      return rc[d];
+    }
   return MV_OK;
 }
 
@@ -176,15 +208,57 @@ void keep_events(mv_ctx* ctx, int device, int first_stage, std::vector<hipEvent_
   ctx->pending.push_back(PendingEvents{device, first_stage, std::move(evs)});
 }
 
-// Enqueues the batch path (batch.hip) for n signatures on stream s.
+// Accounts the batch flags of every slot whose last call has completed (non-blocking):
+// counters, and the adaptive group policy (a failed equation arms the guard).
+void poll_flags(mv_ctx* ctx, Device& dev) {
+  for (int k = 0; k < Device::kSlots; k++) {
+    const uint32_t ng = dev.flag_groups[k];
+    if (!ng || hipEventQuery(dev.slot_done[k]) != hipSuccess) continue;
+    dev.flag_groups[k] = 0;
+    const uint32_t* f = dev.h_flags + k * Device::kFlagWords;
+    ctx->batches++;
+    ctx->groups_run += ng;
+    uint32_t bad = 0;
+    for (uint32_t g = 0; g < ng; g++) bad += f[1 + g] ? 0u : 1u;
+    ctx->groups_failed += bad;
+    if (!f[0]) {
+      ctx->fallbacks++;
+      ctx->guard_left = kGuardBatches;
+    }
+  }
+}
+
+uint32_t pick_groups(mv_ctx* ctx) {
+  if (ctx->groups_fixed) return ctx->groups_fixed;
+  if (ctx->guard_left.fetch_sub(1) > 0) return ctx->guard_groups;
+  ctx->guard_left.store(0);
+  return 1;
+}
+
+// Enqueues the batch path (batch.hip) for n signatures on stream s. flag_dst (optional,
+// device) receives the all-groups flag word.
 mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
-                        const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s, uint32_t* flag_dst,
-                        bool flag_dst_host) {
+                        const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s,
+                        uint32_t* flag_dst) {
+  poll_flags(ctx, dev);
   const int slot = dev.next_slot;
   dev.next_slot = (slot + 1) % Device::kSlots;
   if (!dev.slot_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.slot_done[slot], hipEventDisableTiming));
-  if (dev.slot_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.slot_done[slot], 0));
-  HIPCHK(ctx, dev.bscr[slot].ensure(mvk::batch_scratch_bytes(n)));
+  if (!dev.h_flags) {
+    HIPCHK(ctx, hipHostMalloc((void**)&dev.h_flags, sizeof(uint32_t) * Device::kSlots * Device::kFlagWords,
+                              hipHostMallocDefault));
+    memset(dev.h_flags, 0, sizeof(uint32_t) * Device::kSlots * Device::kFlagWords);
+  }
+  if (dev.slot_used[slot]) {
+    if (dev.flag_groups[slot]) {  // the slot's previous call must be accounted before its words are reused
+      HIPCHK(ctx, hipEventSynchronize(dev.slot_done[slot]));
+      poll_flags(ctx, dev);
+    }
+    HIPCHK(ctx, hipStreamWaitEvent(s, dev.slot_done[slot], 0));
+  }
+  const uint32_t groups = pick_groups(ctx);
+  // scratch for the largest group count, so the adaptive policy never reallocates
+  HIPCHK(ctx, dev.bscr[slot].ensure(mvk::batch_scratch_bytes(n, mvk::BATCH_MAX_GROUPS)));
   HIPCHK(ctx, dev.vscr[slot].ensure(mvk::verify_scratch_bytes(n)));
   uint32_t key[10];
   memcpy(key, ctx->secret, 32);
@@ -198,14 +272,35 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   // committee keys: A comes from the comb tables built at mv_set_committee (no per-signature decode)
   const bool com_a = d_key_idx && dev.committee_loaded && d_pk == dev.committee_pk.as<uint8_t>() &&
                      !(ctx->flags & MV_FLAG_NO_COMB);
-  HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, key, dev.btab.p, dev.bscr[slot].p,
+  HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
                                        com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr));
   keep_events(ctx, dev.id, 0, evs);
-  if (flag_dst)
-    HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, flag_dst_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, s));
+  if (flag_dst) HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, hipMemcpyDeviceToDevice, s));
+  const uint32_t ng = (n + mvk::batch_group_size(n, groups) - 1) / mvk::batch_group_size(n, groups);
+  HIPCHK(ctx, hipMemcpyAsync(dev.h_flags + slot * Device::kFlagWords, flag, sizeof(uint32_t) * (1 + ng),
+                             hipMemcpyDeviceToHost, s));
   HIPCHK(ctx, hipEventRecord(dev.slot_done[slot], s));
   dev.slot_used[slot] = true;
+  dev.flag_groups[slot] = ng;
+  return MV_OK;
+}
+
+// k_verify (single path) on stream s with the device's scratch ring (per-wave tables)
+mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
+                         const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s) {
+  if (n == 0) return MV_OK;
+  const int slot = dev.sscr_next;
+  dev.sscr_next = (slot + 1) % Device::kSlots;
+  if (!dev.sscr_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.sscr_done[slot], hipEventDisableTiming));
+  if (dev.sscr_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.sscr_done[slot], 0));
+  if (dev.sscr[slot].cap < mvk::verify_scratch_bytes(n)) {
+    HIPCHK(ctx, hipDeviceSynchronize());  // the old buffer may still be read by another stream's call
+    HIPCHK(ctx, dev.sscr[slot].ensure(mvk::verify_scratch_bytes(n)));
+  }
+  HIPCHK(ctx, mvk::launch_verify(d_msg, d_sig, d_pk, d_key_idx, n, dev.btab.p, dev.sscr[slot].p, d_status, s));
+  HIPCHK(ctx, hipEventRecord(dev.sscr_done[slot], s));
+  dev.sscr_used[slot] = true;
   return MV_OK;
 }
 
@@ -217,21 +312,17 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
     HIPCHK(ctx, mvk::launch_verify_comb(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
                                         dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s));
   } else {
-    HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(n)));
-    HIPCHK(ctx, mvk::launch_verify(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.btab.p,
-                                   dev.scratch.p, d_status, s));
+    return enqueue_verify(ctx, dev, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, d_status, s);
   }
   return MV_OK;
 }
 
 // The device block pipeline on stream s (enqueue only): k_block_parse -> k_block_hash ->
 // signatures (batch path for >= MV_BATCH_MIN blocks, else committee verify) ->
-// k_block_verdict. d_md / d_bd may be null (scratch then). h_flag (optional, host) receives
-// the batch flag; *batched says whether the batch path ran.
+// k_block_verdict. d_md / d_bd may be null (scratch then).
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
                          const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
-                         hipStream_t s, uint32_t* h_flag, bool* batched) {
-  *batched = false;
+                         hipStream_t s) {
   if (n == 0) return MV_OK;
   const mvh::Committee& com = ctx->committee;
   const int slot = dev.blk_next;
@@ -283,10 +374,12 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
                                       com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
   HIPCHK(ctx, mark(1));
   HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
+  // a block whose digest does not match is rejected ahead of its signature (types.rs:327-332):
+  // s >= l takes it out of the batch equation, so a tampered block never fails the batch
+  HIPCHK(ctx, mvk::launch_block_digest_gate(claimed, bd, facts, n, sig, s));
   HIPCHK(ctx, mark(2));
   if (!(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN) {
-    st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, h_flag, h_flag != nullptr);
-    *batched = true;
+    st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, nullptr);
   } else {
     st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s);
   }
@@ -360,14 +453,11 @@ mv_status verify_blocks_host_parse(mv_ctx* ctx, const uint8_t* buf, const uint64
       // msg digests stay on the device and feed the verify kernel directly
       HIPCHK(ctx, mvk::launch_block_hash(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
                                          dev.msg.as<uint8_t>(), dev.out2.as<uint8_t>(), dev.stream));
-      bool batched = false;
-      uint32_t h_flag = 1;
       if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
         mv_status st2 = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
                                       dev.committee_pk.as<uint8_t>(), dev.keyidx.as<uint32_t>(), m,
-                                      dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
+                                      dev.status.as<uint8_t>(), dev.stream, nullptr);
         if (st2 != MV_OK) return st2;
-        batched = true;
       } else {
         mv_status st2 = enqueue_committee_verify(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
                                                  dev.keyidx.as<uint32_t>(), m, dev.status.as<uint8_t>(), dev.stream);
@@ -378,10 +468,7 @@ mv_status verify_blocks_host_parse(mv_ctx* ctx, const uint8_t* buf, const uint64
       HIPCHK(ctx, hipMemcpyAsync(bd.data(), dev.out2.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(ss.data(), dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-      if (batched) {
-        ctx->batches++;
-        if (!h_flag) ctx->fallbacks++;
-      }
+      poll_flags(ctx, dev);
       for (uint32_t k = 0; k < m; k++) {
         status[i + k] = mvh::block_verdict(facts[k], com, &bd[32 * (size_t)k], ss[k]);
         if (msg_digest) memcpy(msg_digest + 32 * (i + k), &md[32 * (size_t)k], 32);
@@ -415,6 +502,10 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   mv_ctx* ctx = new mv_ctx();
   if (cfg && cfg->max_batch) ctx->max_batch = cfg->max_batch;
   if (cfg) ctx->flags = cfg->flags;
+  if (const char* e = getenv("MV_GUARD_GROUPS")) {  // experiments: sub-batches while guarded
+    const int g = atoi(e);
+    if (g >= 1 && g <= mvk::BATCH_MAX_GROUPS) ctx->guard_groups = (uint32_t)g;
+  }
   {
     FILE* f = fopen("/dev/urandom", "rb");
     size_t got = f ? fread(ctx->secret, 1, sizeof(ctx->secret), f) : 0;
@@ -460,10 +551,14 @@ void mv_destroy(mv_ctx* ctx) {
     (void)hipDeviceSynchronize();  // device-API calls may have run on the caller's streams
     for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
                       &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
-                      &dev.keyok, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0], &dev.vscr[1], &dev.blk[0], &dev.blk[1]})
+                      &dev.keyok, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0], &dev.vscr[1], &dev.blk[0], &dev.blk[1],
+                      &dev.sscr[0], &dev.sscr[1]})
       b->release();
     for (hipEvent_t ev : dev.slot_done)
       if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : dev.sscr_done)
+      if (ev) (void)hipEventDestroy(ev);
+    if (dev.h_flags) (void)hipHostFree(dev.h_flags);
     for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
     dev.h_in.release();
@@ -486,8 +581,11 @@ mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks, const uint64_t* stak
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; i++) total += stakes[i];
   c.quorum_threshold = 2 * total / 3;
-  ctx->committee = c;
-  ctx->has_committee = true;
+  // unpublish first: if a device step fails below, the context is left with no committee
+  // (block calls then refuse with MV_E_NO_COMMITTEE) rather than host facts that disagree
+  // with half-built device tables
+  ctx->has_committee = false;
+  for (auto& dev : ctx->devs) dev.committee_loaded = false;
   for (auto& dev : ctx->devs) {
     HIPCHK(ctx, hipSetDevice(dev.id));
     HIPCHK(ctx, hipDeviceSynchronize());  // earlier device-API work may still read the old tables
@@ -501,13 +599,15 @@ mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks, const uint64_t* stak
     HIPCHK(ctx, mvk::launch_comb_init(dev.committee_pk.as<uint8_t>(), n, 1, dev.combA.p, dev.keyok.as<uint8_t>(),
                                       dev.stream));
     HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-    dev.committee_loaded = true;
   }
   if (key_ok) {
     Device& dev = ctx->devs[0];
     HIPCHK(ctx, hipSetDevice(dev.id));
     HIPCHK(ctx, hipMemcpy(key_ok, dev.keyok.p, n, hipMemcpyDeviceToHost));
   }
+  ctx->committee = std::move(c);
+  for (auto& dev : ctx->devs) dev.committee_loaded = true;
+  ctx->has_committee = true;
   return MV_OK;
 }
 
@@ -582,28 +682,22 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
         dpk = dev.committee_pk.as<uint8_t>();
         dki = dev.keyidx.as<uint32_t>();
       }
-      bool batched = false;
-      uint32_t h_flag = 1;
       if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
         mv_status st = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, dki, m,
-                                     dev.status.as<uint8_t>(), dev.stream, &h_flag, true);
+                                     dev.status.as<uint8_t>(), dev.stream, nullptr);
         if (st != MV_OK) return st;
-        batched = true;
       } else if (dki) {
         mv_status st = enqueue_committee_verify(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dki, m,
                                                 dev.status.as<uint8_t>(), dev.stream);
         if (st != MV_OK) return st;
       } else {
-        HIPCHK(ctx, dev.scratch.ensure(mvk::verify_scratch_bytes(m)));
-        HIPCHK(ctx, mvk::launch_verify(dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, nullptr, m, dev.btab.p,
-                                       dev.scratch.p, dev.status.as<uint8_t>(), dev.stream));
+        mv_status st = enqueue_verify(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(), dpk, nullptr, m,
+                                      dev.status.as<uint8_t>(), dev.stream);
+        if (st != MV_OK) return st;
       }
       HIPCHK(ctx, hipMemcpyAsync(status + i, dev.status.p, m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-      if (batched) {
-        ctx->batches++;
-        if (!h_flag) ctx->fallbacks++;
-      }
+      poll_flags(ctx, dev);
     }
     return MV_OK;
   });
@@ -673,18 +767,13 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
       HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
       uint8_t* dout = dev.out2.as<uint8_t>();
       const uint8_t* dbuf = dev.bytes.as<uint8_t>();
-      bool batched = false;
-      uint32_t h_flag = 1;
       mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
                                     (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
-                                    dout + 32 * (size_t)m, dev.stream, &h_flag, &batched);
+                                    dout + 32 * (size_t)m, dev.stream);
       if (st != MV_OK) return st;
       HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-      if (batched) {
-        ctx->batches++;
-        if (!h_flag) ctx->fallbacks++;
-      }
+      poll_flags(ctx, dev);
       const uint8_t* ho = dev.h_out.as<uint8_t>();
       memcpy(status + i, ho + 64 * (size_t)m, m);
       if (msg_digest) memcpy(msg_digest + 32 * i, ho, 32 * (size_t)m);
@@ -714,9 +803,7 @@ mv_status mv_dev_verify_blocks(mv_ctx* ctx, int device, const uint8_t* d_buf, ui
   if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
   HIPCHK(ctx, hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
-  bool batched = false;
-  return enqueue_blocks(ctx, *dev, d_buf, buf_bytes, d_off, d_len, n, d_status, d_msg_digest, d_block_digest, s,
-                        nullptr, &batched);
+  return enqueue_blocks(ctx, *dev, d_buf, buf_bytes, d_off, d_len, n, d_status, d_msg_digest, d_block_digest, s);
 }
 
 mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
@@ -729,9 +816,7 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
   if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
   HIPCHK(ctx, hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
-  HIPCHK(ctx, dev->scratch.ensure(mvk::verify_scratch_bytes(n)));
-  HIPCHK(ctx, mvk::launch_verify(d_msg, d_sig, d_pk, nullptr, n, dev->btab.p, dev->scratch.p, d_status, s));
-  return MV_OK;
+  return enqueue_verify(ctx, *dev, d_msg, d_sig, d_pk, nullptr, n, d_status, s);
 }
 
 mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
@@ -746,7 +831,22 @@ mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_
   if (n == 0) return MV_OK;
   HIPCHK(ctx, hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
-  return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok, false);
+  return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok);
+}
+
+mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return MV_E_INVALID_ARG;
+  mv_status st = mv_batch_stats(ctx, out, out + 1);
+  out[2] = ctx->groups_run.load();
+  out[3] = ctx->groups_failed.load();
+  return st;
+}
+
+mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups) {
+  if (!ctx || groups > (uint32_t)mvk::BATCH_MAX_GROUPS) return set_err(ctx, MV_E_INVALID_ARG, "groups > 16");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->groups_fixed = groups;
+  return MV_OK;
 }
 
 mv_status mv_set_stage_timing(mv_ctx* ctx, int enable) {
@@ -785,6 +885,13 @@ mv_status mv_stage_times(mv_ctx* ctx, double* ms, uint64_t* calls, int reset) {
 
 mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks) {
   if (!ctx) return MV_E_INVALID_ARG;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (auto& dev : ctx->devs) {
+      (void)hipSetDevice(dev.id);
+      poll_flags(ctx, dev);
+    }
+  }
   if (batches) *batches = ctx->batches.load();
   if (fallbacks) *fallbacks = ctx->fallbacks.load();
   return MV_OK;

@@ -637,6 +637,29 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
   }
 }
 
+MV_DEV bool digest_same(const uint8_t* claimed, const uint8_t* digest, uint32_t i) {
+  const uint4* a = reinterpret_cast<const uint4*>(claimed + 32 * (size_t)i);
+  const uint4* b = reinterpret_cast<const uint4*>(digest + 32 * (size_t)i);
+  const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+  return ((a0.x ^ b0.x) | (a0.y ^ b0.y) | (a0.z ^ b0.z) | (a0.w ^ b0.w) | (a1.x ^ b1.x) | (a1.y ^ b1.y) |
+          (a1.z ^ b1.z) | (a1.w ^ b1.w)) == 0;
+}
+
+// Between the hashes and the signature check: a parsed block whose digest differs from the
+// claimed one gets DIGEST_MISMATCH whatever its signature (types.rs:327-332 comes before the
+// signature check at :346-348), so its s is set to 2^256 - 1 (>= l): it is then excluded
+// from the batch equation like the blocks ingest rejects ahead of the signature.
+__global__ void __launch_bounds__(256) k_block_digest_gate(const uint8_t* __restrict__ claimed,
+                                                           const uint8_t* __restrict__ digest,
+                                                           const uint32_t* __restrict__ facts, uint32_t n,
+                                                           uint8_t* __restrict__ sig) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !(facts[i] & BF_PARSED) || digest_same(claimed, digest, i)) return;
+  uint4* s4 = reinterpret_cast<uint4*>(sig + 64 * (size_t)i + 32);
+  s4[0] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  s4[1] = make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+
 // status[i] in the order of StatementBlock::verify (types.rs:315-376)
 __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restrict__ facts,
                                                        const uint8_t* __restrict__ claimed,
@@ -650,11 +673,7 @@ __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restric
   if (!(f & BF_PARSED)) {
     st = MV_BLOCK_PARSE_ERROR;
   } else {
-    const uint4* a = reinterpret_cast<const uint4*>(claimed + 32 * (size_t)i);
-    const uint4* b = reinterpret_cast<const uint4*>(digest + 32 * (size_t)i);
-    const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
-    const bool same = ((a0.x ^ b0.x) | (a0.y ^ b0.y) | (a0.z ^ b0.z) | (a0.w ^ b0.w) | (a1.x ^ b1.x) |
-                       (a1.y ^ b1.y) | (a1.z ^ b1.z) | (a1.w ^ b1.w)) == 0;
+    const bool same = digest_same(claimed, digest, i);
     const uint32_t inc = (f >> BF_INC_SHIFT) & 0xffu;
     st = !same                      ? MV_BLOCK_DIGEST_MISMATCH
          : !(f & BF_EPOCH_OK)       ? MV_BLOCK_EPOCH_MISMATCH
@@ -689,6 +708,13 @@ hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uin
     hipLaunchKernelGGL(mv::k_block_parse, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, cv, io);
   else
     hipLaunchKernelGGL(mv::k_block_ingest, dim3(n), dim3(64), 0, s, buf, off, len, n, cv, io);
+  return hipGetLastError();
+}
+
+hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* digest, const uint32_t* facts, uint32_t n,
+                                    uint8_t* sig, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_block_digest_gate, dim3((n + 255) / 256), dim3(256), 0, s, claimed, digest, facts, n, sig);
   return hipGetLastError();
 }
 

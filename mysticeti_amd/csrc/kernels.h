@@ -10,7 +10,9 @@ size_t btable_bytes();
 hipError_t launch_btable_init(void* d_btab, hipStream_t s);
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
-                         const uint32_t* skip = nullptr);
+                         const uint32_t* skip = nullptr, uint32_t skip_group = 0);
+// skip (optional, device): per-group flags; the signatures of group g = i / skip_group
+// (skip_group a multiple of 256; 0 = one group) are not verified when skip[g] != 0.
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
                        uint8_t* sig, hipStream_t s);
 hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
@@ -25,15 +27,20 @@ hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const
                                   uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
 hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s);
 // batch.hip: random-linear-combination batch verify with exact on-device fallback.
+// The batch is cut into `groups` sub-batches (1..BATCH_MAX_GROUPS, whole 1024-signature
+// chunks, batch_group_size signatures each), one combined equation per group.
 // key = 32-byte secret + 64-bit call counter (the z_i PRF key); *flag_out receives the
-// device address of the batch flag (1 = the combined equation held). ev (optional):
-// BATCH_STAGES + 1 events, recorded before the first stage and after each stage.
+// device address of the flag words: [0] = 1 if every group's equation held, [1 + g] = 1
+// if group g's held. ev (optional): BATCH_STAGES + 1 events, recorded before the first
+// stage and after each stage.
 constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
-size_t batch_scratch_bytes(uint32_t n);
+constexpr int BATCH_MAX_GROUPS = 16;
+size_t batch_scratch_bytes(uint32_t n, uint32_t groups);
+uint32_t batch_group_size(uint32_t n, uint32_t groups);
 hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
-                               uint32_t n, const uint32_t key[10], const void* btab, void* bscratch,
-                               void* vscratch, uint8_t* status, hipStream_t s, uint32_t** flag_out,
-                               hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
+                               uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
+                               void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
+                               uint32_t** flag_out, hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
                                const uint8_t* key_ok = nullptr);
 // comb_a / key_ok (optional, with key_idx): the committee's comb tables (comb.hip, tables of
 // -A) and per-key decode flags; k_bv_prep then reads each signature's A from entry [0][1]
@@ -50,6 +57,10 @@ hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uin
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s);
+// sig[i]'s s := 2^256 - 1 (outside the batch equation) for every parsed block whose computed
+// digest differs from its claimed one
+hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* digest, const uint32_t* facts, uint32_t n,
+                                    uint8_t* sig, hipStream_t s);
 hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, const uint8_t* digest,
                                 const uint8_t* sig_status, uint32_t n, uint8_t* status, hipStream_t s);
 }  // namespace mvk

@@ -161,9 +161,11 @@ template <int MINW>
 __global__ void __launch_bounds__(256, MINW)
     k_verify(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
              const uint32_t* __restrict__ key_idx, uint32_t n, const uint4* __restrict__ btab_g,
-             uint4* __restrict__ scratch, uint8_t* __restrict__ status, const uint32_t* __restrict__ skip) {
-  // batch fallback (batch.hip): nothing to do when the batch equation already held
-  if (skip && *skip) return;
+             uint4* __restrict__ scratch, uint8_t* __restrict__ status, const uint32_t* __restrict__ skip,
+             uint32_t skip_group) {
+  // batch fallback (batch.hip): nothing to do for a group whose equation held (skip_group
+  // is a multiple of the block size, so the test is uniform over the block)
+  if (skip && skip[skip_group ? blockIdx.x * blockDim.x / skip_group : 0]) return;
   __shared__ uint4 btab[2 * BT_TABLE];
   lds_btab_load(btab, btab_g, 2 * BT_TABLE);
   MV_PHASE(0);
@@ -575,17 +577,17 @@ hipError_t launch_btable_init(void* d_btab, hipStream_t s) {
 }
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
-                         const uint32_t* skip) {
+                         const uint32_t* skip, uint32_t skip_group) {
   if (n == 0) return hipSuccess;
   if (verify_variant() == 1)
     hipLaunchKernelGGL(mv::k_verify<1>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                       (const uint4*)btab, (uint4*)scratch, status, skip);
+                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group);
   else if (verify_variant() == 3)
     hipLaunchKernelGGL(mv::k_verify<3>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                       (const uint4*)btab, (uint4*)scratch, status, skip);
+                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group);
   else
     hipLaunchKernelGGL(mv::k_verify<2>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                       (const uint4*)btab, (uint4*)scratch, status, skip);
+                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group);
   return hipGetLastError();
 }
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,

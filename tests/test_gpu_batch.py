@@ -192,3 +192,53 @@ def test_committee_keys_batch_equation_uses_comb_a(engine, golden):
     assert nb == 1 and nf == 0
     assert (st == want).all()
     assert (want == 2).any()
+
+
+def counters_delta(engine, fn):
+    c0 = engine.batch_counters()
+    out = fn()
+    c1 = engine.batch_counters()
+    return out, tuple(b - a for a, b in zip(c0, c1))
+
+
+@pytest.mark.parametrize("n,groups,want_groups", [(16384, 8, 8), (16384 + 100, 8, 6), (9000, 16, 9)])
+def test_sub_batch_equations_reverify_only_failing_groups(engine, n, groups, want_groups):
+    """Fixed sub-batch equations: every group's equation holds on a valid batch; bad
+    signatures fail exactly the groups that hold them, and only those are re-verified
+    (the verdicts stay exact)."""
+    msg, sig, pk = signed(engine, n, 21 + n)
+    engine.set_batch_groups(groups)
+    try:
+        st, d = counters_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+        assert (st == 0).all()
+        assert d == (1, 0, want_groups, 0)
+        gsize = -(-(-(-n // 1024)) // groups) * 1024  # whole 1024-signature chunks per group
+        s2 = sig.copy()
+        bad = [5, 3 * gsize + 7, 3 * gsize + 100, n - 1]
+        for b in bad:
+            s2[b, 40] ^= 0x10  # s stays < l, R decodes: only an equation can catch it
+        st, d = counters_delta(engine, lambda: engine.ed25519_verify(msg, s2, pk))
+        ref = O.verify_batch(pk, s2, msg)
+        assert (st == ref).all() and (st[bad] == 1).all()
+        failing = len({b // gsize for b in bad})
+        assert d == (1, 1, want_groups, failing)
+    finally:
+        engine.set_batch_groups(0)
+
+
+def test_adaptive_guard_after_a_failed_batch():
+    """Default policy: one equation per batch; a failed equation arms the guard, and the next
+    batches are cut into sub-batch equations (a bad signature then re-verifies one group)."""
+    with M.Engine(devices=(0,)) as eng:
+        n = 16384
+        msg, sig, pk = signed(eng, n, 31)
+        s2 = sig.copy()
+        s2[100, 40] ^= 0x10
+        st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, s2, pk))
+        assert st[100] == 1 and (np.delete(st, 100) == 0).all()
+        assert d == (1, 1, 1, 1)
+        st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, s2, pk))
+        assert st[100] == 1 and (np.delete(st, 100) == 0).all()
+        assert d == (1, 1, 8, 1)
+        st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, sig, pk))
+        assert (st == 0).all() and d == (1, 0, 8, 0)

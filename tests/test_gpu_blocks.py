@@ -115,3 +115,27 @@ def test_edge_blocks_through_batch_path(engine, golden):
         assert [int(x) for x in st] == [c["status"] for c in cases] * reps
         assert b1 - b0 == 1
         assert f1 - f0 == (0 if drop_bad_sig else 1)
+
+
+def test_tampered_blocks_stay_out_of_the_batch_equation(engine, golden):
+    """A block whose digest does not match is DIGEST_MISMATCH whatever its signature
+    (types.rs:327-332 before :346-348). Tampered blocks -- s flipped with the digest left
+    stale, or a pre-image byte changed -- are taken out of the combined equation after the
+    hashes, so 4,096 blocks with tampered ones pass the batch with no fallback."""
+    g = golden("blocks_config1.json")
+    pks, stakes, epoch = committee_arrays(g["committee"])
+    engine.set_committee(pks, stakes, epoch)
+    bins = [b.bincode() for b in B.gen_config1(O.sign)]
+    t1 = bytearray(bins[17])
+    t1[-20] ^= 0x04  # s bit: invalid signature, stale digest
+    t2 = bytearray(bins[2222])
+    t2[-64 - 8 - 8 - 1 - 3] ^= 0x01  # meta_creation_time_ns byte: new message, stale digest
+    bins[17], bins[2222] = bytes(t1), bytes(t2)
+    b0, f0 = engine.batch_stats()
+    st, md, bd = engine.verify_blocks(bins)
+    b1, f1 = engine.batch_stats()
+    assert b1 - b0 == 1 and f1 - f0 == 0
+    assert st[17] == 2 and st[2222] == 2 and (np.delete(st, [17, 2222]) == 0).all()
+    for i in (17, 2222):
+        ost, omd, obd = O.block_verify(bins[i], pks, stakes, epoch)
+        assert ost == 2 and md[i].tobytes() == omd and bd[i].tobytes() == obd
