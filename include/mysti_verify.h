@@ -131,7 +131,8 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
  * 127-bit z_i (BLAKE2b PRF keyed per context and call) is checked first; if it fails, every
  * signature is re-verified individually on the same stream, so each verdict is exact (an
  * invalid signature survives a passing combination with probability <= 2^-127).
- * `d_pk` rows are indexed by item, or by `d_key_idx` (device array) when it is non-NULL.
+ * `d_pk` rows are indexed by item, or by `d_key_idx` (device array) when it is non-NULL; every
+ * d_key_idx[i] must then be a row of d_pk (the library cannot bound-check device arrays).
  * Enqueues only; `d_batch_ok` (optional, device, 4 bytes) receives 1 if the combination held. */
 mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
                                       const uint8_t* d_pk, const uint32_t* d_key_idx, uint32_t n,
@@ -157,10 +158,10 @@ mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks);
  * sub-batch, out[2] sub-batch equations checked, out[3] sub-batch equations that failed
  * (each re-verified signature by signature). Device-API calls are counted once complete. */
 mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out /* 4 */);
-/* Sub-batch equations per batch-path call. groups = 0 (default): adaptive -- one combined
- * equation per batch; after a batch whose equation failed, the next 64 batches are cut into
- * 8 sub-batches (whole 1024-signature chunks) with one equation each, so a bad signature
- * re-verifies only its sub-batch. groups = 1..16 fixes the count. Verdicts never depend on it. */
+/* Sub-batch equations per batch-path call: the batch is cut into groups of whole 1024-signature
+ * chunks, each with its own combined equation, and a failed equation re-verifies only its group.
+ * groups = 0 (default): adaptive -- 4 groups per batch; after a batch whose equation failed,
+ * the next 64 batches are cut into 8. groups = 1..16 fixes the count. Verdicts never depend on it. */
 mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups);
 /* Stage timing: when enabled, every call records HIP events on its stream around its
  * stages: batch path 0..5 (prep, sort, bucket, reduce, final, fallback), block pipeline

@@ -32,6 +32,7 @@
 // A scalars (< l < 2^253) windows 0..15.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fe25519.h"
 #include "ge25519.h"
@@ -466,21 +467,28 @@ __global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned 
 }
 
 // ---------------------------------------------------------------- buckets
-// Lane = bucket (g, w, |d|): T = the sum of the bucket's points. Windows are laid out
-// high-first in the grid (window 15's buckets hold four times the entries), every group's
-// windows side by side, and each point is loaded one add ahead.
+// Lane = segment of `seg` consecutive buckets (g, w, j*seg .. j*seg + seg - 1), consumed from
+// the top bucket down: T = running sum of the segment's buckets, V = sum of T after every
+// bucket = sum_b (b + 1) B_{j*seg + b}. The segment then stands for V + (j * seg) T in the
+// window's sum (k_bv_reduce). seg = 1: T only (V = T). Windows are laid out high-first in the
+// grid (window 15's buckets hold four times the entries), every group's windows side by side,
+// and each point is loaded one add ahead.
 __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
-                                                   const uint32_t* __restrict__ ents, uint32_t ngroups,
-                                                   uint4* __restrict__ segT) {
+                                                   const uint32_t* __restrict__ ents, uint32_t ngroups, uint32_t seg,
+                                                   uint4* __restrict__ segV, uint4* __restrict__ segT) {
+  const uint32_t nsw = BV_NB / seg;  // segments per (group, window) row
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lin >= ngroups * BV_NKG) return;
-  const uint32_t span = ngroups * BV_NB;
+  if (lin >= ngroups * BV_NW * nsw) return;
+  const uint32_t span = ngroups * nsw;
   const uint32_t w = BV_NW - 1 - lin / span;
-  const uint32_t key = ((lin % span) / BV_NB) * BV_NKG + w * BV_NB + lin % BV_NB;
-  p3 T;
+  const uint32_t g = (lin % span) / nsw, j = lin % nsw;
+  const uint32_t sidx = (g * BV_NW + w) * nsw + j;  // segment index, row-major
+  const uint32_t key0 = g * BV_NKG + w * BV_NB + j * seg;
+  p3 T, V;
   p3_identity(T);
-  const uint32_t e_lo = offs[key];
-  uint32_t e = offs[key + 1];
+  p3_identity(V);
+  const uint32_t e_lo = offs[key0];
+  uint32_t e = offs[key0 + seg];
   uint4 q[7];
   uint32_t ent = 0;
   if (e > e_lo) {
@@ -490,23 +498,30 @@ __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts
 #pragma unroll
     for (int i = 0; i < 7; i++) q[i] = p[i];
   }
-  for (uint32_t k = offs[key + 1]; k > e_lo; k--) {
-    precomp pc;
-    quads_to_precomp(pc, q);
-    const bool neg = ent & 1u;
-    if (e > e_lo) {  // next point in flight during this add
-      e--;
-      ent = ents[e];
-      const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+  uint32_t b1 = offs[key0 + seg];
+  for (int b = (int)seg - 1; b >= 0; b--) {
+    const uint32_t b0 = offs[key0 + b];
+    for (uint32_t k = b1; k > b0; k--) {
+      precomp pc;
+      quads_to_precomp(pc, q);
+      const bool neg = ent & 1u;
+      if (e > e_lo) {  // next point in flight during this add
+        e--;
+        ent = ents[e];
+        const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
 #pragma unroll
-      for (int i = 0; i < 7; i++) q[i] = p[i];
+        for (int i = 0; i < 7; i++) q[i] = p[i];
+      }
+      precomp_cneg(pc, neg);
+      p1p1 t;
+      p3_add_precomp(t, T, pc);
+      p1p1_to_p3(T, t);
     }
-    precomp_cneg(pc, neg);
-    p1p1 t;
-    p3_add_precomp(t, T, pc);
-    p1p1_to_p3(T, t);
+    b1 = b0;
+    if (seg > 1) p3_acc(V, T);
   }
-  p3_store(segT, key, T);
+  if (seg > 1) p3_store(segV, sidx, V);
+  p3_store(segT, sidx, T);
 }
 
 // ---------------------------------------------------------------- reduction
@@ -515,8 +530,8 @@ __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts
 // become one element with index q:
 //   V' = sum V_t + scale * sum_t t T_t,   T' = sum T_t,   scale' = FAN * scale.
 // scale is a power of two (log2 = shift): the multiplication is `shift` doublings.
-// First level (inV == nullptr): the elements are the buckets, m = |d| - 1, so V_m = T_m
-// and scale = 1: V' = sum_t (t + 1) T_t, the sum of the running sums.
+// First level with one bucket per segment (inV == nullptr): the elements are the buckets,
+// m = |d| - 1, so V_m = T_m and scale = 1: V' = sum_t (t + 1) T_t, the sum of the running sums.
 __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV, const uint4* __restrict__ inT,
                                                   uint32_t cnt_in, int fan, int shift, uint32_t rows,
                                                   uint4* __restrict__ outV, uint4* __restrict__ outT) {
@@ -650,7 +665,7 @@ namespace mvk {
 namespace {
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BatchLayout {
-  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
+  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
   BatchLayout(uint32_t n, uint32_t groups) {
     using namespace mv;
     const size_t nblk = (n + 255) / 256;
@@ -666,6 +681,7 @@ struct BatchLayout {
     tmp = take((size_t)(BV_NWR + BV_NW) * n * 8);
     offs = take(((size_t)groups * BV_NKG + 1) * 4);
     ents = take((size_t)(BV_NWR + BV_NW) * n * 4);
+    segV = take((size_t)groups * BV_NKG / 2 * P3_QUADS * 16);  // segments of >= 2 buckets only
     segT = take((size_t)groups * BV_NKG * P3_QUADS * 16);
     const size_t lv = (size_t)groups * (BV_NKG / BV_FAN) * P3_QUADS * 16;
     rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
@@ -681,6 +697,16 @@ mv::BvGroups batch_groups(uint32_t n, uint32_t want) {
   if (g > nchunk) g = nchunk;
   const uint32_t cpg = (nchunk + g - 1) / g;
   return mv::BvGroups{(nchunk + cpg - 1) / cpg, cpg};
+}
+// buckets per bucket-kernel lane (a power of two): MV_BV_SEG=<k> for experiments
+uint32_t bucket_segment(uint32_t groups) {
+  static const int env = [] {
+    const char* e = getenv("MV_BV_SEG");
+    return e ? atoi(e) : -1;
+  }();
+  uint32_t seg = env > 0 ? (uint32_t)env : (groups >= 8 ? groups : 1u);
+  if (seg > 64) seg = 64;
+  return 1u << (31 - __builtin_clz(seg));
 }
 }  // namespace
 
@@ -710,6 +736,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   unsigned long long* tmp = (unsigned long long*)(base + L.tmp);
   uint32_t* offs = (uint32_t*)(base + L.offs);
   uint32_t* ents = (uint32_t*)(base + L.ents);
+  uint4* segV = (uint4*)(base + L.segV);
   uint4* segT = (uint4*)(base + L.segT);
   uint4* rv[2] = {(uint4*)(base + L.rV0), (uint4*)(base + L.rV1)};
   uint4* rt[2] = {(uint4*)(base + L.rT0), (uint4*)(base + L.rT1)};
@@ -734,13 +761,18 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G, tmp);
   hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, G.count, ents, offs);
   mark(2);
-  hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * BV_NKG / 256), dim3(256), 0, s, pts, offs, ents, G.count, segT);
+  // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
+  // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
+  // through memory and the reduction stays the size of one group's
+  const uint32_t seg = bucket_segment(G.count);
+  hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * BV_NKG / seg / 256), dim3(256), 0, s, pts, offs, ents, G.count, seg,
+                     segV, segT);
   mark(3);
-  const uint4* inV = nullptr;  // first level: V = T (one bucket per element)
+  const uint4* inV = seg > 1 ? segV : nullptr;  // one bucket per segment: V = T
   const uint4* inT = segT;
   const uint32_t rows = G.count * BV_NW;
-  uint32_t cnt = BV_NB;
-  int shift = 0;
+  uint32_t cnt = BV_NB / seg;
+  int shift = 31 - __builtin_clz(seg);  // log2(seg)
   int pp = 0;
   while (cnt > 1) {
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;

@@ -126,10 +126,12 @@ struct mv_ctx {
   uint32_t secret[8] = {0};         // batch-path z_i PRF key (from /dev/urandom)
   std::atomic<uint64_t> calls{0};   // batch calls, the PRF's per-call input
   std::atomic<uint64_t> batches{0}, fallbacks{0}, groups_run{0}, groups_failed{0};
-  // sub-batch equations per batch: groups_fixed != 0 forces that many; 0 = adaptive: one
-  // equation, and after a batch whose equation failed, the next kGuardBatches batches are
-  // cut into guard_groups sub-batch equations (a failure then re-verifies one group).
+  // sub-batch equations per batch: groups_fixed != 0 forces that many; 0 = adaptive:
+  // base_groups equations (4 cost nothing measurable over 1: the sort runs on 4x more, 4x
+  // smaller partitions), and after a batch whose equation failed, the next kGuardBatches
+  // batches are cut into guard_groups (a failure then re-verifies 1/8 of the batch).
   uint32_t groups_fixed = 0;
+  uint32_t base_groups = 4;
   uint32_t guard_groups = 8;
   std::atomic<int> guard_left{0};
   // stage timing (mv_set_stage_timing): event sets of calls not yet read back
@@ -232,7 +234,7 @@ uint32_t pick_groups(mv_ctx* ctx) {
   if (ctx->groups_fixed) return ctx->groups_fixed;
   if (ctx->guard_left.fetch_sub(1) > 0) return ctx->guard_groups;
   ctx->guard_left.store(0);
-  return 1;
+  return ctx->base_groups;
 }
 
 // Enqueues the batch path (batch.hip) for n signatures on stream s. flag_dst (optional,
@@ -505,6 +507,10 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   if (const char* e = getenv("MV_GUARD_GROUPS")) {  // experiments: sub-batches while guarded
     const int g = atoi(e);
     if (g >= 1 && g <= mvk::BATCH_MAX_GROUPS) ctx->guard_groups = (uint32_t)g;
+  }
+  if (const char* e = getenv("MV_BASE_GROUPS")) {  // experiments: sub-batches when not guarded
+    const int g = atoi(e);
+    if (g >= 1 && g <= mvk::BATCH_MAX_GROUPS) ctx->base_groups = (uint32_t)g;
   }
   {
     FILE* f = fopen("/dev/urandom", "rb");

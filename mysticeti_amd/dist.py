@@ -51,3 +51,36 @@ def all_ranks_ok(ok: bool, dist=None) -> bool:
     t = torch.tensor([0 if ok else 1], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item()) == 0
+
+
+def cpu_share() -> Tuple[int, str]:
+    """Host cores this process may use: min of the CPU affinity mask, the cgroup v2/v1 CPU
+    quota and OMP_NUM_THREADS (the GPU box exports its share there); with the source."""
+    import os
+
+    cores, src = os.cpu_count() or 1, "os.cpu_count"
+    try:
+        a = len(os.sched_getaffinity(0))
+        if a < cores:
+            cores, src = a, "sched_getaffinity"
+    except (AttributeError, OSError):
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None and int(quota) < cores:
+        cores, src = max(1, int(quota)), "cgroup cpu quota"
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < cores:
+        cores, src = int(omp), "OMP_NUM_THREADS"
+    return cores, src
