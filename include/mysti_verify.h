@@ -82,6 +82,8 @@ typedef struct mv_config {
   uint32_t device_mask; /* bit i = use HIP device i; 0 = device 0 only */
   uint32_t max_batch;   /* items per device launch chunk; 0 = default (1<<20) */
   uint32_t flags;       /* MV_FLAG_* */
+  uint32_t shards_per_device; /* 0/1 = one; k > 1: k logical shards (stream + buffers each) per device,
+                                 host-buffer calls shard across them exactly as across GPUs */
 } mv_config;
 
 mv_status mv_create(const mv_config* cfg, mv_ctx** out);
@@ -112,9 +114,20 @@ mv_status mv_ed25519_sign(mv_ctx* ctx, const uint8_t* seed, const uint8_t* msg, 
 /* StatementBlock::verify on n bincode-serialized blocks buf[off[i] .. off[i]+len[i]).
  * status[i] = MV_BLOCK_*; msg_digest[i] = Blake2b-256(pre-image) (the signed message),
  * block_digest[i] = Blake2b-256(pre-image || signature); either digest array may be NULL.
- * Requires mv_set_committee. */
+ * Requires mv_set_committee. Concurrent callers are coalesced: a call joins a submission
+ * queue, and a caller that finds no device pass running takes every queued call into one
+ * pass (the online path: n - 1 peer tasks each with a block or two share a GPU round trip).
+ * Several devices: the merged blocks are split into contiguous shards of about equal bytes. */
 mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                            uint8_t* status, uint8_t* msg_digest, uint8_t* block_digest);
+
+/* Submission-queue counters: mv_verify_blocks calls, and device passes that served them. */
+mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes);
+
+/* Host-only helper (no device needed): the shard plan of the multi-device paths -- cut[0..parts]
+ * splits items [0, n) into contiguous shards of about equal total weight (block calls weigh a
+ * block by its bincode bytes + 64). */
+mv_status mv_shard_plan(const uint64_t* weights, uint64_t n, uint32_t parts, uint64_t* cut /* parts + 1 */);
 
 /* Host-only helper (no device needed): the signed pre-image of one bincode block
  * (BlockDigest::digest_without_signature, crypto.rs:85-128). Returns the pre-image

@@ -40,6 +40,7 @@ EXPORTS = [
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
     "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
+    "mv_queue_stats", "mv_shard_plan",
 ]
 # batch path stages, then the block pipeline's (mv_stage_times order, MV_NSTAGES)
 STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback", "parse", "hash", "verify", "verdict"]
@@ -52,7 +53,8 @@ class MvError(RuntimeError):
 
 
 class _Config(ctypes.Structure):
-    _fields_ = [("device_mask", ctypes.c_uint32), ("max_batch", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+    _fields_ = [("device_mask", ctypes.c_uint32), ("max_batch", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("shards_per_device", ctypes.c_uint32)]
 
 
 _lib = None
@@ -83,6 +85,8 @@ def load_library(path: str = LIB_PATH):
     lib.mv_batch_stats.argtypes = [vp, vp, vp]
     lib.mv_batch_counters.argtypes = [vp, vp]
     lib.mv_set_batch_groups.argtypes = [vp, u32]
+    lib.mv_queue_stats.argtypes = [vp, vp, vp]
+    lib.mv_shard_plan.argtypes = [vp, u64, u32, vp]
     lib.mv_set_stage_timing.argtypes = [vp, ctypes.c_int]
     lib.mv_stage_times.argtypes = [vp, vp, vp, ctypes.c_int]
     lib.mv_dev_verify_blocks.argtypes = [vp, ctypes.c_int, vp, u64, vp, vp, u32, vp, vp, vp, vp]
@@ -109,17 +113,18 @@ class Engine:
     """One mv_ctx: the devices it shards over, their streams and buffers."""
 
     def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0, batch: bool = True, comb: bool = True,
-                 host_parse: bool = False):
+                 host_parse: bool = False, shards_per_device: int = 1):
         """batch=False sets MV_FLAG_NO_BATCH: host-buffer verifies check every signature alone.
         comb=False sets MV_FLAG_NO_COMB: committee keys go through the per-signature ladder,
         not the per-key comb tables. host_parse=True sets MV_FLAG_HOST_PARSE: verify_blocks
-        parses the bincode on the host instead of on the GPU."""
+        parses the bincode on the host instead of on the GPU. shards_per_device > 1 makes
+        that many logical shards per device (host calls shard across them as across GPUs)."""
         self.lib = load_library()
         mask = 0
         for d in devices:
             mask |= 1 << int(d)
         flags = (0 if batch else FLAG_NO_BATCH) | (0 if comb else FLAG_NO_COMB) | (FLAG_HOST_PARSE if host_parse else 0)
-        cfg = _Config(mask, max_batch, flags)
+        cfg = _Config(mask, max_batch, flags, shards_per_device)
         h = ctypes.c_void_p()
         rc = self.lib.mv_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != MV_OK:
@@ -247,6 +252,12 @@ class Engine:
         """Sub-batch equations per batch: 0 = adaptive (default), 1..16 fixed."""
         self._check(self.lib.mv_set_batch_groups(self.ctx, int(groups)), "mv_set_batch_groups")
 
+    def queue_stats(self) -> Tuple[int, int]:
+        """(mv_verify_blocks calls, device passes that served them)."""
+        c, p = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.mv_queue_stats(self.ctx, ctypes.byref(c), ctypes.byref(p)), "mv_queue_stats")
+        return c.value, p.value
+
     def set_stage_timing(self, enable: bool = True):
         self._check(self.lib.mv_set_stage_timing(self.ctx, 1 if enable else 0), "mv_set_stage_timing")
 
@@ -294,6 +305,17 @@ def block_preimage(bincode: bytes) -> Optional[bytes]:
     out = np.zeros(max(n, 1), dtype=np.uint8)
     lib.mv_block_preimage(_p(b), len(bincode), _p(out), n)
     return out[:n].tobytes()
+
+
+def shard_plan(weights, parts: int) -> List[int]:
+    """Host-only: the contiguous shard cuts the multi-device paths use (balanced by weight)."""
+    lib = load_library()
+    w = np.ascontiguousarray(np.asarray(weights, dtype=np.uint64))
+    cut = np.zeros(parts + 1, dtype=np.uint64)
+    rc = lib.mv_shard_plan(_p(w) if w.size else None, w.size, parts, _p(cut))
+    if rc != MV_OK:
+        raise MvError(f"mv_shard_plan failed ({rc})")
+    return [int(c) for c in cut]
 
 
 def version() -> str:

@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -140,8 +142,26 @@ struct mv_ctx {
   std::vector<PendingEvents> pending;
   double stage_ms[MV_NSTAGES] = {0};
   uint64_t stage_calls[MV_NSTAGES] = {0};
-  bool has_committee = false;
+  std::atomic<bool> has_committee{false};
   mvh::Committee committee;
+  // block submission queue (mv_verify_blocks): concurrent callers' requests are merged into
+  // one device pass by whichever caller finds the engine idle (flat combining)
+  struct BlockReq;
+  std::mutex q_mu;
+  std::condition_variable q_cv;
+  std::deque<BlockReq*> q;
+  bool q_busy = false;
+  std::atomic<uint64_t> q_calls{0}, q_passes{0};
+};
+
+struct mv_ctx::BlockReq {
+  const uint8_t* buf;
+  const uint64_t *off, *len;
+  uint32_t n;
+  uint8_t *status, *md, *bd;
+  mv_status rc = MV_OK;
+  std::string err;
+  bool done = false;
 };
 
 namespace {
@@ -169,18 +189,17 @@ mv_status set_err(mv_ctx* ctx, mv_status code, const std::string& msg) {
   return code;
 }
 
-// Runs fn(device, lo, hi) for each device's contiguous shard of [0, n), one thread per device.
+// Runs fn(device, cut[d], cut[d + 1]) for every device with a non-empty shard, one thread
+// per device (cut: nd + 1 ascending item indices from 0 to n).
 template <class Fn>
-mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
+mv_status for_each_cut(mv_ctx* ctx, const std::vector<uint64_t>& cut, Fn fn) {
   const size_t nd = ctx->devs.size();
-  if (nd == 1 || n < 2 * 256) {
-    return fn(ctx->devs[0], 0, n);
-  }
   std::vector<mv_status> rc(nd, MV_OK);
   std::vector<std::string> errs(nd);
   std::vector<std::thread> th;
   for (size_t d = 0; d < nd; d++) {
-    uint64_t lo = n * d / nd, hi = n * (d + 1) / nd;
+    const uint64_t lo = cut[d], hi = cut[d + 1];
+    if (lo == hi) continue;
     th.emplace_back([&, d, lo, hi] {
       t_err = &errs[d];
       rc[d] = fn(ctx->devs[d], lo, hi);
@@ -194,6 +213,16 @@ mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
       return rc[d];
     }
   return MV_OK;
+}
+
+// Runs fn(device, lo, hi) for each device's contiguous shard of [0, n) (equal counts).
+template <class Fn>
+mv_status for_each_shard(mv_ctx* ctx, uint64_t n, Fn fn) {
+  const size_t nd = ctx->devs.size();
+  if (nd == 1 || n < 2 * 256) return fn(ctx->devs[0], 0, n);
+  std::vector<uint64_t> cut(nd + 1);
+  for (size_t d = 0; d <= nd; d++) cut[d] = n * d / nd;
+  return for_each_cut(ctx, cut, fn);
 }
 
 // count + 1 timing events (empty when stage timing is off)
@@ -482,6 +511,121 @@ mv_status verify_blocks_host_parse(mv_ctx* ctx, const uint8_t* buf, const uint64
   });
 }
 
+// cut[0..parts]: contiguous shards of [0, n) with about equal sums of weights (bytes of
+// bincode for block calls): cut[d] is the item boundary whose prefix sum is
+// closest to d/parts of the total; every shard is non-empty while n >= parts.
+std::vector<uint64_t> balanced_cuts(const uint64_t* w, uint64_t n, uint32_t parts) {
+  std::vector<long double> pre(n + 1, 0.0L);
+  for (uint64_t i = 0; i < n; i++) pre[i + 1] = pre[i] + (long double)w[i];
+  std::vector<uint64_t> cut(parts + 1, n);
+  cut[0] = 0;
+  for (uint32_t d = 1; d < parts; d++) {
+    const long double target = pre[n] * d / parts;
+    uint64_t c = (uint64_t)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+    if (c > 0 && c <= n && target - pre[c - 1] < pre[c] - target) c--;
+    if (c > n) c = n;
+    const uint64_t lo = cut[d - 1] + (n >= parts ? 1 : 0);
+    const uint64_t hi = n >= parts ? n - (parts - d) : n;
+    cut[d] = c < lo ? lo : (c > hi ? hi : c);
+  }
+  return cut;
+}
+
+// One device pass over a list of blocks gathered from several requests: raw bincode packed
+// (8-aligned, 16 zero bytes after the last block) with offset/length arrays into pinned
+// staging, one H2D; parse, hashes, signatures and checks on the GPU; one D2H of
+// [msg digests | block digests | statuses]; verdicts scattered back to each block's owner.
+struct BlockItem {
+  const uint8_t* p;
+  uint64_t len;
+  uint8_t *st, *md, *bd;
+};
+
+mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint64_t lo, uint64_t hi) {
+  HIPCHK(ctx, hipSetDevice(dev.id));
+  uint64_t i = lo;
+  while (i < hi) {
+    uint64_t j = i, bytes = 0;
+    while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += (it[j++].len + 7) & ~7ull;
+    const uint32_t m = (uint32_t)(j - i);
+    const size_t buf_bytes = (bytes + 16 + 15) & ~(size_t)15;
+    const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
+    HIPCHK(ctx, dev.h_in.ensure(total));
+    uint8_t* h = dev.h_in.as<uint8_t>();
+    uint64_t* hoff = (uint64_t*)(h + o_off);
+    uint64_t* hlen = (uint64_t*)(h + o_len);
+    uint64_t pos = 0;
+    for (uint32_t k = 0; k < m; k++) {
+      const uint64_t l = it[i + k].len;
+      memcpy(h + pos, it[i + k].p, l);
+      hoff[k] = pos;
+      hlen[k] = l;
+      const uint64_t next = (pos + l + 7) & ~7ull;
+      memset(h + pos + l, 0, next - pos - l);
+      pos = next;
+    }
+    memset(h + pos, 0, buf_bytes - pos);
+    HIPCHK(ctx, dev.bytes.ensure(total));
+    HIPCHK(ctx, dev.out2.ensure(65 * (size_t)m + 256));
+    HIPCHK(ctx, dev.h_out.ensure(65 * (size_t)m));
+    HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
+    uint8_t* dout = dev.out2.as<uint8_t>();
+    const uint8_t* dbuf = dev.bytes.as<uint8_t>();
+    mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
+                                  (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
+                                  dout + 32 * (size_t)m, dev.stream);
+    if (st != MV_OK) return st;
+    HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
+    HIPCHK(ctx, hipStreamSynchronize(dev.stream));
+    poll_flags(ctx, dev);
+    const uint8_t* ho = dev.h_out.as<uint8_t>();
+    for (uint32_t k = 0; k < m; k++) {
+      const BlockItem& b = it[i + k];
+      *b.st = ho[64 * (size_t)m + k];
+      if (b.md) memcpy(b.md, ho + 32 * (size_t)k, 32);
+      if (b.bd) memcpy(b.bd, ho + 32 * ((size_t)m + k), 32);
+    }
+    i = j;
+  }
+  return MV_OK;
+}
+
+// The combining caller's pass over every request it took from the queue.
+void run_block_requests(mv_ctx* ctx, std::vector<mv_ctx::BlockReq*>& reqs) {
+  std::vector<BlockItem> items;
+  size_t total = 0;
+  for (auto* r : reqs) total += r->n;
+  items.reserve(total);
+  for (auto* r : reqs)
+    for (uint32_t k = 0; k < r->n; k++)
+      items.push_back(BlockItem{r->buf + r->off[k], r->len[k], r->status + k, r->md ? r->md + 32 * (size_t)k : nullptr,
+                                r->bd ? r->bd + 32 * (size_t)k : nullptr});
+  std::string err;
+  mv_status rc;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->q_passes++;
+    t_err = &err;
+    const size_t nd = ctx->devs.size();
+    if (nd == 1 || items.size() < 2 * nd) {
+      rc = verify_block_items(ctx, ctx->devs[0], items.data(), 0, items.size());
+    } else {
+      std::vector<uint64_t> w(items.size());
+      for (size_t k = 0; k < items.size(); k++) w[k] = items[k].len + 64;  // bytes, plus a per-block constant
+      rc = for_each_cut(ctx, balanced_cuts(w.data(), w.size(), (uint32_t)nd),
+                        [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
+                          return verify_block_items(ctx, dev, items.data(), lo, hi);
+                        });
+      if (rc != MV_OK) err = ctx->err;
+    }
+    t_err = nullptr;
+  }
+  for (auto* r : reqs) {
+    r->rc = rc;
+    if (rc != MV_OK) r->err = err;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -521,15 +665,20 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
       return MV_E_INVALID_ARG;  // no entropy source: refuse rather than use predictable z_i
     }
   }
+  // shards_per_device > 1: several logical devices (stream + buffers each) per HIP device;
+  // host-buffer calls shard across them as across GPUs (tests the sharding on one GPU)
+  const uint32_t reps = cfg && cfg->shards_per_device > 1 ? (cfg->shards_per_device > 8 ? 8 : cfg->shards_per_device) : 1;
   for (int d = 0; d < 32; d++) {
     if (!(mask & (1u << d))) continue;
     if (d >= ndev) {
       delete ctx;
       return MV_E_NO_DEVICE;
     }
-    Device dev;
-    dev.id = d;
-    ctx->devs.push_back(dev);
+    for (uint32_t r = 0; r < reps; r++) {
+      Device dev;
+      dev.id = d;
+      ctx->devs.push_back(dev);
+    }
   }
   for (auto& dev : ctx->devs) {
     hipError_t e = hipSetDevice(dev.id);
@@ -736,58 +885,54 @@ mv_status mv_ed25519_sign(mv_ctx* ctx, const uint8_t* seed, const uint8_t* msg, 
 mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                            uint8_t* status, uint8_t* msg_digest, uint8_t* block_digest) {
   if (!ctx || (n && (!buf || !off || !len || !status))) return set_err(ctx, MV_E_INVALID_ARG, "bad block args");
-  std::lock_guard<std::mutex> lk(ctx->mu);
   if (!ctx->has_committee) return set_err(ctx, MV_E_NO_COMMITTEE, "mv_set_committee first");
-  if (ctx->flags & MV_FLAG_HOST_PARSE) return verify_blocks_host_parse(ctx, buf, off, len, n, status, msg_digest,
-                                                                       block_digest);
-  // Device ingest: the host only packs the raw bincode (8-aligned, 16 pad bytes after the
-  // last block) with the offset and length arrays into pinned staging, one H2D; parse,
-  // hashes, signatures and checks run on the GPU; one D2H of [digests | digests | status].
-  return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
-    HIPCHK(ctx, hipSetDevice(dev.id));
-    uint64_t i = lo;
-    while (i < hi) {
-      uint64_t j = i, bytes = 0;
-      while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += (len[j++] + 7) & ~7ull;
-      const uint32_t m = (uint32_t)(j - i);
-      const size_t buf_bytes = (bytes + 16 + 15) & ~(size_t)15;
-      const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
-      HIPCHK(ctx, dev.h_in.ensure(total));
-      uint8_t* h = dev.h_in.as<uint8_t>();
-      uint64_t* hoff = (uint64_t*)(h + o_off);
-      uint64_t* hlen = (uint64_t*)(h + o_len);
-      uint64_t pos = 0;
-      for (uint32_t k = 0; k < m; k++) {
-        const uint64_t l = len[i + k];
-        memcpy(h + pos, buf + off[i + k], l);
-        hoff[k] = pos;
-        hlen[k] = l;
-        const uint64_t next = (pos + l + 7) & ~7ull;
-        memset(h + pos + l, 0, next - pos - l);
-        pos = next;
-      }
-      memset(h + pos, 0, buf_bytes - pos);
-      HIPCHK(ctx, dev.bytes.ensure(total));
-      HIPCHK(ctx, dev.out2.ensure(65 * (size_t)m + 256));
-      HIPCHK(ctx, dev.h_out.ensure(65 * (size_t)m));
-      HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
-      uint8_t* dout = dev.out2.as<uint8_t>();
-      const uint8_t* dbuf = dev.bytes.as<uint8_t>();
-      mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
-                                    (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
-                                    dout + 32 * (size_t)m, dev.stream);
-      if (st != MV_OK) return st;
-      HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
-      HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-      poll_flags(ctx, dev);
-      const uint8_t* ho = dev.h_out.as<uint8_t>();
-      memcpy(status + i, ho + 64 * (size_t)m, m);
-      if (msg_digest) memcpy(msg_digest + 32 * i, ho, 32 * (size_t)m);
-      if (block_digest) memcpy(block_digest + 32 * i, ho + 32 * (size_t)m, 32 * (size_t)m);
-      i = j;
+  if (n == 0) return MV_OK;
+  if (ctx->flags & MV_FLAG_HOST_PARSE) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return verify_blocks_host_parse(ctx, buf, off, len, n, status, msg_digest, block_digest);
+  }
+  // Flat combining: the request joins the queue; a caller that finds no pass running takes
+  // every queued request (its own included) into one device pass, so n - 1 peer tasks each
+  // submitting a block or two (net_sync.rs:214-221, 314-386) share one GPU round trip.
+  mv_ctx::BlockReq req{buf, off, len, n, status, msg_digest, block_digest};
+  ctx->q_calls++;
+  std::unique_lock<std::mutex> ql(ctx->q_mu);
+  ctx->q.push_back(&req);
+  while (!req.done) {
+    if (ctx->q_busy) {
+      ctx->q_cv.wait(ql);
+      continue;
     }
-    return MV_OK;
-  });
+    ctx->q_busy = true;
+    std::vector<mv_ctx::BlockReq*> batch(ctx->q.begin(), ctx->q.end());
+    ctx->q.clear();
+    ql.unlock();
+    run_block_requests(ctx, batch);
+    ql.lock();
+    for (auto* r : batch) r->done = true;
+    ctx->q_busy = false;
+    ctx->q_cv.notify_all();
+  }
+  ql.unlock();
+  if (req.rc != MV_OK) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->err = req.err;
+  }
+  return req.rc;
+}
+
+mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes) {
+  if (!ctx) return MV_E_INVALID_ARG;
+  if (calls) *calls = ctx->q_calls.load();
+  if (passes) *passes = ctx->q_passes.load();
+  return MV_OK;
+}
+
+mv_status mv_shard_plan(const uint64_t* weights, uint64_t n, uint32_t parts, uint64_t* cut) {
+  if ((n && !weights) || !cut || parts == 0) return MV_E_INVALID_ARG;
+  std::vector<uint64_t> c = balanced_cuts(weights, n, parts);
+  memcpy(cut, c.data(), sizeof(uint64_t) * (parts + 1));
+  return MV_OK;
 }
 
 static Device* find_dev(mv_ctx* ctx, int device) {

@@ -14,7 +14,6 @@
  *                      threshold_clock_valid_non_genesis threshold_clock.rs:12-35;
  *                      quorum = stake > 2*total/3 (committee.rs:56-57,125-127).
  */
-#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
@@ -273,30 +272,18 @@ typedef struct {
   uint32_t n_auth;
   uint64_t epoch;
   uint8_t *status, *msgd, *blkd;
-  size_t lo, hi;
 } bjob_t;
 
-static void* block_worker(void* arg) {
+static void block_item(void* arg, size_t i) {
   bjob_t* j = (bjob_t*)arg;
-  for (size_t i = j->lo; i < j->hi; i++)
-    j->status[i] = (uint8_t)orc_block_verify(j->buf + j->off[i], j->len[i], j->pks, j->stakes, j->n_auth, j->epoch,
-                                             j->msgd ? j->msgd + 32 * i : NULL, j->blkd ? j->blkd + 32 * i : NULL);
-  return NULL;
+  j->status[i] = (uint8_t)orc_block_verify(j->buf + j->off[i], j->len[i], j->pks, j->stakes, j->n_auth, j->epoch,
+                                           j->msgd ? j->msgd + 32 * i : NULL, j->blkd ? j->blkd + 32 * i : NULL);
 }
 
+/* persistent pool (pool.c), one block per item */
 void orc_block_verify_batch(const uint8_t* buf, const uint64_t* off, const uint64_t* len, size_t n,
                             const uint8_t* committee_pks, const uint64_t* stakes, uint32_t n_auth, uint64_t epoch,
                             uint8_t* status, uint8_t* msg_digests, uint8_t* block_digests, int threads) {
-  if (threads <= 0) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
-  if (threads > 256) threads = 256;
-  if ((size_t)threads > n) threads = n ? (int)n : 1;
-  pthread_t tid[256];
-  bjob_t jobs[256];
-  for (int t = 0; t < threads; t++) {
-    bjob_t j = {buf, off, len, committee_pks, stakes, n_auth, epoch, status, msg_digests, block_digests,
-                n * t / threads, n * (t + 1) / threads};
-    jobs[t] = j;
-    pthread_create(&tid[t], NULL, block_worker, &jobs[t]);
-  }
-  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  bjob_t j = {buf, off, len, committee_pks, stakes, n_auth, epoch, status, msg_digests, block_digests};
+  orc_parallel_for(n, threads, 1, block_item, &j);
 }

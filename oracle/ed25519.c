@@ -665,51 +665,31 @@ void orc_ed25519_sign(const uint8_t seed[32], const uint8_t* msg, size_t msg_len
   sc_muladd(sig + 32, k, a_red, r);
 }
 
-/* ---------------- threaded batches ---------------- */
+/* ---------------- threaded batches (persistent pool, pool.c) ---------------- */
 typedef struct {
   const uint8_t *pk, *sig, *msg, *seed;
   uint8_t *status, *pk_out, *sig_out;
-  size_t lo, hi;
 } batch_job;
 
-static void* verify_worker(void* arg) {
+static void verify_item(void* arg, size_t i) {
   batch_job* j = (batch_job*)arg;
-  for (size_t i = j->lo; i < j->hi; i++)
-    j->status[i] = (uint8_t)orc_ed25519_verify(j->pk + 32 * i, j->sig + 64 * i, j->msg + 32 * i, 32);
-  return NULL;
+  j->status[i] = (uint8_t)orc_ed25519_verify(j->pk + 32 * i, j->sig + 64 * i, j->msg + 32 * i, 32);
 }
-static void* sign_worker(void* arg) {
+static void sign_item(void* arg, size_t i) {
   batch_job* j = (batch_job*)arg;
-  for (size_t i = j->lo; i < j->hi; i++) {
-    orc_ed25519_pubkey(j->seed + 32 * i, j->pk_out + 32 * i);
-    orc_ed25519_sign(j->seed + 32 * i, j->msg + 32 * i, 32, j->sig_out + 64 * i);
-  }
-  return NULL;
-}
-
-static void run_threads(void* (*fn)(void*), batch_job* proto, size_t n, int threads) {
-  ensure_init();
-  if (threads <= 0) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
-  if (threads > 256) threads = 256;
-  if ((size_t)threads > n) threads = n ? (int)n : 1;
-  pthread_t tid[256];
-  batch_job jobs[256];
-  for (int t = 0; t < threads; t++) {
-    jobs[t] = *proto;
-    jobs[t].lo = n * t / threads;
-    jobs[t].hi = n * (t + 1) / threads;
-    pthread_create(&tid[t], NULL, fn, &jobs[t]);
-  }
-  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  orc_ed25519_pubkey(j->seed + 32 * i, j->pk_out + 32 * i);
+  orc_ed25519_sign(j->seed + 32 * i, j->msg + 32 * i, 32, j->sig_out + 64 * i);
 }
 
 void orc_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg32, size_t n,
                               uint8_t* status, int threads) {
-  batch_job j = {pk, sig, msg32, NULL, status, NULL, NULL, 0, 0};
-  run_threads(verify_worker, &j, n, threads);
+  ensure_init();
+  batch_job j = {pk, sig, msg32, NULL, status, NULL, NULL};
+  orc_parallel_for(n, threads, 64, verify_item, &j);
 }
 void orc_ed25519_sign_batch(const uint8_t* seed, const uint8_t* msg32, size_t n, uint8_t* pk, uint8_t* sig,
                             int threads) {
-  batch_job j = {NULL, NULL, msg32, seed, NULL, pk, sig, 0, 0};
-  run_threads(sign_worker, &j, n, threads);
+  ensure_init();
+  batch_job j = {NULL, NULL, msg32, seed, NULL, pk, sig};
+  orc_parallel_for(n, threads, 64, sign_item, &j);
 }

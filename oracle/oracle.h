@@ -46,6 +46,11 @@ int orc_point_decodes(const uint8_t enc[32]);
 void orc_scalar_reduce_wide(const uint8_t in[64], uint8_t out[32]);
 
 /* batch verify on `threads` host threads (0 = all cores); msgs are 32 B each. */
+/* pool.c: fn(ctx, i) for i in [0, n) on `threads` threads (the caller + persistent workers),
+ * handed out `grain` items at a time. */
+typedef void (*orc_item_fn)(void* ctx, size_t i);
+void orc_parallel_for(size_t n, int threads, size_t grain, orc_item_fn fn, void* ctx);
+
 void orc_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg32, size_t n,
                               uint8_t* status, int threads);
 void orc_ed25519_sign_batch(const uint8_t* seed, const uint8_t* msg32, size_t n, uint8_t* pk, uint8_t* sig,

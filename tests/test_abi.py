@@ -82,3 +82,29 @@ def test_host_preimage_rejects_garbage():
     for _ in range(200):
         b = rng.integers(0, 256, size=int(rng.integers(0, 400)), dtype=np.uint8).tobytes()
         assert M.block_preimage(b) == O.block_preimage(b)
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 8])
+def test_shard_plan_balances_ragged_bytes(lib, parts):
+    """The multi-device split: contiguous shards covering every item once, each
+    non-empty; every cut is the item boundary whose byte prefix is closest to its share of the
+    total (so no shard exceeds the ideal share by more than the largest block)."""
+    import mysticeti_amd as M
+
+    rng = np.random.default_rng(parts)
+    for n in (parts, parts + 1, 37, 1000):
+        w = rng.integers(41, 20000, size=n).astype(np.uint64)
+        w[rng.integers(0, n, size=max(1, n // 50))] = 2_000_000  # a few huge blocks
+        cut = M.shard_plan(w, parts)
+        assert cut[0] == 0 and cut[-1] == n and all(a < b for a, b in zip(cut, cut[1:]))
+        share = float(w.sum()) / parts
+        pre = np.concatenate([[0], np.cumsum(w.astype(np.float64))])
+        for d in range(1, parts):
+            c, target = cut[d], share * d
+            lo, hi = cut[d - 1] + 1, n - (parts - d)  # non-empty shards on both sides
+            best = min(range(lo, hi + 1), key=lambda k: abs(pre[k] - target))
+            assert abs(pre[c] - target) <= abs(pre[best] - target) + 1e-6, (n, d, cut)
+        sums = [int(w[a:b].sum()) for a, b in zip(cut, cut[1:])]
+        assert max(sums) <= share + int(w.max()) + 1
+    assert M.shard_plan([], 4) == [0, 0, 0, 0, 0]
+    assert M.shard_plan([5, 5], 4)[-1] == 2
