@@ -145,6 +145,7 @@ def main():
                          "config4: HBM-resident 100-validator blocks through the device block pipeline; "
                          "config5: p50/p99 latency of 64-block batches, GPU vs host cores")
     ap.add_argument("--batches", type=int, default=10000, help="config5: GPU batches timed per shape")
+    ap.add_argument("--conc-seconds", type=float, default=3.0, help="config5: seconds of concurrent 1-block callers")
     ap.add_argument("--corrupt", type=int, default=0, help="signatures per batch with a flipped s bit")
     ap.add_argument("--groups", type=int, default=0, help="sub-batch equations per batch (0 = adaptive)")
     ap.add_argument("--sustain-repeats", type=int, default=5, help="repeats of the sustained-rate measurement")

@@ -416,7 +416,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   }
   if (st != MV_OK) return st;
   HIPCHK(ctx, mark(3));
-  HIPCHK(ctx, mvk::launch_block_verdict(facts, claimed, bd, sst, n, d_status, s));
+  HIPCHK(ctx, mvk::launch_block_verdict(facts, claimed, md, bd, sst, n, d_status, s));
   HIPCHK(ctx, mark(4));
   keep_events(ctx, dev.id, kBlockStage0, evs);
   HIPCHK(ctx, hipEventRecord(dev.blk_done[slot], s));
@@ -502,6 +502,10 @@ mv_status verify_blocks_host_parse(mv_ctx* ctx, const uint8_t* buf, const uint64
       poll_flags(ctx, dev);
       for (uint32_t k = 0; k < m; k++) {
         status[i + k] = mvh::block_verdict(facts[k], com, &bd[32 * (size_t)k], ss[k]);
+        if (!facts[k].parsed) {  // no pre-image: zero digests, as the device path
+          memset(&md[32 * (size_t)k], 0, 32);
+          memset(&bd[32 * (size_t)k], 0, 32);
+        }
         if (msg_digest) memcpy(msg_digest + 32 * (i + k), &md[32 * (size_t)k], 32);
         if (block_digest) memcpy(block_digest + 32 * (i + k), &bd[32 * (size_t)k], 32);
       }

@@ -660,10 +660,12 @@ __global__ void __launch_bounds__(256) k_block_digest_gate(const uint8_t* __rest
   s4[1] = make_uint4(~0u, ~0u, ~0u, ~0u);
 }
 
-// status[i] in the order of StatementBlock::verify (types.rs:315-376)
+// status[i] in the order of StatementBlock::verify (types.rs:315-376). A block that does not
+// deserialize has no pre-image: its two digests are zeroed, so every output is deterministic.
 __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restrict__ facts,
                                                        const uint8_t* __restrict__ claimed,
-                                                       const uint8_t* __restrict__ digest,
+                                                       uint8_t* __restrict__ msg_digest,
+                                                       uint8_t* __restrict__ digest,
                                                        const uint8_t* __restrict__ sig_status, uint32_t n,
                                                        uint8_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -672,6 +674,13 @@ __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restric
   uint8_t st;
   if (!(f & BF_PARSED)) {
     st = MV_BLOCK_PARSE_ERROR;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    uint4* m4 = reinterpret_cast<uint4*>(msg_digest + 32 * (size_t)i);
+    uint4* d4 = reinterpret_cast<uint4*>(digest + 32 * (size_t)i);
+    m4[0] = z;
+    m4[1] = z;
+    d4[0] = z;
+    d4[1] = z;
   } else {
     const bool same = digest_same(claimed, digest, i);
     const uint32_t inc = (f >> BF_INC_SHIFT) & 0xffu;
@@ -718,11 +727,11 @@ hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* diges
   return hipGetLastError();
 }
 
-hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, const uint8_t* digest,
+hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, uint8_t* msg_digest, uint8_t* digest,
                                 const uint8_t* sig_status, uint32_t n, uint8_t* status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mv::k_block_verdict, dim3((n + 255) / 256), dim3(256), 0, s, facts, claimed, digest, sig_status,
-                     n, status);
+  hipLaunchKernelGGL(mv::k_block_verdict, dim3((n + 255) / 256), dim3(256), 0, s, facts, claimed, msg_digest, digest,
+                     sig_status, n, status);
   return hipGetLastError();
 }
 

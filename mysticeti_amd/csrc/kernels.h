@@ -61,6 +61,7 @@ hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uin
 // digest differs from its claimed one
 hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* digest, const uint32_t* facts, uint32_t n,
                                     uint8_t* sig, hipStream_t s);
-hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, const uint8_t* digest,
+// status in the types.rs order; zeroes both digests of blocks that do not deserialize
+hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, uint8_t* msg_digest, uint8_t* digest,
                                 const uint8_t* sig_status, uint32_t n, uint8_t* status, hipStream_t s);
 }  // namespace mvk
