@@ -1,14 +1,17 @@
 /* ORACLE / TEST INFRASTRUCTURE ONLY: a persistent worker pool for the CPU legs.
  *
- * orc_parallel_for(n, threads, fn, ctx) runs fn(ctx, i) for i in [0, n) on `threads`
+ * orc_parallel_for(n, threads, grain, fn, ctx) runs fn(ctx, i) for i in [0, n) on `threads`
  * threads: the caller plus threads - 1 pool workers that live for the process. Items are
- * handed out one grain at a time from an atomic counter (dynamic balance for ragged
- * blocks). Workers spin briefly on the job generation before sleeping on a condition
- * variable, so back-to-back small batches (the config-5 latency path: 64 blocks, a few
- * hundred microseconds of work) pay neither thread creation nor a sleep/wake per batch.
- * Replaces the thread-per-batch pthread_create/join of round 1.
+ * handed out one grain at a time from an atomic counter (dynamic balance for ragged blocks).
+ * Every worker has its own mailbox: the caller posts the job's generation to the mailboxes of
+ * exactly the helpers it wants and waits for each of them to post it back, so a worker can
+ * never act on another job's parameters. Workers spin briefly on their mailbox before
+ * sleeping on a condition variable, so back-to-back small batches (the config-5 latency path:
+ * 64 blocks, a few hundred microseconds of work) pay neither thread creation nor a sleep and
+ * wake per batch. Replaces the thread-per-batch pthread_create/join of round 1.
  */
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -18,34 +21,27 @@
 #include "oracle.h"
 
 #define POOL_MAX 256
-#define SPIN_ITERS 200000 /* ~50-100 us of pause loops before a worker sleeps */
+#define SPIN_ITERS 2000 /* ~30 us of pause loops before a worker sleeps */
 
 typedef struct {
+  _Atomic uint64_t post; /* generation of the job this worker must take part in */
+  _Atomic uint64_t done; /* generation it has finished */
+  char pad[48];
+} mailbox_t;
+
+static struct {
   pthread_mutex_t mu;
   pthread_cond_t cv;
   pthread_mutex_t submit_mu; /* one job at a time */
   int nworkers;
-  _Atomic uint64_t gen;
-  /* current job */
+  uint64_t gen;
+  /* the current job, written before any mailbox is posted */
   orc_item_fn fn;
   void* ctx;
   size_t n, grain;
-  int active; /* workers (by index) taking part */
   _Atomic size_t next;
-  _Atomic int finished;
-} pool_t;
-
-static pool_t g_pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, 0, 0,
-                        NULL, NULL, 0, 1, 0, 0, 0};
-
-static void run_items(pool_t* p) {
-  for (;;) {
-    size_t i = atomic_fetch_add(&p->next, p->grain);
-    if (i >= p->n) break;
-    size_t e = i + p->grain < p->n ? i + p->grain : p->n;
-    for (; i < e; i++) p->fn(p->ctx, i);
-  }
-}
+  mailbox_t box[POOL_MAX];
+} g_pool = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .submit_mu = PTHREAD_MUTEX_INITIALIZER};
 
 static inline void cpu_relax(void) {
 #if defined(__x86_64__)
@@ -53,30 +49,33 @@ static inline void cpu_relax(void) {
 #endif
 }
 
-/* arg = worker index (low 16 bits) | the job generation current when it was created (the
- * next job, not yet published, is the first one it must take) */
+static void run_items(void) {
+  for (;;) {
+    size_t i = atomic_fetch_add(&g_pool.next, g_pool.grain);
+    if (i >= g_pool.n) break;
+    size_t e = i + g_pool.grain < g_pool.n ? i + g_pool.grain : g_pool.n;
+    for (; i < e; i++) g_pool.fn(g_pool.ctx, i);
+  }
+}
+
 static void* worker(void* arg) {
-  const uint64_t a = (uint64_t)(uintptr_t)arg;
-  const int idx = (int)(a & 0xffff);
-  pool_t* p = &g_pool;
-  uint64_t seen = a >> 16;
+  mailbox_t* mb = &g_pool.box[(int)(intptr_t)arg];
+  uint64_t seen = 0; /* posts start at generation 1: a job posted before this thread ran is still seen */
   for (;;) {
     uint64_t g;
     int spins = 0;
-    while ((g = atomic_load_explicit(&p->gen, memory_order_acquire)) == seen && spins < SPIN_ITERS) {
+    while ((g = atomic_load_explicit(&mb->post, memory_order_acquire)) == seen && spins < SPIN_ITERS) {
       cpu_relax();
       spins++;
     }
     if (g == seen) {
-      pthread_mutex_lock(&p->mu);
-      while ((g = atomic_load(&p->gen)) == seen) pthread_cond_wait(&p->cv, &p->mu);
-      pthread_mutex_unlock(&p->mu);
+      pthread_mutex_lock(&g_pool.mu);
+      while ((g = atomic_load(&mb->post)) == seen) pthread_cond_wait(&g_pool.cv, &g_pool.mu);
+      pthread_mutex_unlock(&g_pool.mu);
     }
     seen = g;
-    if (idx < p->active) {
-      run_items(p);
-      atomic_fetch_add_explicit(&p->finished, 1, memory_order_release);
-    }
+    run_items();
+    atomic_store_explicit(&mb->done, g, memory_order_release);
   }
   return NULL;
 }
@@ -85,37 +84,40 @@ void orc_parallel_for(size_t n, int threads, size_t grain, orc_item_fn fn, void*
   if (threads <= 0) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
   if (threads > POOL_MAX) threads = POOL_MAX;
   if (grain == 0) grain = 1;
-  if ((size_t)threads > (n + grain - 1) / grain) threads = n ? (int)((n + grain - 1) / grain) : 1;
-  pool_t* p = &g_pool;
-  pthread_mutex_lock(&p->submit_mu);
+  const size_t chunks = (n + grain - 1) / grain;
+  if ((size_t)threads > chunks) threads = chunks ? (int)chunks : 1;
+  pthread_mutex_lock(&g_pool.submit_mu);
   if (threads == 1) {
     for (size_t i = 0; i < n; i++) fn(ctx, i);
-    pthread_mutex_unlock(&p->submit_mu);
+    pthread_mutex_unlock(&g_pool.submit_mu);
     return;
   }
-  while (p->nworkers < threads - 1) {
+  while (g_pool.nworkers < threads - 1) {
     pthread_t t;
     pthread_attr_t a;
     pthread_attr_init(&a);
     pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
-    const uint64_t arg = ((uint64_t)atomic_load(&p->gen) << 16) | (uint64_t)p->nworkers;
-    if (pthread_create(&t, &a, worker, (void*)(uintptr_t)arg) != 0) break;
+    const int ok = pthread_create(&t, &a, worker, (void*)(intptr_t)g_pool.nworkers) == 0;
     pthread_attr_destroy(&a);
-    p->nworkers++;
+    if (!ok) break;
+    g_pool.nworkers++;
   }
-  const int helpers = threads - 1 < p->nworkers ? threads - 1 : p->nworkers;
-  p->fn = fn;
-  p->ctx = ctx;
-  p->n = n;
-  p->grain = grain;
-  p->active = helpers;
-  atomic_store(&p->next, 0);
-  atomic_store(&p->finished, 0);
-  pthread_mutex_lock(&p->mu);
-  atomic_fetch_add_explicit(&p->gen, 1, memory_order_release);
-  pthread_cond_broadcast(&p->cv);
-  pthread_mutex_unlock(&p->mu);
-  run_items(p);
-  while (atomic_load_explicit(&p->finished, memory_order_acquire) < helpers) cpu_relax();
-  pthread_mutex_unlock(&p->submit_mu);
+  const int helpers = threads - 1 < g_pool.nworkers ? threads - 1 : g_pool.nworkers;
+  const uint64_t g = ++g_pool.gen;
+  g_pool.fn = fn;
+  g_pool.ctx = ctx;
+  g_pool.n = n;
+  g_pool.grain = grain;
+  atomic_store(&g_pool.next, 0);
+  pthread_mutex_lock(&g_pool.mu);
+  for (int w = 0; w < helpers; w++) atomic_store_explicit(&g_pool.box[w].post, g, memory_order_release);
+  pthread_cond_broadcast(&g_pool.cv);
+  pthread_mutex_unlock(&g_pool.mu);
+  run_items();
+  for (int w = 0; w < helpers; w++)
+    for (int spins = 0; atomic_load_explicit(&g_pool.box[w].done, memory_order_acquire) != g; spins++) {
+      if (spins < SPIN_ITERS) cpu_relax();
+      else sched_yield();  /* more threads than free cores: let the helper run */
+    }
+  pthread_mutex_unlock(&g_pool.submit_mu);
 }
