@@ -66,8 +66,11 @@ typedef int32_t mv_status;
 #define MV_BLOCK_SIG_INVALID 6             /* types.rs:346-348 */
 #define MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY 7 /* types.rs:350-355 */
 #define MV_BLOCK_INCLUDE_ROUND 8           /* types.rs:356-361 */
-#define MV_BLOCK_VOTE_RANGE 9              /* types.rs:363-370, 440-460 */
+#define MV_BLOCK_VOTE_RANGE 9              /* first failing VoteRange (types.rs:363-370): end < start, */
+                                           /* "offset_end_exclusive must be greater or equal ..." :441-446 */
 #define MV_BLOCK_THRESHOLD_CLOCK 10        /* types.rs:371-374, threshold_clock.rs:12-35 */
+#define MV_BLOCK_VOTE_RANGE_TOO_LONG 11    /* end - start >= 2^20, "Include is too large ..." :447-453 */
+#define MV_BLOCK_VOTE_RANGE_END_TOO_LARGE 12 /* end >= 2^20, "offset_end_exclusive is too large ..." :454-458 */
 
 /* mv_config.flags */
 #define MV_FLAG_NO_BATCH 1u /* host-buffer verify: never use the batch (random linear combination) path */

@@ -29,11 +29,12 @@ MV_OK = 0
 SIG_OK, SIG_INVALID, SIG_MALFORMED_KEY = 0, 1, 2
 BLOCK_STATUS = [
     "OK", "PARSE_ERROR", "DIGEST_MISMATCH", "EPOCH_MISMATCH", "UNKNOWN_AUTHOR", "GENESIS", "SIG_INVALID",
-    "INCLUDE_UNKNOWN_AUTHORITY", "INCLUDE_ROUND", "VOTE_RANGE", "THRESHOLD_CLOCK",
+    "INCLUDE_UNKNOWN_AUTHORITY", "INCLUDE_ROUND", "VOTE_RANGE", "THRESHOLD_CLOCK", "VOTE_RANGE_TOO_LONG",
+    "VOTE_RANGE_END_TOO_LARGE",
 ]
 (BLOCK_OK, BLOCK_PARSE_ERROR, BLOCK_DIGEST_MISMATCH, BLOCK_EPOCH_MISMATCH, BLOCK_UNKNOWN_AUTHOR,
  BLOCK_GENESIS, BLOCK_SIG_INVALID, BLOCK_INCLUDE_UNKNOWN_AUTHORITY, BLOCK_INCLUDE_ROUND,
- BLOCK_VOTE_RANGE, BLOCK_THRESHOLD_CLOCK) = range(11)
+ BLOCK_VOTE_RANGE, BLOCK_THRESHOLD_CLOCK, BLOCK_VOTE_RANGE_TOO_LONG, BLOCK_VOTE_RANGE_END_TOO_LARGE) = range(13)
 
 EXPORTS = [
     "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",

@@ -187,7 +187,12 @@ bool parse_block(const uint8_t* buf, size_t len, const Committee* committee, uin
       write_ref(w, blk);
       w.be64(start);
       w.be64(end);
-      if (end < start || end - start >= kMaxRangeLen || end >= kMaxRangeLen) f.vote_range_bad = true;
+      // VoteRange::verify (types.rs:440-460): its three checks in order; the first failing range decides
+      if (!f.vote_range_error)
+        f.vote_range_error = end < start                    ? MV_BLOCK_VOTE_RANGE
+                             : end - start >= kMaxRangeLen ? MV_BLOCK_VOTE_RANGE_TOO_LONG
+                             : end >= kMaxRangeLen         ? MV_BLOCK_VOTE_RANGE_END_TOO_LARGE
+                                                           : 0;
     } else {
       return false;
     }
@@ -217,7 +222,7 @@ uint8_t block_verdict(const BlockFacts& f, const Committee& c, const uint8_t com
   if (f.round == 0) return MV_BLOCK_GENESIS;
   if (sig_status != MV_SIG_OK) return MV_BLOCK_SIG_INVALID;
   if (f.include_error) return f.include_error;
-  if (f.vote_range_bad) return MV_BLOCK_VOTE_RANGE;
+  if (f.vote_range_error) return f.vote_range_error;
   if (!f.threshold_ok) return MV_BLOCK_THRESHOLD_CLOCK;
   return MV_BLOCK_OK;
 }

@@ -33,7 +33,7 @@ struct BlockFacts {
   uint8_t claimed_digest[32];
   uint8_t signature[64];
   uint8_t include_error = 0;  // 0, MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY or MV_BLOCK_INCLUDE_ROUND (first failing include)
-  bool vote_range_bad = false;
+  uint8_t vote_range_error = 0;  // first failing VoteRange: MV_BLOCK_VOTE_RANGE* or 0
   bool threshold_ok = false;
   uint64_t preimage_len = 0;
 };

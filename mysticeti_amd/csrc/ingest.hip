@@ -25,10 +25,16 @@
 
 namespace mv {
 
-constexpr uint32_t BF_PARSED = 1u, BF_EPOCH_OK = 2u, BF_AUTHOR_OK = 4u, BF_GENESIS = 8u, BF_VR_BAD = 16u,
-                   BF_QUORUM = 32u;
+constexpr uint32_t BF_PARSED = 1u, BF_EPOCH_OK = 2u, BF_AUTHOR_OK = 4u, BF_GENESIS = 8u, BF_QUORUM = 32u;
 constexpr int BF_INC_SHIFT = 8;               // first failing include: MV_BLOCK_INCLUDE_* or 0
+constexpr int BF_VR_SHIFT = 16;               // first failing VoteRange: vr_code() or 0
 constexpr uint64_t VR_MAX_LEN = 1024 * 1024;  // VoteRange::verify MAX_LEN (types.rs:448)
+
+// VoteRange::verify (types.rs:440-460), its checks in order: 1 = end < start, 2 = length
+// >= MAX_LEN, 3 = end >= MAX_LEN, 0 = valid
+MV_DEV uint32_t vr_code(uint64_t s0, uint64_t s1) {
+  return s1 < s0 ? 1u : (s1 - s0 >= VR_MAX_LEN ? 2u : (s1 >= VR_MAX_LEN ? 3u : 0u));
+}
 
 // 8 little-endian bytes at any address (the buffer is readable 16 bytes past every block)
 MV_DEV uint64_t peek8(const uint8_t* p) {
@@ -178,7 +184,7 @@ MV_DEV void ingest_lane(const uint8_t* buf, uint64_t o, uint64_t L, uint32_t i, 
   }
   // statements
   const uint64_t n_st = r.u64();
-  bool vr_bad = false;
+  uint32_t vr_first = 0;
   for (uint64_t k = 0; r.ok && k < n_st; k++) {
     const uint32_t tag = r.u32();
     if (!r.ok) break;
@@ -233,7 +239,7 @@ MV_DEV void ingest_lane(const uint8_t* buf, uint64_t o, uint64_t L, uint32_t i, 
       w.ref(a, rd, d);
       w.be64(s0);
       w.be64(s1);
-      if (s1 < s0 || s1 - s0 >= VR_MAX_LEN || s1 >= VR_MAX_LEN) vr_bad = true;
+      if (!vr_first) vr_first = vr_code(s0, s1);
     } else {
       r.ok = false;
     }
@@ -266,7 +272,7 @@ MV_DEV void ingest_lane(const uint8_t* buf, uint64_t o, uint64_t L, uint32_t i, 
     w.flush();
     io.pre_len[i] = plen;
     f = BF_PARSED | (ep == cv.epoch ? BF_EPOCH_OK : 0u) | (me_a < n_auth ? BF_AUTHOR_OK : 0u) |
-        (me_r == 0 ? BF_GENESIS : 0u) | (vr_bad ? BF_VR_BAD : 0u) | (quorum ? BF_QUORUM : 0u) |
+        (me_r == 0 ? BF_GENESIS : 0u) | (vr_first << BF_VR_SHIFT) | (quorum ? BF_QUORUM : 0u) |
         (inc_err << BF_INC_SHIFT);
     const uint64_t d0 = peek8(me_d), d1 = peek8(me_d + 8), d2 = peek8(me_d + 16), d3 = peek8(me_d + 24);
     uint4* cd = reinterpret_cast<uint4*>(io.claimed + 32 * (size_t)i);
@@ -447,7 +453,7 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
     else n_st = rd64(pos);
     pos += 8;
   }
-  uint32_t vr_bad = 0;
+  uint32_t vr_first = 0xffffffffu;  // (statement index << 2) | vr_code of the first failing range
   for (uint64_t k0 = 0; ok && k0 < n_st; k0 += IG_CHUNK) {
     // Locate up to IG_CHUNK statements. Speculation: lane j assumes the j statements
     // before it are VoteRanges (76 B in bincode, 65 in the pre-image) and checks its own
@@ -549,7 +555,8 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
         pre_copy32(pre, q + 17, win, d + p + 28);
         pre_be64(pre, q + 49, s0);
         pre_be64(pre, q + 57, s1);
-        vr_bad |= (s1 < s0 || s1 - s0 >= VR_MAX_LEN || s1 >= VR_MAX_LEN) ? 1u : 0u;
+        const uint32_t code = vr_code(s0, s1);
+        if (code && vr_first == 0xffffffffu) vr_first = ((uint32_t)(k0 + lane) << 2) | code;
       }
     }
     // Share payloads, copied by the whole wave
@@ -600,9 +607,10 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
     }
     stake = wave_sum64(stake);
     const uint32_t inc_code = inc_first == 0xffffffffu ? 0u : (inc_first & 15u);
-    vr_bad = wave_or(vr_bad);
+    vr_first = wave_min(vr_first);
+    const uint32_t vr = vr_first == 0xffffffffu ? 0u : (vr_first & 3u);
     f = BF_PARSED | (ep == cv.epoch ? BF_EPOCH_OK : 0u) | (me_a < n_auth ? BF_AUTHOR_OK : 0u) |
-        (me_r == 0 ? BF_GENESIS : 0u) | (vr_bad ? BF_VR_BAD : 0u) | (stake > cv.quorum_thr ? BF_QUORUM : 0u) |
+        (me_r == 0 ? BF_GENESIS : 0u) | (vr << BF_VR_SHIFT) | (stake > cv.quorum_thr ? BF_QUORUM : 0u) |
         (inc_code << BF_INC_SHIFT);
   }
   __syncthreads();
@@ -684,13 +692,16 @@ __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restric
   } else {
     const bool same = digest_same(claimed, digest, i);
     const uint32_t inc = (f >> BF_INC_SHIFT) & 0xffu;
+    const uint32_t vr = (f >> BF_VR_SHIFT) & 3u;
     st = !same                      ? MV_BLOCK_DIGEST_MISMATCH
          : !(f & BF_EPOCH_OK)       ? MV_BLOCK_EPOCH_MISMATCH
          : !(f & BF_AUTHOR_OK)      ? MV_BLOCK_UNKNOWN_AUTHOR
          : (f & BF_GENESIS)         ? MV_BLOCK_GENESIS
          : sig_status[i] != MV_SIG_OK ? MV_BLOCK_SIG_INVALID
          : inc                      ? (uint8_t)inc
-         : (f & BF_VR_BAD)          ? MV_BLOCK_VOTE_RANGE
+         : vr == 1                  ? MV_BLOCK_VOTE_RANGE
+         : vr == 2                  ? MV_BLOCK_VOTE_RANGE_TOO_LONG
+         : vr == 3                  ? MV_BLOCK_VOTE_RANGE_END_TOO_LARGE
          : !(f & BF_QUORUM)         ? MV_BLOCK_THRESHOLD_CLOCK
                                     : MV_BLOCK_OK;
   }

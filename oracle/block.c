@@ -111,7 +111,7 @@ typedef struct {
 } parsed_t;
 
 /* Walks a statement; writes its pre-image bytes into s (may be a NULL sink).
- * vr_bad set to 1 if it is a VoteRange that fails VoteRange::verify. */
+ * *vr_bad set to the ORC_BLOCK_VOTE_RANGE* code of the first VoteRange that fails VoteRange::verify. */
 static void walk_statement(cur_t* c, sink_t* s, int* vr_bad) {
   uint32_t tag = rd_u32(c);
   if (c->err) return;
@@ -162,8 +162,10 @@ static void walk_statement(cur_t* c, sink_t* s, int* vr_bad) {
     put_be64(s, start);
     put_be64(s, end);
     const uint64_t MAX_LEN = 1024 * 1024;
-    if (vr_bad && !*vr_bad) {
-      if (end < start || (end - start) >= MAX_LEN || end >= MAX_LEN) *vr_bad = 1;
+    if (vr_bad && !*vr_bad) { /* VoteRange::verify (types.rs:440-460), checks in order */
+      *vr_bad = end < start ? ORC_BLOCK_VOTE_RANGE
+                : (end - start) >= MAX_LEN ? ORC_BLOCK_VOTE_RANGE_TOO_LONG
+                : end >= MAX_LEN ? ORC_BLOCK_VOTE_RANGE_END_TOO_LARGE : 0;
     }
   } else {
     c->err = 1;
@@ -242,7 +244,7 @@ int orc_block_verify(const uint8_t* bincode, size_t len, const uint8_t* committe
     if (r.authority >= n_auth) return ORC_BLOCK_INCLUDE_UNKNOWN_AUTHORITY;
     if (r.round >= b.reference.round) return ORC_BLOCK_INCLUDE_ROUND;
   }
-  if (vr_bad) return ORC_BLOCK_VOTE_RANGE;
+  if (vr_bad) return vr_bad;
   /* threshold clock (threshold_clock.rs:12-35) */
   c.pos = b.includes_pos;
   c.err = 0;

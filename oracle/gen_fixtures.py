@@ -333,7 +333,18 @@ def gen_block_edge():
     b = copy.deepcopy(base); b.statements = [("range", base.includes[1], 5, 3)]; resign(b)
     add(b.bincode(), 9, "VoteRange end < start")
     b = copy.deepcopy(base); b.statements = [("range", base.includes[1], 0, 1 << 20)]; resign(b)
-    add(b.bincode(), 9, "VoteRange too long")
+    add(b.bincode(), 11, "VoteRange too long")
+    b = copy.deepcopy(base); b.statements = [("range", base.includes[1], 1, 1 << 20)]; resign(b)
+    add(b.bincode(), 12, "VoteRange end too large")
+    b = copy.deepcopy(base)
+    b.statements = [("range", base.includes[1], 0, 7), ("range", base.includes[2], 2, 1 << 20),
+                    ("range", base.includes[3], 5, 3)]
+    resign(b)
+    add(b.bincode(), 12, "VoteRange: the first failing range decides")
+    b = copy.deepcopy(base)
+    b.includes = b.includes + [B.BlockReference(1, 2, bytes(32)), B.BlockReference(9, 1, bytes(32))]
+    resign(b)
+    add(b.bincode(), 8, "includes: the first failing include decides")
     b = copy.deepcopy(base); b.includes = b.includes[:2]; resign(b)
     add(b.bincode(), 10, "threshold clock: 2 of 4 stake")
     b = copy.deepcopy(base)
@@ -366,8 +377,17 @@ def gen_block_edge():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-1m", action="store_true")
+    ap.add_argument("--only", default="", help="regenerate one fixture file, e.g. block_edge.json")
     args = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
+
+    if args.only:
+        gen = {"block_edge.json": gen_block_edge, "hash_kat.json": gen_hash_kat, "sig_kat.json": gen_sig_kat,
+               "zip215_corpus.json": gen_zip215_corpus}[args.only]
+        with open(os.path.join(GOLDEN, args.only), "w") as f:
+            json.dump(gen(), f, indent=1)
+        print("wrote", args.only)
+        return
 
     def dump(name, obj):
         with open(os.path.join(GOLDEN, name), "w") as f:

@@ -69,8 +69,10 @@ enum {
   ORC_BLOCK_SIG_INVALID = 6,
   ORC_BLOCK_INCLUDE_UNKNOWN_AUTHORITY = 7,
   ORC_BLOCK_INCLUDE_ROUND = 8,
-  ORC_BLOCK_VOTE_RANGE = 9,
+  ORC_BLOCK_VOTE_RANGE = 9,             /* end < start */
   ORC_BLOCK_THRESHOLD_CLOCK = 10,
+  ORC_BLOCK_VOTE_RANGE_TOO_LONG = 11,     /* end - start >= 2^20 */
+  ORC_BLOCK_VOTE_RANGE_END_TOO_LARGE = 12, /* end >= 2^20 */
 };
 
 /* Parse bincode bytes and write the signed pre-image (crypto.rs:85-128).

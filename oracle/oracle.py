@@ -18,7 +18,7 @@ _lib = None
 SIG_OK, SIG_INVALID, SIG_MALFORMED_KEY = 0, 1, 2
 (BLOCK_OK, BLOCK_PARSE_ERROR, BLOCK_DIGEST_MISMATCH, BLOCK_EPOCH_MISMATCH, BLOCK_UNKNOWN_AUTHOR,
  BLOCK_GENESIS, BLOCK_SIG_INVALID, BLOCK_INCLUDE_UNKNOWN_AUTHORITY, BLOCK_INCLUDE_ROUND,
- BLOCK_VOTE_RANGE, BLOCK_THRESHOLD_CLOCK) = range(11)
+ BLOCK_VOTE_RANGE, BLOCK_THRESHOLD_CLOCK, BLOCK_VOTE_RANGE_TOO_LONG, BLOCK_VOTE_RANGE_END_TOO_LARGE) = range(13)
 
 
 def build(force: bool = False, archflags: str | None = None) -> str:
