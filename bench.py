@@ -152,6 +152,9 @@ def main():
     ap.add_argument("--sustain-seconds", type=float, default=2.0, help="seconds per sustained repeat")
     ap.add_argument("--no-adversarial", dest="adversarial", action="store_false",
                     help="skip the 1-bad-signature and config-3 (1%% corrupted) rates")
+    ap.add_argument("--no-config4", dest="config4", action="store_false",
+                    help="skip the config-4 (100-validator blocks) rate in the default line")
+    ap.add_argument("--config4-batch", type=int, default=1 << 20, help="config-4 blocks per GPU per step")
     args = ap.parse_args()
     if args.workload != "config2":
         import bench_blocks
@@ -344,6 +347,17 @@ def main():
                                "only in the sub-batch equations that fail (DESIGN.md 2)")
         ok = all_ranks_ok(ok, dist)
 
+    # config 4 (the largest workload): whole-block verification of HBM-resident 100-validator
+    # blocks, measured in the same run (bench_blocks.config4_measure)
+    cfg4 = None
+    if args.config4 and args.path == "batch" and not args.corrupt:
+        import bench_blocks
+
+        cfg4 = bench_blocks.config4_measure(eng, torch, local_rank, world, dist, n=args.config4_batch,
+                                            steps=args.steps, warmup=args.warmup, nstreams=nstreams,
+                                            cpu=args.cpu_sample > 0)
+        ok = ok and cfg4["correct"]
+
     out = None
     if rank == 0:
         e2e = None
@@ -402,6 +416,7 @@ def main():
             "cpu_baseline": cpu,
             "sustained": sustained,
             "adversarial": adversarial,
+            "config4": cfg4,
             "end_to_end": e2e,
             "correct": bool(ok),
             "path": args.path,

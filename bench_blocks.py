@@ -215,6 +215,24 @@ def _concurrent(eng, lib, blocks, pks, stakes, callers: int, seconds: float):
 
 # ------------------------------------------------------------------ config 4 (throughput)
 def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
+    res = config4_measure(eng, torch, local_rank, world, dist, n=args.batch, steps=args.steps, warmup=args.warmup,
+                          nstreams=max(1, args.streams), cpu=args.cpu_sample > 0)
+    if rank == 0:
+        out = {"metric": METRIC}
+        out.update(res)
+        out["n_gpus"] = world
+        out["steps"], out["warmup"] = args.steps, args.warmup
+        out["higher_is_better"], out["scaling"], out["vs_baseline"], out["dtype"] = True, "weak", None, "u32"
+        print(json.dumps(out), flush=True)
+    return 0 if res["correct"] else 1
+
+
+def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstreams=2, cpu=True) -> dict:
+    """Config 4 on this rank's GPU: `n` HBM-resident config-4 blocks per step through
+    mv_dev_verify_blocks (device parse -> pre-image -> 2 x BLAKE2b -> batch ZIP-215 -> verdicts);
+    value = blocks/s over all ranks (weak scaling). Used by `--workload config4` and by the
+    default bench.py line (its "config4" key)."""
+    import mysticeti_amd as M
     import mysticeti_amd.blocks as MB
     from mysticeti_amd.dist import all_ranks_ok, timed_region
 
@@ -227,7 +245,6 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     nb = len(base)
     base_bytes = int(off[-1] + ln[-1])
     span = (base_bytes + 7) & ~7
-    n = args.batch
     reps = (n + nb - 1) // nb
     host = np.zeros(span, dtype=np.uint8)
     host[:base_bytes] = buf[:base_bytes]
@@ -239,11 +256,10 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     d_off = torch.from_numpy(off_all).to(dev)
     d_len = torch.from_numpy(len_all).to(dev)
     buf_bytes = reps * span
-    # Steps alternate over --streams streams (default 2): the engine's two-slot block scratch
-    # ring orders reuse, and one step's HBM-bound ingest and latency-bound batch tail
-    # (reduce, final) overlap the other step's VALU-bound kernels. Stage times for the
-    # roofline are re-taken on ONE stream after the timed region, so they match rocprofv3.
-    nstreams = max(1, args.streams)
+    # Steps alternate over `nstreams` streams: the engine's two-slot block scratch ring orders
+    # reuse, and one step's HBM-bound ingest and latency-bound batch tail (reduce, final)
+    # overlap the other step's VALU-bound kernels. Stage times for the roofline are re-taken
+    # on ONE stream after the timed region, so they match rocprofv3.
     streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
     d_st = [torch.full((n,), 255, dtype=torch.uint8, device=dev) for _ in range(nstreams)]
     d_md = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(nstreams)]
@@ -257,12 +273,12 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
         eng.dev_verify_blocks(local_rank, d_buf, buf_bytes, d_off, d_len, d_st[j], d_md[j], d_bd[j],
                               streams[j].cuda_stream)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     eng.stage_times(reset=True)
     eng.set_stage_timing(True)
-    elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
+    elapsed = timed_region(step, steps, lambda: torch.cuda.synchronize(dev), dist)
     tot, calls = eng.stage_times()
     eng.set_stage_timing(False)
     stage_ms = {k: round(v / calls[k], 4) for k, v in tot.items() if calls[k]}
@@ -270,7 +286,7 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     if nstreams > 1:
         eng.stage_times(reset=True)
         eng.set_stage_timing(True)
-        for _ in range(2):
+        for _ in range(3):
             eng.dev_verify_blocks(local_rank, d_buf, buf_bytes, d_off, d_len, d_st[0], d_md[0], d_bd[0],
                                   streams[0].cuda_stream)
         torch.cuda.synchronize(dev)
@@ -282,64 +298,59 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     bd = d_bd[0][:nb].cpu().numpy()
     claimed = np.stack([np.frombuffer(b[24:56], dtype=np.uint8) for b in base])
     ok &= bool((bd == claimed).all())
-    msg_ok = hashlib.sha256(d_md[0][:nb].cpu().numpy().tobytes()).hexdigest()
-    ok = all_ranks_ok(ok, dist)
-    value = n * world * args.steps / elapsed
+    msg_sha = hashlib.sha256(d_md[0][:nb].cpu().numpy().tobytes()).hexdigest()
+    value = n * world * steps / elapsed
     L = int(np.mean([len(b) for b in base]))  # bincode length
-    import mysticeti_amd as M
-
     pre_len = len(M.block_preimage(base[0]))  # the host codec (block_codec.cpp)
     # shared prefix: (L-1)//128 compressions, then 1 final for B2(P) and the rest of B2(P || sig)
     comp_exec = (pre_len + 64 - 1) // 128 + 2
     comp_alg = -(-pre_len // 128) + -(-(pre_len + 64) // 128)
     hash_ms = stage_ms.get("hash")
-    out = None
-    if rank == 0:
-        cpu = None
-        if args.cpu_sample > 0:
-            lib = _oracle_native()
-            res = {}
-            CPU_THREADS, share_src = _cpu_threads()
-            for threads, seconds in ((1, 4.0), (CPU_THREADS, 8.0)):
-                done, t0 = 0, time.perf_counter()
-                sub = nb if threads > 1 else 400
-                o2, l2 = off[:sub].copy(), ln[:sub].copy()
-                while time.perf_counter() - t0 < seconds:
-                    st = _cpu_blocks(lib, buf, o2, l2, pks, stakes, threads)
-                    ok &= bool((st == 0).all())
-                    done += sub
-                res[threads] = (done / (time.perf_counter() - t0), done)
-            cpu = {"value": round(res[CPU_THREADS][0], 1), "unit": "blocks/s", "cores": CPU_THREADS, "kind": "port",
-                   "sample": f"{res[CPU_THREADS][1]} config-4 blocks on {CPU_THREADS} threads; single core: "
-                             f"{res[1][1]} blocks", "single_core_value": round(res[1][0], 1),
+    cpu_res = None
+    if cpu:
+        lib = _oracle_native()
+        threads, share_src = _cpu_threads()
+        res = {}
+        for t, seconds in ((1, 4.0), (threads, 8.0)):
+            done, t0 = 0, time.perf_counter()
+            sub = nb if t > 1 else 400
+            o2, l2 = off[:sub].copy(), ln[:sub].copy()
+            while time.perf_counter() - t0 < seconds:
+                st = _cpu_blocks(lib, buf, o2, l2, pks, stakes, t)
+                ok &= bool((st == 0).all())
+                done += sub
+            res[t] = (done / (time.perf_counter() - t0), done)
+        cpu_res = {"value": round(res[threads][0], 1), "unit": "blocks/s", "cores": threads, "kind": "port",
+                   "sample": f"{res[threads][1]} config-4 blocks on {threads} threads (~8 s); single core: "
+                             f"{res[1][1]} blocks (~4 s)", "single_core_value": round(res[1][0], 1),
                    "host_cpu": _host_cpu(), "nproc": os.cpu_count(), "cores_source": share_src,
                    "impl": "oracle/block.c StatementBlock::verify (parse, 2 x BLAKE2b, ZIP-215 verify), gcc -O3 "
-                           "-march=native"}
-        roof = None
-        if hash_ms:
-            ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
-            roof = {"bound": "valu", "kernel": "k_block_hash", "kernel_ms": hash_ms,
-                    "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
-                    "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": None,
-                    "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
-                                      f"algorithmic) x {W_BLAKE2B_OPS} ops"}
-        out = {"metric": METRIC, "value": round(value, 1), "unit": "blocks/s (= verified block signatures/s)",
-               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "u32",
-               "data": f"synthetic config-4 blocks ({nb} distinct, signed on the GPU, replicated in HBM)",
-               "config": {"workload": "config4: 100-validator blocks, 67 includes, 512-B tx, 66 VoteRanges, "
-                                      "HBM-resident bincode, device parse + verify", "blocks_per_gpu": n,
-                          "bincode_bytes_per_block": L, "preimage_bytes": pre_len,
-                          "parallelism": f"shard-per-gpu x{world}, no collective"},
-               "roofline": roof, "pipeline": {"stage_ms": stage_ms, "streams": nstreams,
-                                              "stage_ms_as_run": stage_ms_run if nstreams > 1 else None,
-                                              "note": "stage_ms: 2 post-run steps on one stream (roofline); "
-                                                      "stage_ms_as_run: HIP events with overlapping streams",
-                                              "hbm_bincode_GBps": round(n * L / (elapsed / args.steps) / 1e9, 1)},
-               "cpu_baseline": cpu, "correct": bool(ok), "sha256_msg_digests_first_corpus": msg_ok}
-        if cpu:
-            out["speedup_vs_cpu"] = {"all_cores": round(value / world / cpu["value"], 1),
-                                     "single_core": round(value / world / cpu["single_core_value"], 1)}
-        print(json.dumps(out), flush=True)
-    return 0 if ok else 1
+                           "-march=native, persistent thread pool"}
+    roof = None
+    if hash_ms:
+        ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
+        roof = {"bound": "valu", "kernel": "k_b2_quad", "kernel_ms": hash_ms,
+                "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
+                "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": None,
+                "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
+                                  f"algorithmic) x {W_BLAKE2B_OPS} ops"}
+    ok = all_ranks_ok(ok, dist)
+    out = {"value": round(value, 1), "unit": "blocks/s (= verified block signatures/s)",
+           "ms_per_step": round(elapsed / steps * 1e3, 4),
+           "data": f"synthetic config-4 blocks ({nb} distinct, signed on the GPU, replicated in HBM)",
+           "config": {"workload": "config4: 100-validator blocks, 67 includes, 512-B tx, 66 VoteRanges, "
+                                  "HBM-resident bincode, device parse + verify", "blocks_per_gpu": n,
+                      "bincode_bytes_per_block": L, "preimage_bytes": pre_len,
+                      "parallelism": f"shard-per-gpu x{world}, no collective"},
+           "roofline": roof,
+           "pipeline": {"stage_ms": stage_ms, "streams": nstreams,
+                        "stage_ms_as_run": stage_ms_run if nstreams > 1 else None,
+                        "note": "stage_ms: 3 post-run steps on one stream (roofline); "
+                                "stage_ms_as_run: HIP events with overlapping streams",
+                        "hbm_bincode_GBps": round(n * L / (elapsed / steps) / 1e9, 1)},
+           "cpu_baseline": cpu_res, "correct": bool(ok), "sha256_msg_digests_first_corpus": msg_sha}
+    if cpu_res:
+        out["speedup_vs_cpu"] = {"all_cores": round(value / world / cpu_res["value"], 1),
+                                 "single_core": round(value / world / cpu_res["single_core_value"], 1)}
+    del d_buf, d_st, d_md, d_bd
+    return out
