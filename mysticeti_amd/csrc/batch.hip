@@ -40,6 +40,7 @@
 #include "kernels.h"
 #include "scalar25519.h"
 #include "tables.h"
+#include "comb.h"
 
 namespace mv {
 
@@ -162,6 +163,7 @@ struct CommitteeA {
   const uint4* tab;  // nullptr: decode A per signature
   const uint8_t* ok;
   uint32_t stride;   // uint4 per key table
+  uint32_t aggregate;  // 1: A's term is summed per key (k_bv_keyacc / k_bv_keypts), no A points
 };
 
 // one decode at a time at 3 waves/SIMD beat two decodes in lock-step at 2 (seq3 vs
@@ -241,15 +243,17 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
       decompress1(P, okR, rw);
       precomp_from_affine(pc, P);
       if (live) pt_store(pts, gid, pc);
-      const uint4* e = ca.tab + (size_t)kid * ca.stride + 8;  // row 0, entry 1 (8 uint4 per entry)
-      uint4 q[7];
-#pragma unroll
-      for (int k = 0; k < 7; k++) q[k] = e[k];
-      quads_to_precomp(pc, q);
-      precomp_cneg(pc, true);  // -(-A) = A
-      fe_canon(pc.xy2d, pc.xy2d);
       okA = ca.ok[kid] != 0;
-      if (live) pt_store(pts, (size_t)n + gid, pc);
+      if (!ca.aggregate) {
+        const uint4* e = ca.tab + (size_t)kid * ca.stride + 8;  // row 0, entry 1 (8 uint4 per entry)
+        uint4 q[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) q[k] = e[k];
+        quads_to_precomp(pc, q);
+        precomp_cneg(pc, true);  // -(-A) = A
+        fe_canon(pc.xy2d, pc.xy2d);
+        if (live) pt_store(pts, (size_t)n + gid, pc);
+      }
     } else {
 #ifdef MV_PREP_SEQ  // experiment: one decode at a time (fewer registers, more waves)
     p3 P;
@@ -352,7 +356,8 @@ MV_DEV void load_scalars(uint32_t z[4], uint32_t zk[8], const uint4* scal, uint3
   zk[4] = q2.x; zk[5] = q2.y; zk[6] = q2.z; zk[7] = q2.w;
 }
 // chunk c = 1024 signatures: entries per (group-local) partition -> pcount[c][p]
-__global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restrict__ scal, uint32_t n,
+// skipA: the A scalars are summed per committee key instead (no A bucket entries)
+__global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restrict__ scal, uint32_t n, uint32_t skipA,
                                                            uint32_t* __restrict__ pcount) {
   __shared__ uint32_t hist[BV_NPG];
   for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) hist[i] = 0;
@@ -361,6 +366,10 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restri
   if (gid < n) {
     uint32_t z[4], zk[8];
     load_scalars(z, zk, scal, gid);
+    if (skipA) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) zk[i] = 0;
+    }
     bv_for_digits(z, zk, [&](int w, int d, int) { atomicAdd(&hist[bv_key(w, d) >> BV_FINE_BITS], 1u); });
   }
   __syncthreads();
@@ -412,7 +421,7 @@ __global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ p
 __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __restrict__ scal, uint32_t n,
                                                              const uint32_t* __restrict__ poff,
                                                              const uint32_t* __restrict__ pstart, BvGroups G,
-                                                             unsigned long long* __restrict__ tmp) {
+                                                             uint32_t skipA, unsigned long long* __restrict__ tmp) {
   __shared__ uint32_t rank[BV_NPG];
   for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) rank[i] = 0;
   __syncthreads();
@@ -421,6 +430,10 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __rest
     const uint32_t g = blockIdx.x / G.cpg;
     uint32_t z[4], zk[8];
     load_scalars(z, zk, scal, gid);
+    if (skipA) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) zk[i] = 0;
+    }
     const uint32_t* po = poff + (size_t)blockIdx.x * BV_NPG;
     const uint32_t* ps = pstart + (size_t)g * BV_NPG;
     bv_for_digits(z, zk, [&](int w, int d, int isA) {
@@ -475,12 +488,12 @@ __global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned 
 // and each point is loaded one add ahead.
 __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ ents, uint32_t ngroups, uint32_t seg,
-                                                   uint4* __restrict__ segV, uint4* __restrict__ segT) {
+                                                   uint32_t nw, uint4* __restrict__ segV, uint4* __restrict__ segT) {
   const uint32_t nsw = BV_NB / seg;  // segments per (group, window) row
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lin >= ngroups * BV_NW * nsw) return;
+  if (lin >= ngroups * nw * nsw) return;  // windows nw.. carry no entries (per-key A term)
   const uint32_t span = ngroups * nsw;
-  const uint32_t w = BV_NW - 1 - lin / span;
+  const uint32_t w = nw - 1 - lin / span;
   const uint32_t g = (lin % span) / nsw, j = lin % nsw;
   const uint32_t sidx = (g * BV_NW + w) * nsw + j;  // segment index, row-major
   const uint32_t key0 = g * BV_NKG + w * BV_NB + j * seg;
@@ -532,14 +545,18 @@ __global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts
 // scale is a power of two (log2 = shift): the multiplication is `shift` doublings.
 // First level with one bucket per segment (inV == nullptr): the elements are the buckets,
 // m = |d| - 1, so V_m = T_m and scale = 1: V' = sum_t (t + 1) T_t, the sum of the running sums.
+// Output rows are compact, r = g * nw + w; the first level (from_keys) reads the bucket
+// kernel's key-space layout, row (g, w) at (g * BV_NW + w) * cnt_in.
 __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV, const uint4* __restrict__ inT,
-                                                  uint32_t cnt_in, int fan, int shift, uint32_t rows,
-                                                  uint4* __restrict__ outV, uint4* __restrict__ outT) {
+                                                  uint32_t cnt_in, int fan, int shift, uint32_t rows, uint32_t nw,
+                                                  uint32_t from_keys, uint4* __restrict__ outV,
+                                                  uint4* __restrict__ outT) {
   const uint32_t cnt_out = (cnt_in + fan - 1) / fan;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= cnt_out * rows) return;
   const uint32_t r = gid / cnt_out, q = gid % cnt_out;
-  const size_t base = (size_t)r * cnt_in + (size_t)q * fan;
+  const uint32_t rin = from_keys ? (r / nw) * BV_NW + r % nw : r;
+  const size_t base = (size_t)rin * cnt_in + (size_t)q * fan;
   const int m = (int)min((uint32_t)fan, cnt_in - q * fan);
   p3 U, Sx, X;
   p3_identity(U);
@@ -569,11 +586,108 @@ __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV,
   p3_store(outT, gid, U);
 }
 
+// ---------------------------------------------------------------- per-key A term
+// Committee keys (the block path): every signature of key b has A = A_b, so
+//     sum_i [z_i k_i] A_i = sum_b [c_b] A_b,   c_b = sum_{i: key i = b} z_i k_i mod l,
+// one fixed-base multiplication per (group, key) on the key's comb table (32 mixed
+// additions) instead of 16 bucket entries per signature.
+constexpr int BV_MAXKEYS = 512;  // committee size bound (types.rs:118-121)
+
+// chunk c = 1024 signatures: column sums of z k per key -> kpart[c][key][8] (u64 words,
+// each < 2^42). Excluded signatures have z k = 0 (k_bv_prep).
+__global__ void __launch_bounds__(PART_CHUNK) k_bv_keyacc(const uint4* __restrict__ scal,
+                                                          const uint32_t* __restrict__ key_idx, uint32_t n,
+                                                          uint32_t nkeys, unsigned long long* __restrict__ kpart) {
+  __shared__ unsigned long long ks[BV_MAXKEYS * 8];
+  for (uint32_t i = threadIdx.x; i < nkeys * 8; i += PART_CHUNK) ks[i] = 0;
+  __syncthreads();
+  const uint32_t gid = blockIdx.x * PART_CHUNK + threadIdx.x;
+  if (gid < n) {
+    const uint4* sc = scal + (size_t)gid * SC_QUADS;
+    const uint4 q1 = sc[1], q2 = sc[2];
+    const uint32_t w[8] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    const uint32_t key = key_idx[gid];
+    if (key < nkeys && (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7])) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) atomicAdd(&ks[key * 8 + k], (unsigned long long)w[k]);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nkeys * 8; i += PART_CHUNK) kpart[(size_t)blockIdx.x * nkeys * 8 + i] = ks[i];
+}
+
+// Block g = group: thread t takes keys t, t + 256, ...: c = sum over the group's chunks,
+// reduced mod l, [c](-A_b) from the key's comb table of -A, summed; a tree over the block
+// -> asum[g] = +sum_b [c_b] A_b (negated at the end).
+__global__ void __launch_bounds__(256) k_bv_keypts(const unsigned long long* __restrict__ kpart, uint32_t nchunk,
+                                                   uint32_t cpg, uint32_t nkeys, const uint4* __restrict__ combA,
+                                                   uint4* __restrict__ asum) {
+  __shared__ uint4 red[P3_QUADS][256];
+  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  const uint32_t c0 = g * cpg, c1 = min(nchunk, c0 + cpg);
+  p3 acc;
+  p3_identity(acc);
+  for (uint32_t b = t; b < nkeys; b += blockDim.x) {
+    unsigned long long col[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t c = c0; c < c1; c++) {
+      const unsigned long long* p = kpart + ((size_t)c * nkeys + b) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; k++) col[k] += p[k];
+    }
+    uint32_t x[16], r[8], sd[8];
+    unsigned long long carry = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const unsigned long long v = col[k] + carry;  // col < 2^52: no overflow
+      x[k] = (uint32_t)v;
+      carry = v >> 32;
+    }
+    x[8] = (uint32_t)carry;
+    x[9] = (uint32_t)(carry >> 32);
+#pragma unroll
+    for (int k = 10; k < 16; k++) x[k] = 0;
+    sc_reduce512(r, x);
+    sc_recode256(sd, r);
+    p3 P;
+    ct_sum(P, combA + (size_t)b * CT_TABLE, sd, 0, CT_ROWS);
+    p3_acc(acc, P);
+  }
+  uint4 q[9];
+  p3_to_quads(q, acc);
+#pragma unroll
+  for (int k = 0; k < 9; k++) red[k][t] = q[k];
+  __syncthreads();
+  for (uint32_t h = blockDim.x / 2; h > 0; h >>= 1) {
+    if (t < h) {
+      p3 A, B;
+#pragma unroll
+      for (int k = 0; k < 9; k++) q[k] = red[k][t];
+      quads_to_p3(A, q);
+#pragma unroll
+      for (int k = 0; k < 9; k++) q[k] = red[k][t + h];
+      quads_to_p3(B, q);
+      p3_acc(A, B);
+      p3_to_quads(q, A);
+#pragma unroll
+      for (int k = 0; k < 9; k++) red[k][t] = q[k];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) q[k] = red[k][0];
+    quads_to_p3(acc, q);
+    p3_neg(acc, acc);  // the tables hold -A
+    p3_store(asum, g, acc);
+  }
+}
+
 // ---------------------------------------------------------------- final check
 // One 128-thread block. Lane g of wave 0: Horner over group g's window sums (V of the last
 // reduction level, one per window). Lane g of wave 1: -[sum z s mod l]B of group g on the
 // LDS B table. flags[1 + g] = group g's equation held; flags[0] = all of them held.
-__global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV,
+__global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV, uint32_t nw,
+                                                  const uint4* __restrict__ asum,
                                                   const unsigned long long* __restrict__ bsum_part, uint32_t nparts,
                                                   uint32_t parts_per_group, uint32_t ngroups,
                                                   const uint4* __restrict__ btab_g, uint32_t* __restrict__ flags) {
@@ -627,11 +741,15 @@ __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV
     }
   } else if (lane < ngroups) {
     p3 S;
-    const size_t row0 = (size_t)lane * BV_NW;
-    p3_load(acc, winV, row0 + BV_NW - 1);
-    for (int w = BV_NW - 2; w >= 0; w--) {
+    const size_t row0 = (size_t)lane * nw;
+    p3_load(acc, winV, row0 + nw - 1);
+    for (int w = (int)nw - 2; w >= 0; w--) {
       p3_dbl_n(acc, BV_C);
       p3_load(S, winV, row0 + w);
+      p3_acc(acc, S);
+    }
+    if (asum) {  // the per-key A term of the group (k_bv_keypts)
+      p3_load(S, asum, lane);
       p3_acc(acc, S);
     }
   }
@@ -665,7 +783,8 @@ namespace mvk {
 namespace {
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BatchLayout {
-  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, flag, total;
+  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, kpart, asum,
+      flag, total;
   BatchLayout(uint32_t n, uint32_t groups) {
     using namespace mv;
     const size_t nblk = (n + 255) / 256;
@@ -686,6 +805,8 @@ struct BatchLayout {
     const size_t lv = (size_t)groups * (BV_NKG / BV_FAN) * P3_QUADS * 16;
     rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
     bsum = take(nblk * BSUM_WORDS * 8);
+    kpart = take(nchunk * BV_MAXKEYS * 8 * 8);
+    asum = take((size_t)BV_MAXG * P3_QUADS * 16);
     flag = take((1 + BV_MAXG) * 4);
     total = o;
   }
@@ -698,6 +819,15 @@ mv::BvGroups batch_groups(uint32_t n, uint32_t want) {
   const uint32_t cpg = (nchunk + g - 1) / g;
   return mv::BvGroups{(nchunk + cpg - 1) / cpg, cpg};
 }
+// MV_NO_KEY_AGG=1 (experiments): committee keys keep one A bucket entry per signature
+bool agg_disabled() {
+  static const bool v = [] {
+    const char* e = getenv("MV_NO_KEY_AGG");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // buckets per bucket-kernel lane (a power of two): MV_BV_SEG=<k> for experiments
 uint32_t bucket_segment(uint32_t groups) {
   static const int env = [] {
@@ -719,7 +849,8 @@ uint32_t batch_group_size(uint32_t n, uint32_t groups) {
 hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
-                               uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok) {
+                               uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok,
+                               uint32_t n_keys) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
@@ -741,6 +872,8 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   uint4* rv[2] = {(uint4*)(base + L.rV0), (uint4*)(base + L.rV1)};
   uint4* rt[2] = {(uint4*)(base + L.rT0), (uint4*)(base + L.rT1)};
   unsigned long long* bsum = (unsigned long long*)(base + L.bsum);
+  unsigned long long* kpart = (unsigned long long*)(base + L.kpart);
+  uint4* asum = (uint4*)(base + L.asum);
   uint32_t* flag = (uint32_t*)(base + L.flag);
   if (flag_out) *flag_out = flag;
   const uint32_t nblk = (n + 255) / 256;
@@ -750,27 +883,37 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   const uint32_t nchunk = (n + PART_CHUNK - 1) / PART_CHUNK;
   const uint32_t nparts = G.count * BV_NPG;
   mark(0);
-  CommitteeA ca{key_idx && key_ok ? static_cast<const uint4*>(comb_a) : nullptr, key_ok,
-                (uint32_t)(comb_table_bytes(1) / sizeof(uint4))};
+  // committee keys with their comb tables: A from the tables, and its term summed per key
+  const bool com = key_idx && key_ok && comb_a;
+  const bool agg = com && n_keys > 0 && n_keys <= (uint32_t)BV_MAXKEYS && !agg_disabled();
+  CommitteeA ca{com ? static_cast<const uint4*>(comb_a) : nullptr, key_ok,
+                (uint32_t)(comb_table_bytes(1) / sizeof(uint4)), agg ? 1u : 0u};
+  const uint32_t nw = agg ? BV_NWR : BV_NW;  // windows with bucket entries
   hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,
                      status);
   mark(1);
-  hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, pcount);
+  hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, agg ? 1u : 0u, pcount);
   hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(256), 0, s, pcount, nchunk, G, poff, ptot);
   hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, nparts, pstart);
-  hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G, tmp);
+  hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
+                     agg ? 1u : 0u, tmp);
   hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, G.count, ents, offs);
   mark(2);
   // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
   // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
   // through memory and the reduction stays the size of one group's
   const uint32_t seg = bucket_segment(G.count);
-  hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * BV_NKG / seg / 256), dim3(256), 0, s, pts, offs, ents, G.count, seg,
-                     segV, segT);
+  hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
+                     G.count, seg, nw, segV, segT);
+  if (agg) {
+    hipLaunchKernelGGL(k_bv_keyacc, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, key_idx, n, n_keys, kpart);
+    hipLaunchKernelGGL(k_bv_keypts, dim3(G.count), dim3(256), 0, s, kpart, nchunk, G.cpg, n_keys,
+                       static_cast<const uint4*>(comb_a), asum);
+  }
   mark(3);
   const uint4* inV = seg > 1 ? segV : nullptr;  // one bucket per segment: V = T
   const uint4* inT = segT;
-  const uint32_t rows = G.count * BV_NW;
+  const uint32_t rows = G.count * nw;
   uint32_t cnt = BV_NB / seg;
   int shift = 31 - __builtin_clz(seg);  // log2(seg)
   int pp = 0;
@@ -778,8 +921,8 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
     const uint32_t out = (cnt + fan - 1) / fan;
     const uint32_t lanes = out * rows;
-    hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rows,
-                       rv[pp], rt[pp]);
+    hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rows, nw,
+                       inT == segT ? 1u : 0u, rv[pp], rt[pp]);
     inV = rv[pp];
     inT = rt[pp];
     pp ^= 1;
@@ -787,8 +930,8 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     cnt = out;
   }
   mark(4);
-  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, bsum, nblk, G.cpg * (PART_CHUNK / 256), G.count,
-                     (const uint4*)btab, flag);
+  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, nw, agg ? (const uint4*)asum : nullptr, bsum, nblk,
+                     G.cpg * (PART_CHUNK / 256), G.count, (const uint4*)btab, flag);
   mark(5);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

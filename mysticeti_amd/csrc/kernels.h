@@ -41,10 +41,12 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
-                               const uint8_t* key_ok = nullptr);
+                               const uint8_t* key_ok = nullptr, uint32_t n_keys = 0);
 // comb_a / key_ok (optional, with key_idx): the committee's comb tables (comb.hip, tables of
 // -A) and per-key decode flags; k_bv_prep then reads each signature's A from entry [0][1]
 // of its key's table instead of decoding A (the key was decoded once, at mv_set_committee).
+// n_keys (committee size, <= 512) > 0 also sums A's term per key: sum_b [c_b] A_b on the
+// comb tables replaces the 16 A bucket entries per signature.
 // comb.hip: per-key comb tables C[i][j] = [j 256^i](+-P) and the committee-key verify.
 // enc == nullptr builds the table of B; negate = 1 stores -P (committee keys).
 size_t comb_table_bytes(uint32_t nbases);
