@@ -191,7 +191,10 @@ template <bool DUAL>
 __global__ void __launch_bounds__(64) k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                 const uint64_t* __restrict__ len, uint32_t n,
                                                 uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
-  __shared__ uint64_t mbuf[2][16][16];  // [buffer][string][word]
+  // [buffer][string][word], rows padded to 17 words: the 16 strings' rows start 34 banks
+  // apart, so the lanes of one message-word read (one word per string) hit distinct banks
+  // (unpadded, strings qd and qd + 2 shared a bank: 8-way conflicts, ~1/3 of the kernel)
+  __shared__ uint64_t mbuf[2][16][17];
   const uint32_t lane = threadIdx.x, q = lane & 3, qd = lane >> 2;
   const uint32_t i = blockIdx.x * 16 + qd;
   const bool live = i < n;

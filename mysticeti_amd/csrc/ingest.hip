@@ -337,12 +337,15 @@ MV_DEV void pre_be64(uint8_t* pre, uint32_t p, uint64_t x) {
 #pragma unroll
   for (int b = 0; b < 8; b++) pre[p + b] = (uint8_t)(x >> (56 - 8 * b));
 }
-// 32 bytes from the window (any alignment) into the pre-image: 9 word reads issued together
-MV_DEV void pre_copy32(uint8_t* pre, uint32_t p, const uint32_t* win, uint32_t q) {
-  const uint32_t i = q >> 2, sh = (q & 3) * 8;
-  uint32_t w[9];
+// 32 bytes of the window at byte q (any alignment): the 9 covering words, read together
+MV_DEV void win_read32(uint32_t w[9], const uint32_t* win, uint32_t q) {
+  const uint32_t i = q >> 2;
 #pragma unroll
   for (int k = 0; k < 9; k++) w[k] = win[i + k];
+}
+// ... written to the pre-image at p (q = the byte address they were read from)
+MV_DEV void pre_write32(uint8_t* pre, uint32_t p, const uint32_t w[9], uint32_t q) {
+  const uint32_t sh = (q & 3) * 8;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const uint32_t x = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh);
@@ -372,11 +375,17 @@ MV_DEV uint64_t wave_sum64(uint64_t x) {
 __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                      const uint64_t* __restrict__ len, uint32_t n, CommitteeView cv,
                                                      IngestOut io) {
-  __shared__ uint32_t win[IG_WIN / 4 + 8];      // the block's bincode (from its aligned start)
-  __shared__ uint64_t pre64[IG_WIN / 8];        // its pre-image || signature
+  // The block's bincode (from its aligned start), transcoded IN PLACE into its pre-image ||
+  // signature: every element's pre-image starts at or before its bincode and the elements
+  // are produced in order, so an element's pre-image never reaches bincode not yet read
+  // (each chunk's lanes read their elements into registers before any of them writes). One
+  // 10-KB buffer instead of two doubles the waves per CU (LDS-limited, 7 -> 14).
+  __shared__ uint64_t win64[IG_WIN / 8 + 4];
   __shared__ uint32_t st_pos[IG_CHUNK], st_pre[IG_CHUNK];
   __shared__ uint32_t seen[16];                 // authorities of round r-1 among the includes
-  uint8_t* pre = reinterpret_cast<uint8_t*>(pre64);
+  uint32_t* win = reinterpret_cast<uint32_t*>(win64);
+  uint64_t* pre64 = win64;
+  uint8_t* pre = reinterpret_cast<uint8_t*>(win64);
   const uint32_t lane = threadIdx.x;
   const uint32_t i = blockIdx.x;
   const uint64_t o = off[i], L = len[i];
@@ -395,7 +404,7 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
     constexpr int IG_LOADS = IG_WIN / 8 / 64;
     static_assert(IG_WIN % 512 == 0, "the window is whole 64-lane rounds of 8-byte loads");
     const uint64_t* src = reinterpret_cast<const uint64_t*>(buf + (o - d));
-    uint64_t* w64 = reinterpret_cast<uint64_t*>(win);
+    uint64_t* w64 = win64;
     const uint32_t nw = (uint32_t)((d + L + 15) >> 3);
     uint64_t t[IG_LOADS];
 #pragma unroll
@@ -421,6 +430,9 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
   }
   const uint64_t n_inc = ok ? rd64(56) : 0;
   if (ok && n_inc > (uint64_t)((Lb - 64) / 56)) ok = false;
+  // the claimed digest (bincode bytes 24..56), one word per lane 0..7, before the includes'
+  // pre-images overwrite it
+  const uint32_t claimed_w = (ok && lane < 8) ? rd32(24 + 4 * lane) : 0u;
   uint32_t bad = 0, inc_first = 0xffffffffu;
   if (ok) {
     if (lane < 8) {
@@ -433,12 +445,15 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
       const uint32_t p = 64 + 56 * k;
       const uint64_t a = rd64(p), r = rd64(p + 8);
       bad |= rd64(p + 16) != 32;
+      uint64_t dg[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) dg[m] = rd64(p + 24 + 8 * m);  // digest bytes as they lie
       // pre-image offset 16 + 48 k is 8-byte aligned: six 64-bit LDS stores, not 48 byte stores
       uint64_t* pq = pre64 + 2 + 6 * k;
       pq[0] = __builtin_bswap64(a);  // big-endian u64 (pre_be64)
       pq[1] = __builtin_bswap64(r);
 #pragma unroll
-      for (int m = 0; m < 4; m++) pq[2 + m] = rd64(p + 24 + 8 * m);  // digest bytes as they lie
+      for (int m = 0; m < 4; m++) pq[2 + m] = dg[m];
       const uint32_t code = a >= n_auth ? MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY : (r >= me_r ? MV_BLOCK_INCLUDE_ROUND : 0u);
       if (code && inc_first == 0xffffffffu) inc_first = (k << 4) | code;
       if (me_r > 0 && r == me_r - 1 && a < n_auth) atomicOr(&seen[(uint32_t)a >> 5], 1u << (a & 31));
@@ -521,52 +536,78 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
     __syncthreads();
     const uint32_t cnt = c;
     ok = lok;
-    bool is_share = false;
+    // (a) every lane reads its statement into registers
+    uint32_t kind = 0;  // 1 Share, 2 Accept, 3 Reject(None), 4 Reject(Some), 5 VoteRange
+    uint32_t q = 0, ps = 0;
+    uint64_t a = 0, r = 0, x = 0, y = 0, a2 = 0, r2 = 0, z2 = 0;
+    uint32_t dg[9], dg2[9];
     if (lane < cnt) {
-      const uint32_t p = st_pos[lane], q = st_pre[lane];
+      const uint32_t p = st_pos[lane];
+      q = st_pre[lane];
+      ps = p;
       const uint32_t tag = rd32(p);
       if (tag == 0) {
-        pre[q] = 0;
-        is_share = true;
-      } else if (tag == 1) {
-        const uint64_t a = rd64(p + 4), r = rd64(p + 12), off1 = rd64(p + 60);
+        kind = 1;
+      } else {
+        a = rd64(p + 4);
+        r = rd64(p + 12);
         bad |= rd64(p + 20) != 32;
-        const uint32_t vote = rd32(p + 68);
-        const uint32_t some = vote == 1 ? rd8(p + 72) : 0u;
-        pre[q] = (uint8_t)(vote == 0 ? 1 : (some == 0 ? 2 : 3));
-        pre_be64(pre, q + 1, a);
-        pre_be64(pre, q + 9, r);
-        pre_copy32(pre, q + 17, win, d + p + 28);
-        pre_be64(pre, q + 49, off1);
-        if (vote == 1 && some == 1) {
-          const uint64_t a2 = rd64(p + 73), r2 = rd64(p + 81), off2 = rd64(p + 129);
-          bad |= rd64(p + 89) != 32;
-          pre_be64(pre, q + 57, a2);
-          pre_be64(pre, q + 65, r2);
-          pre_copy32(pre, q + 73, win, d + p + 97);
-          pre_be64(pre, q + 105, off2);
+        win_read32(dg, win, d + p + 28);
+        x = rd64(p + 60);
+        if (tag == 1) {
+          const uint32_t vote = rd32(p + 68);
+          const uint32_t some = vote == 1 ? rd8(p + 72) : 0u;
+          kind = vote == 0 ? 2 : (some == 0 ? 3 : 4);
+          if (kind == 4) {
+            a2 = rd64(p + 73);
+            r2 = rd64(p + 81);
+            bad |= rd64(p + 89) != 32;
+            win_read32(dg2, win, d + p + 97);
+            z2 = rd64(p + 129);
+          }
+        } else {  // tag 2
+          kind = 5;
+          y = rd64(p + 68);
+          const uint32_t code = vr_code(x, y);
+          if (code && vr_first == 0xffffffffu) vr_first = ((uint32_t)(k0 + lane) << 2) | code;
         }
-      } else {  // tag 2
-        const uint64_t a = rd64(p + 4), r = rd64(p + 12), s0 = rd64(p + 60), s1 = rd64(p + 68);
-        bad |= rd64(p + 20) != 32;
-        pre[q] = 4;
-        pre_be64(pre, q + 1, a);
-        pre_be64(pre, q + 9, r);
-        pre_copy32(pre, q + 17, win, d + p + 28);
-        pre_be64(pre, q + 49, s0);
-        pre_be64(pre, q + 57, s1);
-        const uint32_t code = vr_code(s0, s1);
-        if (code && vr_first == 0xffffffffu) vr_first = ((uint32_t)(k0 + lane) << 2) | code;
       }
     }
-    // Share payloads, copied by the whole wave
-    uint64_t shares = __ballot(is_share);
+    // (b) Share payloads, moved down by the whole wave 64 bytes at a time (each round reads
+    // before it writes, and the destination lies below the source)
+    uint64_t shares = __ballot(kind == 1);
     while (shares) {
       const uint32_t j = (uint32_t)__builtin_ctzll(shares);
       shares &= shares - 1;
-      const uint32_t p = st_pos[j], q = st_pre[j];
+      const uint32_t p = st_pos[j], qj = st_pre[j];
       const uint32_t l = (uint32_t)rd64(p + 4);
-      for (uint32_t t = lane; t < l; t += 64) pre[q + 1 + t] = (uint8_t)rd8(p + 12 + t);
+      for (uint32_t t = lane; t < ((l + 63) & ~63u); t += 64) {
+        const uint32_t v = t < l ? rd8(p + 12 + t) : 0u;
+        if (t < l) pre[qj + 1 + t] = (uint8_t)v;
+      }
+    }
+    // (c) every lane writes its statement's pre-image
+    if (kind == 1) {
+      pre[q] = 0;
+    } else if (kind >= 2 && kind <= 4) {
+      pre[q] = (uint8_t)(kind - 1);
+      pre_be64(pre, q + 1, a);
+      pre_be64(pre, q + 9, r);
+      pre_write32(pre, q + 17, dg, d + ps + 28);
+      pre_be64(pre, q + 49, x);
+      if (kind == 4) {
+        pre_be64(pre, q + 57, a2);
+        pre_be64(pre, q + 65, r2);
+        pre_write32(pre, q + 73, dg2, d + ps + 97);
+        pre_be64(pre, q + 105, z2);
+      }
+    } else if (kind == 5) {
+      pre[q] = 4;
+      pre_be64(pre, q + 1, a);
+      pre_be64(pre, q + 9, r);
+      pre_write32(pre, q + 17, dg, d + ps + 28);
+      pre_be64(pre, q + 49, x);
+      pre_be64(pre, q + 57, y);
     }
     pos = p;
     ppos = pp;
@@ -596,7 +637,8 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
       pre[ppos + 16] = (uint8_t)marker;
       pre_be64(pre, ppos + 17, ep);
     }
-    pre[ppos + 25 + lane] = (uint8_t)rd8(spos + lane);  // P || sig
+    const uint32_t sb = rd8(spos + lane);  // P || sig (read by every lane before any writes)
+    pre[ppos + 25 + lane] = (uint8_t)sb;
     // threshold clock: stake of the distinct round r-1 authorities among the includes
     // (lane j sums authorities j, j + 64, ...: independent loads, one latency)
     uint64_t stake = 0;
@@ -621,17 +663,13 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
     const uint32_t nw = (plen + 64 + 7) >> 3;
     for (uint32_t k = lane; k < nw; k += 64) dst[k] = pre64[k];
   }
+  if (ok && lane < 8) reinterpret_cast<uint32_t*>(io.claimed + 32 * (size_t)i)[lane] = claimed_w;
   if (lane == 0) {
     io.pre_off[i] = so;
     io.pre_len[i] = ok ? plen : 0;
-    uint32_t sw[16];
+    uint32_t sw[16];  // the signature, from its pre-image copy (its bincode was overwritten)
 #pragma unroll
-    for (int q = 0; q < 16; q++) sw[q] = ok ? rd32(spos + 4 * q) : 0u;
-    if (ok) {
-      uint4* cd = reinterpret_cast<uint4*>(io.claimed + 32 * (size_t)i);
-      cd[0] = make_uint4(rd32(24), rd32(28), rd32(32), rd32(36));
-      cd[1] = make_uint4(rd32(40), rd32(44), rd32(48), rd32(52));
-    }
+    for (int q = 0; q < 16; q++) sw[q] = ok ? lds_u32(win, plen + 4 * q) : 0u;
     const bool sig_decides = ok && (f & BF_EPOCH_OK) && (f & BF_AUTHOR_OK) && !(f & BF_GENESIS);
     if (!sig_decides) {
 #pragma unroll
