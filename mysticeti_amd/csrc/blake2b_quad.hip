@@ -122,6 +122,11 @@ MV_DEV void compress(uint64_t& h0, uint64_t& h1, const uint64_t* m, uint32_t q, 
 }
 #undef MV_QG
 
+MV_DEV uint32_t wave_min32(uint32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, m));
+  return x;
+}
 MV_DEV uint32_t wave_max(uint32_t x) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, m));
@@ -208,11 +213,43 @@ __global__ void __launch_bounds__(64) k_b2_quad(const uint8_t* __restrict__ buf,
   uint64_t b, lim, t;
   bool fin, mfin;
   uint64_t w[4];
-  pl.at(0, b, lim, t, fin, mfin);
-  load_quarter(w, p, b, lim, q);
+  // Steps [0, nfull): whole 128-byte blocks that every string of the wave has and that are
+  // neither final nor the message's last (the shared prefix of the block path): no plan, no
+  // masking, counters 128 (s + 1). The remaining steps go through the plan.
+  uint32_t nfull = 0;
+  if (DUAL) {
+    const uint64_t c = live ? pl.common : 0;
+    nfull = (uint32_t)wave_min32((uint32_t)(c > 0xffffffffull ? 0xffffffffull : c));
+  } else {
+    const uint64_t c = live ? pl.last : 0;
+    nfull = (uint32_t)wave_min32((uint32_t)(c > 0xffffffffull ? 0xffffffffull : c));
+  }
+  nfull = nfull > nmax ? nmax : nfull;
+  if (nfull > 0) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + 4 * q;
 #pragma unroll
-  for (int j = 0; j < 4; j++) mbuf[0][qd][4 * q + j] = w[j];
-  for (uint32_t s = 0; s < nmax; s++) {
+    for (int j = 0; j < 4; j++) mbuf[0][qd][4 * q + j] = src[j];
+  } else {
+    pl.at(0, b, lim, t, fin, mfin);
+    load_quarter(w, p, b, lim, q);
+#pragma unroll
+    for (int j = 0; j < 4; j++) mbuf[0][qd][4 * q + j] = w[j];
+  }
+  for (uint32_t s = 0; s < nfull; s++) {
+    __syncthreads();
+    if (s + 1 < nfull) {  // the next whole block, in flight during this compression
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + (size_t)(s + 1) * 16 + 4 * q;
+#pragma unroll
+      for (int j = 0; j < 4; j++) w[j] = src[j];
+    } else {
+      pl.at(s + 1, b, lim, t, fin, mfin);
+      load_quarter(w, p, b, lim, q);
+    }
+    compress(h0, h1, mbuf[s & 1][qd], q, iv0, iv1, 128ull * (s + 1), false);
+#pragma unroll
+    for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][qd][4 * q + j] = w[j];
+  }
+  for (uint32_t s = nfull; s < nmax; s++) {
     __syncthreads();
     uint64_t bn, limn, tn;
     bool finn, mfinn;
