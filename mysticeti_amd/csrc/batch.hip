@@ -41,6 +41,7 @@
 #include "scalar25519.h"
 #include "tables.h"
 #include "comb.h"
+#include "quad25519.h"
 
 namespace mv {
 
@@ -690,19 +691,17 @@ __global__ void __launch_bounds__(256) k_bv_keypts(const unsigned long long* __r
 }
 
 // ---------------------------------------------------------------- final check
-// One 128-thread block. Lane g of wave 0: Horner over group g's window sums (V of the last
-// reduction level, one per window). Lane g of wave 1: -[sum z s mod l]B of group g on the
-// LDS B table. flags[1 + g] = group g's equation held; flags[0] = all of them held.
+// One 128-thread block. Quad g of wave 0: Horner over group g's window sums (V of the last
+// reduction level, one per window), four lanes per point. Lane g of wave 1: -[sum z s mod l]B
+// of group g on the comb table of B. flags[1 + g] = group g's equation held; flags[0] = all.
 __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV, uint32_t nw,
                                                   const uint4* __restrict__ asum,
                                                   const unsigned long long* __restrict__ bsum_part, uint32_t nparts,
                                                   uint32_t parts_per_group, uint32_t ngroups,
-                                                  const uint4* __restrict__ btab_g, uint32_t* __restrict__ flags) {
-  __shared__ uint4 btab[BT_TABLE];
+                                                  const uint4* __restrict__ combB, uint32_t* __restrict__ flags) {
   __shared__ unsigned long long sb[BV_MAXG][BSUM_WORDS];
   __shared__ uint4 sbp[BV_MAXG][P3_QUADS];
   __shared__ uint32_t sflag[BV_MAXG];
-  lds_btab_load(btab, btab_g, BT_TABLE);
   for (uint32_t i = threadIdx.x; i < BV_MAXG * BSUM_WORDS; i += blockDim.x) (&sb[0][0])[i] = 0;
   __syncthreads();
   for (uint32_t g = 0; g < ngroups; g++) {
@@ -718,7 +717,6 @@ __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV
     for (int c = 0; c < BSUM_WORDS; c++) atomicAdd(&sb[g][c], acc[c]);
   }
   __syncthreads();
-  p3 acc;
   const uint32_t lane = threadIdx.x & 63;
   if (threadIdx.x >= 64) {
     if (lane < ngroups) {
@@ -738,45 +736,56 @@ __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV
       uint32_t r[8], sd[8];
       sc_reduce512(r, x);
       sc_recode256(sd, r);
+      // [x]B on the comb table of B (mv_create): 32 mixed additions, no doublings (a ladder
+      // would be 248 doublings, as long as the Horner chain beside it)
       p3 P;
-      basemul(P, sd, btab);
+      ct_sum(P, combB, sd, 0, CT_ROWS);
       p3_neg(P, P);
       uint4 q[9];
       p3_to_quads(q, P);
 #pragma unroll
       for (int i = 0; i < 9; i++) sbp[lane][i] = q[i];
     }
-  } else if (lane < ngroups) {
-    p3 S;
-    const size_t row0 = (size_t)lane * nw;
-    p3_load(acc, winV, row0 + nw - 1);
+  }
+  // Horner over group g's window sums on quad g of wave 0 (quad25519.h: a doubling is one
+  // squaring and one multiplication deep), then the per-key A term
+  const uint32_t g = lane >> 2;
+  fe v;
+  if (threadIdx.x < 64 && g < ngroups) {
+    const size_t row0 = (size_t)g * nw;
+    qp_load(v, winV, row0 + nw - 1);
     for (int w = (int)nw - 2; w >= 0; w--) {
-      p3_dbl_n(acc, BV_C);
-      p3_load(S, winV, row0 + w);
-      p3_acc(acc, S);
+      fe wv;
+      qp_load(wv, winV, row0 + w);
+      qp_dbl_n(v, BV_C);
+      qp_add(v, wv);
     }
     if (asum) {  // the per-key A term of the group (k_bv_keypts)
-      p3_load(S, asum, lane);
-      p3_acc(acc, S);
+      fe av;
+      qp_load(av, asum, g);
+      qp_add(v, av);
     }
   }
   __syncthreads();
-  if (threadIdx.x < ngroups) {
-    uint4 q[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) q[i] = sbp[threadIdx.x][i];
-    p3 P;
-    quads_to_p3(P, q);
-    p3_acc(acc, P);
-    p3_dbl_n(acc, 3);  // cofactor
-    sflag[threadIdx.x] = p3_is_identity(acc) ? 1u : 0u;
+  if (threadIdx.x < 64 && g < ngroups) {
+    fe bv;
+    qp_load(bv, &sbp[0][0], g);
+    qp_add(v, bv);
+    qp_dbl_n(v, 3);  // cofactor
+    // identity <=> X == 0 and Y == Z (mod p)
+    fe Y, Z;
+    fe_qget<1>(Y, v);
+    fe_qget<2>(Z, v);
+    const bool x0 = fe_is_zero(v);
+    const bool yz = fe_eq(Y, Z);
+    if ((lane & 3) == 0) sflag[g] = x0 && yz ? 1u : 0u;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t all = 1;
-    for (uint32_t g = 0; g < ngroups; g++) {
-      flags[1 + g] = sflag[g];
-      all &= sflag[g];
+    for (uint32_t gg = 0; gg < ngroups; gg++) {
+      flags[1 + gg] = sflag[gg];
+      all &= sflag[gg];
     }
     flags[0] = all;
   }
@@ -857,7 +866,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok,
-                               uint32_t n_keys) {
+                               uint32_t n_keys, const void* comb_b) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
@@ -938,7 +947,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   }
   mark(4);
   hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, nw, agg ? (const uint4*)asum : nullptr, bsum, nblk,
-                     G.cpg * (PART_CHUNK / 256), G.count, (const uint4*)btab, flag);
+                     G.cpg * (PART_CHUNK / 256), G.count, static_cast<const uint4*>(comb_b), flag);
   mark(5);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -17,6 +17,7 @@
 // and 16-bit rotations are byte permutes (v_perm_b32); 32 is a register swap.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.h"
 
@@ -96,29 +97,69 @@ MV_DEV uint64_t qrot(uint64_t x) {
   c = add64(c, d);           \
   b = ror63(b ^ c);
 
-// One compression of the quad's block m[16] (LDS). (h0, h1) = (h[q], h[4 + q]); (iv0, iv1) =
-// (IV[q], IV[4 + q]); t = byte counter (< 2^64), fin = final block.
-MV_DEV void compress(uint64_t& h0, uint64_t& h1, const uint64_t* m, uint32_t q, uint64_t iv0, uint64_t iv1,
-                     uint64_t t, bool fin) {
-  uint64_t a = h0, b = h1, c = iv0, d = iv1;
-  d ^= q == 0 ? t : 0ull;            // v[12] ^= t (t_hi = 0: v[13] unchanged)
-  d = (q == 2 && fin) ? ~d : d;      // v[14] = ~v[14] on the final block
+// One compression of the quad's block m[16] (LDS) for each of NS strings, interleaved: the
+// strings' G chains are independent, so one string's instructions fill the other's
+// dependency and DPP-hazard gaps, and the message-word addresses are computed once for
+// both. (h0, h1) = (h[q], h[4 + q]); (iv0, iv1) = (IV[q], IV[4 + q]); t = byte counter
+// (< 2^64), fin = final block.
+template <int NS>
+MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* const (&m)[NS], uint32_t q,
+                     uint64_t iv0, uint64_t iv1, const uint64_t (&t)[NS], const bool (&fin)[NS]) {
+  uint64_t va[NS], vb[NS], vc[NS], vd[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    va[k] = h0[k];
+    vb[k] = h1[k];
+    vc[k] = iv0;
+    vd[k] = iv1 ^ (q == 0 ? t[k] : 0ull);        // v[12] ^= t (t_hi = 0: v[13] unchanged)
+    vd[k] = (q == 2 && fin[k]) ? ~vd[k] : vd[k];  // v[14] = ~v[14] on the final block
+  }
   const uint32_t sh = 4 * q;
 #pragma unroll
   for (int r = 0; r < 12; r++) {
-    const uint64_t x0 = m[(SEL.v[r][0] >> sh) & 15u], y0 = m[(SEL.v[r][1] >> sh) & 15u];
-    const uint64_t x1 = m[(SEL.v[r][2] >> sh) & 15u], y1 = m[(SEL.v[r][3] >> sh) & 15u];
-    MV_QG(x0, y0)
-    b = qrot<1>(b);
-    c = qrot<2>(c);
-    d = qrot<3>(d);
-    MV_QG(x1, y1)
-    b = qrot<3>(b);
-    c = qrot<2>(c);
-    d = qrot<1>(d);
+    // keep each round's message reads in their round: hoisting all 48 ahead of the chain
+    // (what the scheduler does unchecked) doubles the VGPRs and halves the waves per SIMD
+    asm volatile("" ::: "memory");
+    const uint32_t i0 = (SEL.v[r][0] >> sh) & 15u, i1 = (SEL.v[r][1] >> sh) & 15u;
+    const uint32_t i2 = (SEL.v[r][2] >> sh) & 15u, i3 = (SEL.v[r][3] >> sh) & 15u;
+    uint64_t x0[NS], y0[NS], x1[NS], y1[NS];
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      x0[k] = m[k][i0];
+      y0[k] = m[k][i1];
+      x1[k] = m[k][i2];
+      y1[k] = m[k][i3];
+    }
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      uint64_t a = va[k], b = vb[k], c = vc[k], d = vd[k];
+      MV_QG(x0[k], y0[k])
+      va[k] = a; vb[k] = b; vc[k] = c; vd[k] = d;
+    }
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      vb[k] = qrot<1>(vb[k]);
+      vc[k] = qrot<2>(vc[k]);
+      vd[k] = qrot<3>(vd[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      uint64_t a = va[k], b = vb[k], c = vc[k], d = vd[k];
+      MV_QG(x1[k], y1[k])
+      va[k] = a; vb[k] = b; vc[k] = c; vd[k] = d;
+    }
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      vb[k] = qrot<3>(vb[k]);
+      vc[k] = qrot<2>(vc[k]);
+      vd[k] = qrot<1>(vd[k]);
+    }
   }
-  h0 ^= a ^ c;
-  h1 ^= b ^ d;
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    h0[k] ^= va[k] ^ vc[k];
+    h1[k] ^= vb[k] ^ vd[k];
+  }
 }
 #undef MV_QG
 
@@ -190,83 +231,116 @@ MV_DEV void load_quarter(uint64_t w[4], const uint8_t* p, uint64_t b, uint64_t l
   }
 }
 
-// 16 strings per 64-lane workgroup. DUAL: out0 = B2(P) (msg), out1 = B2(P || sig) (digest);
-// otherwise out0 = B2(string).
-template <bool DUAL>
-__global__ void __launch_bounds__(64) k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+// 16 * NS strings per 64-lane workgroup: quad qd takes strings 16 k + qd, k < NS. DUAL:
+// out0 = B2(P) (msg), out1 = B2(P || sig) (digest); otherwise out0 = B2(string).
+template <bool DUAL, int NS>
+__global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                 const uint64_t* __restrict__ len, uint32_t n,
                                                 uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
   // [buffer][string][word], rows padded to 17 words: the 16 strings' rows start 34 banks
   // apart, so the lanes of one message-word read (one word per string) hit distinct banks
-  // (unpadded, strings qd and qd + 2 shared a bank: 8-way conflicts, ~1/3 of the kernel)
-  __shared__ uint64_t mbuf[2][16][17];
+  __shared__ uint64_t mbuf[2][16 * NS][17];
   const uint32_t lane = threadIdx.x, q = lane & 3, qd = lane >> 2;
-  const uint32_t i = blockIdx.x * 16 + qd;
-  const bool live = i < n;
-  const uint8_t* p = buf + (live ? off[i] : 0);
-  Plan<DUAL> pl;
-  pl.init(live ? len[i] : 0, live);
-  const uint32_t nmax = wave_max(pl.nsteps);
-  const uint64_t iv0 = IV[q], iv1 = IV[4 + q];
-  uint64_t h0 = iv0 ^ (q == 0 ? 0x01010020ull : 0ull), h1 = iv1;  // depth 1, fanout 1, nn = 32
-
-  uint64_t b, lim, t;
-  bool fin, mfin;
-  uint64_t w[4];
-  // Steps [0, nfull): whole 128-byte blocks that every string of the wave has and that are
-  // neither final nor the message's last (the shared prefix of the block path): no plan, no
-  // masking, counters 128 (s + 1). The remaining steps go through the plan.
-  uint32_t nfull = 0;
-  if (DUAL) {
-    const uint64_t c = live ? pl.common : 0;
-    nfull = (uint32_t)wave_min32((uint32_t)(c > 0xffffffffull ? 0xffffffffull : c));
-  } else {
-    const uint64_t c = live ? pl.last : 0;
-    nfull = (uint32_t)wave_min32((uint32_t)(c > 0xffffffffull ? 0xffffffffull : c));
+  uint32_t idx[NS];
+  bool live[NS];
+  const uint8_t* p[NS];
+  Plan<DUAL> pl[NS];
+  uint32_t nsteps_max = 0, nfull_min = 0xffffffffu;
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    idx[k] = blockIdx.x * 16 * NS + 16 * k + qd;
+    live[k] = idx[k] < n;
+    p[k] = buf + (live[k] ? off[idx[k]] : 0);
+    pl[k].init(live[k] ? len[idx[k]] : 0, live[k]);
+    nsteps_max = max(nsteps_max, pl[k].nsteps);
+    // whole 128-byte blocks that are neither final nor the message's last (the shared prefix)
+    const uint64_t c = live[k] ? (DUAL ? pl[k].common : pl[k].last) : 0;
+    nfull_min = min(nfull_min, (uint32_t)(c > 0xffffffffull ? 0xffffffffull : c));
   }
-  nfull = nfull > nmax ? nmax : nfull;
-  if (nfull > 0) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + 4 * q;
+  const uint32_t nmax = wave_max(nsteps_max);
+  const uint32_t nfull = min(wave_min32(nfull_min), nmax);
+  const uint64_t iv0 = IV[q], iv1 = IV[4 + q];
+  uint64_t h0[NS], h1[NS];
 #pragma unroll
-    for (int j = 0; j < 4; j++) mbuf[0][qd][4 * q + j] = src[j];
-  } else {
-    pl.at(0, b, lim, t, fin, mfin);
-    load_quarter(w, p, b, lim, q);
+  for (int k = 0; k < NS; k++) {
+    h0[k] = iv0 ^ (q == 0 ? 0x01010020ull : 0ull);  // depth 1, fanout 1, nn = 32
+    h1[k] = iv1;
+  }
+  uint64_t w[NS][4];
+  const uint64_t* mrow[NS];
+  uint64_t t[NS];
+  bool fin[NS];
+  // Steps [0, nfull): whole blocks of every string of the wave: no plan, no masking,
+  // counters 128 (s + 1). The remaining steps go through the plans.
 #pragma unroll
-    for (int j = 0; j < 4; j++) mbuf[0][qd][4 * q + j] = w[j];
+  for (int k = 0; k < NS; k++) {
+    if (nfull > 0) {
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(p[k]) + 4 * q;
+#pragma unroll
+      for (int j = 0; j < 4; j++) w[k][j] = src[j];
+    } else {
+      uint64_t b, lim, tt;
+      bool f, mf;
+      pl[k].at(0, b, lim, tt, f, mf);
+      load_quarter(w[k], p[k], b, lim, q);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) mbuf[0][16 * k + qd][4 * q + j] = w[k][j];
   }
   for (uint32_t s = 0; s < nfull; s++) {
     __syncthreads();
-    if (s + 1 < nfull) {  // the next whole block, in flight during this compression
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + (size_t)(s + 1) * 16 + 4 * q;
 #pragma unroll
-      for (int j = 0; j < 4; j++) w[j] = src[j];
-    } else {
-      pl.at(s + 1, b, lim, t, fin, mfin);
-      load_quarter(w, p, b, lim, q);
+    for (int k = 0; k < NS; k++) {
+      if (s + 1 < nfull) {  // the next whole block, in flight during this compression
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(p[k]) + (size_t)(s + 1) * 16 + 4 * q;
+#pragma unroll
+        for (int j = 0; j < 4; j++) w[k][j] = src[j];
+      } else {
+        uint64_t b, lim, tt;
+        bool f, mf;
+        pl[k].at(s + 1, b, lim, tt, f, mf);
+        load_quarter(w[k], p[k], b, lim, q);
+      }
+      mrow[k] = mbuf[s & 1][16 * k + qd];
+      t[k] = 128ull * (s + 1);
+      fin[k] = false;
     }
-    compress(h0, h1, mbuf[s & 1][qd], q, iv0, iv1, 128ull * (s + 1), false);
+    compress<NS>(h0, h1, mrow, q, iv0, iv1, t, fin);
 #pragma unroll
-    for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][qd][4 * q + j] = w[j];
+    for (int k = 0; k < NS; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][16 * k + qd][4 * q + j] = w[k][j];
   }
   for (uint32_t s = nfull; s < nmax; s++) {
     __syncthreads();
-    uint64_t bn, limn, tn;
-    bool finn, mfinn;
-    pl.at(s + 1, bn, limn, tn, finn, mfinn);
-    load_quarter(w, p, bn, limn, q);  // next block, in flight during this compression
-    pl.at(s, b, lim, t, fin, mfin);
-    const uint64_t s0 = h0, s1 = h1;
-    compress(h0, h1, mbuf[s & 1][qd], q, iv0, iv1, t, fin);
-    if (DUAL && mfin && s < pl.nsteps) reinterpret_cast<uint64_t*>(out0 + 32 * (size_t)i)[q] = h0;
-    if ((DUAL && mfin) || s >= pl.nsteps) {  // msg stored / string already done: keep h
-      h0 = s0;
-      h1 = s1;
-    }
+    bool mfin[NS];
+    uint64_t s0[NS], s1[NS];
 #pragma unroll
-    for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][qd][4 * q + j] = w[j];
+    for (int k = 0; k < NS; k++) {
+      uint64_t bn, limn, tn, b, lim;
+      bool finn, mfinn;
+      pl[k].at(s + 1, bn, limn, tn, finn, mfinn);
+      load_quarter(w[k], p[k], bn, limn, q);  // next block, in flight during this compression
+      pl[k].at(s, b, lim, t[k], fin[k], mfin[k]);
+      mrow[k] = mbuf[s & 1][16 * k + qd];
+      s0[k] = h0[k];
+      s1[k] = h1[k];
+    }
+    compress<NS>(h0, h1, mrow, q, iv0, iv1, t, fin);
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      if (DUAL && mfin[k] && s < pl[k].nsteps) reinterpret_cast<uint64_t*>(out0 + 32 * (size_t)idx[k])[q] = h0[k];
+      if ((DUAL && mfin[k]) || s >= pl[k].nsteps) {  // msg stored / string already done: keep h
+        h0[k] = s0[k];
+        h1[k] = s1[k];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][16 * k + qd][4 * q + j] = w[k][j];
+    }
   }
-  if (live) reinterpret_cast<uint64_t*>((DUAL ? out1 : out0) + 32 * (size_t)i)[q] = h0;
+#pragma unroll
+  for (int k = 0; k < NS; k++)
+    if (live[k]) reinterpret_cast<uint64_t*>((DUAL ? out1 : out0) + 32 * (size_t)idx[k])[q] = h0[k];
 }
 
 }  // namespace b2q
@@ -274,19 +348,38 @@ __global__ void __launch_bounds__(64) k_b2_quad(const uint8_t* __restrict__ buf,
 
 namespace mvk {
 
+// strings per quad: 1 (the default: measured on config 4, 2 interleaved strings per quad ran
+// at the same speed -- 5.16 vs 5.11 ms -- with 60% more VGPRs). MV_B2Q_NS=2 selects the
+// interleaved kernel (experiments).
+static int b2q_ns(uint32_t) {
+  static const int env = [] {
+    const char* e = getenv("MV_B2Q_NS");
+    return e ? atoi(e) : 0;
+  }();
+  return env == 2 ? 2 : 1;
+}
+
 hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                                hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mv::b2q::k_b2_quad<false>, dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, out,
-                     (uint8_t*)nullptr);
+  if (b2q_ns(n) == 2)
+    hipLaunchKernelGGL((mv::b2q::k_b2_quad<false, 2>), dim3((n + 31) / 32), dim3(64), 0, s, buf, off, len, n, out,
+                       (uint8_t*)nullptr);
+  else
+    hipLaunchKernelGGL((mv::b2q::k_b2_quad<false, 1>), dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, out,
+                       (uint8_t*)nullptr);
   return hipGetLastError();
 }
 
 hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                                   uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mv::b2q::k_b2_quad<true>, dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, msg_out,
-                     dig_out);
+  if (b2q_ns(n) == 2)
+    hipLaunchKernelGGL((mv::b2q::k_b2_quad<true, 2>), dim3((n + 31) / 32), dim3(64), 0, s, buf, off, len, n, msg_out,
+                       dig_out);
+  else
+    hipLaunchKernelGGL((mv::b2q::k_b2_quad<true, 1>), dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, msg_out,
+                       dig_out);
   return hipGetLastError();
 }
 

@@ -306,7 +306,7 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
                                        com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr,
-                                       com_a ? (uint32_t)ctx->committee.size() : 0u));
+                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p));
   keep_events(ctx, dev.id, 0, evs);
   if (flag_dst) HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, hipMemcpyDeviceToDevice, s));
   const uint32_t ng = (n + mvk::batch_group_size(n, groups) - 1) / mvk::batch_group_size(n, groups);
