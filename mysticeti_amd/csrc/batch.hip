@@ -690,6 +690,48 @@ __global__ void __launch_bounds__(256) k_bv_keypts(const unsigned long long* __r
   }
 }
 
+// The same reduction with four lanes per element (quad25519.h), for the levels with few
+// elements, where one lane per element leaves the chip idle and the level's time is one
+// lane's chain of 8 x 3 additions and the doublings.
+__global__ void __launch_bounds__(256) k_bv_reduce_q(const uint4* __restrict__ inV, const uint4* __restrict__ inT,
+                                                     uint32_t cnt_in, int fan, int shift, uint32_t rows, uint32_t nw,
+                                                     uint32_t from_keys, uint4* __restrict__ outV,
+                                                     uint4* __restrict__ outT) {
+  const uint32_t cnt_out = (cnt_in + fan - 1) / fan;
+  const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;  // one element per quad
+  if (gid >= cnt_out * rows) return;
+  const uint32_t r = gid / cnt_out, q = gid % cnt_out;
+  const uint32_t rin = from_keys ? (r / nw) * BV_NW + r % nw : r;
+  const size_t base = (size_t)rin * cnt_in + (size_t)q * fan;
+  const int m = (int)min((uint32_t)fan, cnt_in - q * fan);
+  fe U, Sx, X;
+  qp_identity(U);
+  qp_identity(Sx);
+  if (!inV) {
+    for (int t = m - 1; t >= 0; t--) {
+      qp_load(X, inT, base + t);
+      qp_add(U, X);
+      qp_add(Sx, U);
+    }
+    qp_store(outV, gid, Sx);
+    qp_store(outT, gid, U);
+    return;
+  }
+  fe Vs;
+  qp_identity(Vs);
+  for (int t = m - 1; t >= 0; t--) {
+    qp_load(X, inT, base + t);
+    qp_add(U, X);
+    if (t > 0) qp_add(Sx, U);
+    qp_load(X, inV, base + t);
+    qp_add(Vs, X);
+  }
+  qp_dbl_n(Sx, shift);
+  qp_add(Vs, Sx);
+  qp_store(outV, gid, Vs);
+  qp_store(outT, gid, U);
+}
+
 // ---------------------------------------------------------------- final check
 // One 128-thread block. Quad g of wave 0: Horner over group g's window sums (V of the last
 // reduction level, one per window), four lanes per point. Lane g of wave 1: -[sum z s mod l]B
@@ -844,6 +886,16 @@ bool agg_disabled() {
   return v;
 }
 
+// reduction levels with at most this many elements run four lanes per element
+// (MV_REDUCE_QUAD=<n> for experiments; 0 = never)
+uint32_t reduce_quad_max() {
+  static const int v = [] {
+    const char* e = getenv("MV_REDUCE_QUAD");
+    return e ? atoi(e) : 16384;
+  }();
+  return (uint32_t)v;
+}
+
 // buckets per bucket-kernel lane (a power of two): MV_BV_SEG=<k> for experiments
 uint32_t bucket_segment(uint32_t groups) {
   static const int env = [] {
@@ -937,8 +989,12 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
     const uint32_t out = (cnt + fan - 1) / fan;
     const uint32_t lanes = out * rows;
-    hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rows, nw,
-                       inT == segT ? 1u : 0u, rv[pp], rt[pp]);
+    if (lanes <= reduce_quad_max())  // latency-bound level: four lanes per element
+      hipLaunchKernelGGL(k_bv_reduce_q, dim3((4 * lanes + 255) / 256), dim3(256), 0, s, inV, inT, cnt, fan, shift,
+                         rows, nw, inT == segT ? 1u : 0u, rv[pp], rt[pp]);
+    else
+      hipLaunchKernelGGL(k_bv_reduce, dim3((lanes + 63) / 64), dim3(64), 0, s, inV, inT, cnt, fan, shift, rows, nw,
+                         inT == segT ? 1u : 0u, rv[pp], rt[pp]);
     inV = rv[pp];
     inT = rt[pp];
     pp ^= 1;

@@ -102,4 +102,14 @@ MV_DEV void qp_load(fe& v, const uint4* base, size_t idx) {
   for (int i = 0; i < 9; i++) v.v[i] = w[i];
 }
 
+MV_DEV void qp_identity(fe& v) {
+  const uint32_t c = qlane();
+  fe_set(v, c == 1u || c == 2u ? 1u : 0u);
+}
+MV_DEV void qp_store(uint4* base, size_t idx, const fe& v) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(base + idx * 9) + 9 * qlane();
+#pragma unroll
+  for (int i = 0; i < 9; i++) w[i] = v.v[i];
+}
+
 }  // namespace mv
