@@ -54,13 +54,6 @@ constexpr int BV_FINE_BITS = 8;             // bucket sort: partition = key >> 8
 constexpr int BV_NPG = BV_NKG >> BV_FINE_BITS;  // 7 high magnitude bits), then 256 buckets
 constexpr int BV_FAN = 8;                   // reduction fan-in
 constexpr int BV_MAXG = mvk::BATCH_MAX_GROUPS;  // sub-batch equations per batch
-// precomp point, 27 words: padded to one 128-B line (MV_PT112: packed at 112 B), so a
-// bucket's gather touches one line instead of 1.75 on average
-#ifdef MV_PT112
-constexpr int PT_QUADS = 7;
-#else
-constexpr int PT_QUADS = 8;
-#endif
 constexpr int P3_QUADS = 9;
 constexpr int SC_QUADS = 3;                 // z (4 words), z*k mod l (8 words)
 constexpr int BSUM_WORDS = 12;              // z * s < 2^381
@@ -897,12 +890,12 @@ uint32_t reduce_quad_max() {
 }
 
 // buckets per bucket-kernel lane (a power of two): MV_BV_SEG=<k> for experiments
-uint32_t bucket_segment(uint32_t groups) {
+uint32_t bucket_segment(uint32_t) {
   static const int env = [] {
     const char* e = getenv("MV_BV_SEG");
     return e ? atoi(e) : -1;
   }();
-  uint32_t seg = env > 0 ? (uint32_t)env : (groups >= 8 ? groups : 1u);
+  uint32_t seg = env > 0 ? (uint32_t)env : 1u;  // 1: measured best for 1..16 groups with the quad reduce
   if (seg > 64) seg = 64;
   return 1u << (31 - __builtin_clz(seg));
 }
@@ -1008,7 +1001,9 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // exact fallback: re-verifies the signatures of every group whose equation failed
-  e = launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag + 1, G.cpg * PART_CHUNK);
+  // (R and A as k_bv_prep decoded them: no decompression)
+  e = launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag + 1, G.cpg * PART_CHUNK, pts,
+                    ca.tab && ca.aggregate ? comb_a : nullptr);
   mark(6);
   return e;
 }

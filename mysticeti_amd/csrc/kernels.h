@@ -10,9 +10,12 @@ size_t btable_bytes();
 hipError_t launch_btable_init(void* d_btab, hipStream_t s);
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
-                         const uint32_t* skip = nullptr, uint32_t skip_group = 0);
+                         const uint32_t* skip = nullptr, uint32_t skip_group = 0, const void* prep_pts = nullptr,
+                         const void* prep_comb = nullptr);
 // skip (optional, device): per-group flags; the signatures of group g = i / skip_group
 // (skip_group a multiple of 256; 0 = one group) are not verified when skip[g] != 0.
+// prep_pts (the batch path's fallback): R and A as k_bv_prep decoded them (A from the comb
+// tables prep_comb when it was summed per key), and prep's nonzero statuses kept.
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
                        uint8_t* sig, hipStream_t s);
 hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,

@@ -25,6 +25,7 @@
 #include "kernels.h"
 #include "scalar25519.h"
 #include "tables.h"
+#include "comb.h"
 
 namespace mv {
 
@@ -149,6 +150,16 @@ MV_DEV void vtab_build(uint4* tab, const p3& P) {
   }
 }
 
+// What the batch path's k_bv_prep already decoded (the fallback re-verifies from it): R at
+// pts[i] and A at pts[n + i] (affine precomp), or A from the committee's comb table entry
+// [0][1] = [1](-A) when it was summed per key; status[i] != 0 is prep's final verdict
+// (s >= l or a point that does not decode) and stays.
+struct PrepView {
+  const uint4* pts;   // nullptr: decode A and R here
+  uint32_t n;
+  const uint4* comb;  // non-null: A of key b from the comb tables
+};
+
 // One signature per lane. pk rows are read at key_idx[i] when key_idx != nullptr.
 // MINW = minimum waves per SIMD (2 -> <= 256 VGPRs, 1 -> <= 512).
 //
@@ -162,7 +173,7 @@ __global__ void __launch_bounds__(256, MINW)
     k_verify(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
              const uint32_t* __restrict__ key_idx, uint32_t n, const uint4* __restrict__ btab_g,
              uint4* __restrict__ scratch, uint8_t* __restrict__ status, const uint32_t* __restrict__ skip,
-             uint32_t skip_group) {
+             uint32_t skip_group, PrepView pv) {
   // batch fallback (batch.hip): nothing to do for a group whose equation held (skip_group
   // is a multiple of the block size, so the test is uniform over the block)
   if (skip && skip[skip_group ? blockIdx.x * blockDim.x / skip_group : 0]) return;
@@ -224,7 +235,28 @@ __global__ void __launch_bounds__(256, MINW)
     MV_PHASE(3);
 
     p3 A, R, nR;
-    decompress_x2(A, okA, aw, R, okR, rw);
+    if (pv.pts) {  // decoded by k_bv_prep; lanes prep already rejected keep its verdict
+      const bool prep_ok = status[idx] == 0;
+      okA = prep_ok;
+      okR = prep_ok;
+      s_ok = s_ok && prep_ok;
+      uint4 q[7];
+      precomp pc;
+      const uint4* pr = pv.pts + (size_t)idx * PT_QUADS;
+#pragma unroll
+      for (int k = 0; k < 7; k++) q[k] = pr[k];
+      quads_to_precomp(pc, q);
+      precomp_to_p3(R, pc);
+      const uint4* pa = pv.comb ? pv.comb + (size_t)(key_idx ? key_idx[idx] : idx) * CT_TABLE + CT_QUADS
+                                : pv.pts + ((size_t)pv.n + idx) * PT_QUADS;
+#pragma unroll
+      for (int k = 0; k < 7; k++) q[k] = pa[k];
+      quads_to_precomp(pc, q);
+      if (pv.comb) precomp_cneg(pc, true);  // the tables hold -A
+      precomp_to_p3(A, pc);
+    } else {
+      decompress_x2(A, okA, aw, R, okR, rw);
+    }
     MV_PHASE(4);
     // -[c]A = [|c|](-A) for c >= 0, [|c|]A for c < 0
     if (!c_neg) p3_neg(A, A);
@@ -283,7 +315,7 @@ __global__ void __launch_bounds__(256, MINW)
     p1p1_to_p2(P, Q);
   }
   const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
-  if (gid < n) {
+  if (gid < n && !(pv.pts && !okA)) {  // (prep's own verdicts stay)
     uint8_t st = !okA ? 2 : ((s_ok && okR && ident) ? 0 : 1);
     status[gid] = st;
   }
@@ -577,17 +609,18 @@ hipError_t launch_btable_init(void* d_btab, hipStream_t s) {
 }
 hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
-                         const uint32_t* skip, uint32_t skip_group) {
+                         const uint32_t* skip, uint32_t skip_group, const void* prep_pts, const void* prep_comb) {
   if (n == 0) return hipSuccess;
+  const mv::PrepView pv{static_cast<const uint4*>(prep_pts), n, static_cast<const uint4*>(prep_comb)};
   if (verify_variant() == 1)
     hipLaunchKernelGGL(mv::k_verify<1>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group);
+                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group, pv);
   else if (verify_variant() == 3)
     hipLaunchKernelGGL(mv::k_verify<3>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group);
+                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group, pv);
   else
     hipLaunchKernelGGL(mv::k_verify<2>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group);
+                       (const uint4*)btab, (uint4*)scratch, status, skip, skip_group, pv);
   return hipGetLastError();
 }
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
