@@ -82,6 +82,11 @@ struct HostBuf {
 struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
+  // host-buffer batch verifies: two compute streams and double-buffered device inputs, so
+  // the (pageable) H2D of one chunk runs beside the previous chunk's verification
+  hipStream_t pstream[2] = {nullptr, nullptr};
+  DevBuf pin_msg[2], pin_sig[2], pin_pk[2], pin_st[2];
+  hipEvent_t pin_free[2] = {nullptr, nullptr};
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
   DevBuf committee_pk, stakes, combA, keyok;
@@ -631,6 +636,54 @@ void run_block_requests(mv_ctx* ctx, std::vector<mv_ctx::BlockReq*>& reqs) {
   }
 }
 
+// mv_ed25519_verify's batch path over [lo, hi) of the caller's (pageable) arrays, in chunks
+// of >= MV_BATCH_MIN signatures: chunk c's inputs go to buffer c % 2 by H2D copies issued on
+// compute stream c % 2, so while the host thread stages chunk c + 1 the device verifies
+// chunk c; statuses come back into pinned staging (one D2H per chunk) and are copied out at
+// the end. pk rows by item, or committee keys by key_idx.
+mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
+                                const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status) {
+  const uint64_t m = hi - lo;
+  uint64_t chunks = (m + (1u << 18) - 1) >> 18;  // ~256k signatures per chunk
+  if (chunks < 4) chunks = 4;
+  uint64_t cs = ((m + chunks - 1) / chunks + 1023) & ~1023ull;
+  if (cs < MV_BATCH_MIN) cs = MV_BATCH_MIN;
+  if (cs > ctx->max_batch) cs = ctx->max_batch;
+  for (int k = 0; k < 2; k++) {
+    if (!dev.pstream[k]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking));
+    if (!dev.pin_free[k]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[k], hipEventDisableTiming));
+    HIPCHK(ctx, dev.pin_msg[k].ensure(32 * cs));
+    HIPCHK(ctx, dev.pin_sig[k].ensure(64 * cs));
+    HIPCHK(ctx, dev.pin_pk[k].ensure((pk ? 32 : 4) * cs));
+    HIPCHK(ctx, dev.pin_st[k].ensure(cs));
+  }
+  HIPCHK(ctx, dev.h_out.ensure(m));
+  uint8_t* hst = dev.h_out.as<uint8_t>();
+  const uint8_t* dpk_com = dev.committee_pk.as<uint8_t>();
+  uint64_t c = 0;
+  for (uint64_t i = lo; i < hi; i += cs, c++) {
+    const uint32_t b = (uint32_t)(c & 1);
+    const uint32_t k = (uint32_t)std::min<uint64_t>(cs, hi - i);
+    hipStream_t st = dev.pstream[b];
+    // buffer b was last read by chunk c - 2 on this same stream: stream order protects it
+    HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, msg + 32 * i, 32 * (size_t)k, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, sig + 64 * i, 64 * (size_t)k, hipMemcpyHostToDevice, st));
+    if (pk) HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, pk + 32 * i, 32 * (size_t)k, hipMemcpyHostToDevice, st));
+    else HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, key_idx + i, 4 * (size_t)k, hipMemcpyHostToDevice, st));
+    mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
+                                 pk ? dev.pin_pk[b].as<uint8_t>() : dpk_com,
+                                 pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), st,
+                                 nullptr);
+    if (rc != MV_OK) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[0]));
+  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[1]));
+  poll_flags(ctx, dev);
+  memcpy(status + lo, hst, m);
+  return MV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -718,6 +771,11 @@ void mv_destroy(mv_ctx* ctx) {
       if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.sscr_done)
       if (ev) (void)hipEventDestroy(ev);
+    for (int k = 0; k < 2; k++) {
+      for (DevBuf* b : {&dev.pin_msg[k], &dev.pin_sig[k], &dev.pin_pk[k], &dev.pin_st[k]}) b->release();
+      if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
+      if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
+    }
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);
     for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
@@ -823,6 +881,9 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
   }
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
+    // large host-buffer batches: copies of one chunk beside the verification of the previous
+    if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo >= 4ull * MV_BATCH_MIN && !getenv("MV_NO_PIPELINE"))
+      return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {
       uint32_t m = (uint32_t)std::min<uint64_t>(ctx->max_batch, hi - i);
       HIPCHK(ctx, dev.msg.ensure(32 * (size_t)m));

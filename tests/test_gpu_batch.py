@@ -242,3 +242,25 @@ def test_adaptive_guard_after_a_failed_batch():
         assert d == (1, 1, 8, 1)
         st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, sig, pk))
         assert (st == 0).all() and d == (1, 0, 8, 0)
+
+
+@pytest.mark.parametrize("committee", [False, True])
+def test_pipelined_host_batches(engine, committee):
+    """Host-buffer calls of >= 4 x MV_BATCH_MIN signatures run in chunks whose copies overlap
+    the previous chunk's verification; ragged chunk sizes, committee-key rows and bad
+    signatures in several chunks keep exact verdicts."""
+    rng = np.random.default_rng(41 + committee)
+    n = 5 * M.BATCH_MIN + 333
+    msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    if committee:
+        seeds = rng.integers(0, 256, size=(9, 32), dtype=np.uint8)
+        ki = rng.integers(0, 9, size=n).astype(np.uint32)
+        pk, sig = engine.ed25519_sign(seeds[ki], msg)
+        engine.set_committee(pk[[int(np.nonzero(ki == a)[0][0]) for a in range(9)]], np.ones(9, np.uint64))
+    else:
+        pk, sig = engine.ed25519_sign(rng.integers(0, 256, size=(n, 32), dtype=np.uint8), msg)
+    sig = sig.copy()
+    bad = [3, n // 3, n - 2]
+    sig[bad, 45] ^= 0x20
+    st = engine.ed25519_verify(msg, sig, key_idx=ki) if committee else engine.ed25519_verify(msg, sig, pk)
+    assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
