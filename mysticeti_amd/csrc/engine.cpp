@@ -882,7 +882,7 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
     // large host-buffer batches: copies of one chunk beside the verification of the previous
-    if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo >= 4ull * MV_BATCH_MIN && !getenv("MV_NO_PIPELINE"))
+    if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN && !getenv("MV_NO_PIPELINE"))
       return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {
       uint32_t m = (uint32_t)std::min<uint64_t>(ctx->max_batch, hi - i);

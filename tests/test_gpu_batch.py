@@ -40,7 +40,8 @@ def test_valid_batches_pass_without_fallback(engine, n):
     msg, sig, pk = signed(engine, n, n)
     st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
     assert (st == 0).all()
-    assert nb == 1 and nf == 0
+    # calls above 8 x MV_BATCH_MIN are verified in pipelined chunks, one batch each
+    assert (nb == 1 if n <= 8 * M.BATCH_MIN else nb >= 4) and nf == 0
 
 
 def test_one_bad_signature_falls_back_exactly(engine):
@@ -250,7 +251,7 @@ def test_pipelined_host_batches(engine, committee):
     the previous chunk's verification; ragged chunk sizes, committee-key rows and bad
     signatures in several chunks keep exact verdicts."""
     rng = np.random.default_rng(41 + committee)
-    n = 5 * M.BATCH_MIN + 333
+    n = 9 * M.BATCH_MIN + 333
     msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     if committee:
         seeds = rng.integers(0, 256, size=(9, 32), dtype=np.uint8)
