@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -86,6 +87,7 @@ struct Device {
   // the (pageable) H2D of one chunk runs beside the previous chunk's verification
   hipStream_t pstream[2] = {nullptr, nullptr};
   DevBuf pin_msg[2], pin_sig[2], pin_pk[2], pin_st[2];
+  HostBuf h_stage[2];
   hipEvent_t pin_free[2] = {nullptr, nullptr};
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
@@ -636,19 +638,39 @@ void run_block_requests(mv_ctx* ctx, std::vector<mv_ctx::BlockReq*>& reqs) {
   }
 }
 
+// memcpy with up to `threads` host threads (pageable -> pinned staging)
+void par_memcpy(void* dst, const void* src, size_t bytes, unsigned threads) {
+  if (threads <= 1 || bytes < (4u << 20)) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t part = ((bytes + threads - 1) / threads + 4095) & ~(size_t)4095;
+  for (size_t o = part; o < bytes; o += part)
+    th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
+  memcpy(dst, src, std::min(part, bytes));
+  for (auto& t : th) t.join();
+}
+
 // mv_ed25519_verify's batch path over [lo, hi) of the caller's (pageable) arrays, in chunks
-// of >= MV_BATCH_MIN signatures: chunk c's inputs go to buffer c % 2 by H2D copies issued on
-// compute stream c % 2, so while the host thread stages chunk c + 1 the device verifies
-// chunk c; statuses come back into pinned staging (one D2H per chunk) and are copied out at
-// the end. pk rows by item, or committee keys by key_idx.
+// of >= 8 x MV_BATCH_MIN signatures, three stages deep: the host packs chunk c + 1 into
+// pinned staging (several threads; pageable H2D copies run at a fraction of PCIe) while the
+// device copies chunk c in from pinned memory and verifies it on compute stream c % 2
+// (double-buffered device inputs, stream-ordered reuse); statuses return by one D2H per
+// chunk into pinned staging. pk rows by item, or committee keys by key_idx.
 mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
                                 const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status) {
   const uint64_t m = hi - lo;
-  uint64_t chunks = (m + (1u << 18) - 1) >> 18;  // ~256k signatures per chunk
-  if (chunks < 4) chunks = 4;
+  static const int chunk_log2 = [] {  // MV_PIPE_CHUNK_LOG2 (experiments): signatures per chunk
+    const char* e = getenv("MV_PIPE_CHUNK_LOG2");
+    return e ? atoi(e) : 18;
+  }();
+  uint64_t chunks = (m + (1ull << chunk_log2) - 1) >> chunk_log2;
+  if (chunks < 2) chunks = 2;
   uint64_t cs = ((m + chunks - 1) / chunks + 1023) & ~1023ull;
   if (cs < MV_BATCH_MIN) cs = MV_BATCH_MIN;
   if (cs > ctx->max_batch) cs = ctx->max_batch;
+  const size_t rowb = 32 + 64 + (pk ? 32 : 4);  // staged bytes per signature: msg | sig | pk or key index
   for (int k = 0; k < 2; k++) {
     if (!dev.pstream[k]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking));
     if (!dev.pin_free[k]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[k], hipEventDisableTiming));
@@ -656,29 +678,52 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
     HIPCHK(ctx, dev.pin_sig[k].ensure(64 * cs));
     HIPCHK(ctx, dev.pin_pk[k].ensure((pk ? 32 : 4) * cs));
     HIPCHK(ctx, dev.pin_st[k].ensure(cs));
+    HIPCHK(ctx, dev.h_stage[k].ensure(rowb * cs));
   }
   HIPCHK(ctx, dev.h_out.ensure(m));
   uint8_t* hst = dev.h_out.as<uint8_t>();
   const uint8_t* dpk_com = dev.committee_pk.as<uint8_t>();
+  const unsigned hw = std::thread::hardware_concurrency();
+  static const unsigned max_thr = [] {  // MV_PIPE_THREADS (experiments): host staging threads
+    const char* e = getenv("MV_PIPE_THREADS");
+    return e ? (unsigned)atoi(e) : 8u;
+  }();
+  const unsigned threads = hw == 0 ? 4u : std::min(max_thr, hw);
+  bool staged_used[2] = {false, false};
+  static const bool trace = getenv("MV_PIPE_TRACE") != nullptr;  // diagnostics: host-side stage times
+  auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = now();
   uint64_t c = 0;
   for (uint64_t i = lo; i < hi; i += cs, c++) {
     const uint32_t b = (uint32_t)(c & 1);
     const uint32_t k = (uint32_t)std::min<uint64_t>(cs, hi - i);
     hipStream_t st = dev.pstream[b];
-    // buffer b was last read by chunk c - 2 on this same stream: stream order protects it
-    HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, msg + 32 * i, 32 * (size_t)k, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, sig + 64 * i, 64 * (size_t)k, hipMemcpyHostToDevice, st));
-    if (pk) HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, pk + 32 * i, 32 * (size_t)k, hipMemcpyHostToDevice, st));
-    else HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, key_idx + i, 4 * (size_t)k, hipMemcpyHostToDevice, st));
+    // pinned staging b is free once chunk c - 2's H2D copies (on stream b) are done
+    const double ta = now();
+    if (staged_used[b]) HIPCHK(ctx, hipEventSynchronize(dev.pin_free[b]));
+    const double tb = now();
+    uint8_t* hs = dev.h_stage[b].as<uint8_t>();
+    par_memcpy(hs, msg + 32 * i, 32 * (size_t)k, threads);
+    par_memcpy(hs + 32 * cs, sig + 64 * i, 64 * (size_t)k, threads);
+    if (pk) par_memcpy(hs + 96 * cs, pk + 32 * i, 32 * (size_t)k, threads);
+    else par_memcpy(hs + 96 * cs, key_idx + i, 4 * (size_t)k, threads);
+    HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, hs, 32 * (size_t)k, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, hs + 32 * cs, 64 * (size_t)k, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, hs + 96 * cs, (pk ? 32 : 4) * (size_t)k, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipEventRecord(dev.pin_free[b], st));
+    staged_used[b] = true;
     mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dpk_com,
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), st,
                                  nullptr);
     if (rc != MV_OK) return rc;
     HIPCHK(ctx, hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, st));
+    if (trace) fprintf(stderr, "[pipe] chunk %lu: wait %.0f us, stage+enqueue %.0f us\n", (unsigned long)c, tb - ta, now() - tb);
   }
+  const double t1 = now();
   HIPCHK(ctx, hipStreamSynchronize(dev.pstream[0]));
   HIPCHK(ctx, hipStreamSynchronize(dev.pstream[1]));
+  if (trace) fprintf(stderr, "[pipe] issue %.0f us, drain %.0f us, threads %u\n", t1 - t0, now() - t1, threads);
   poll_flags(ctx, dev);
   memcpy(status + lo, hst, m);
   return MV_OK;
@@ -773,6 +818,7 @@ void mv_destroy(mv_ctx* ctx) {
       if (ev) (void)hipEventDestroy(ev);
     for (int k = 0; k < 2; k++) {
       for (DevBuf* b : {&dev.pin_msg[k], &dev.pin_sig[k], &dev.pin_pk[k], &dev.pin_st[k]}) b->release();
+      dev.h_stage[k].release();
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
@@ -881,8 +927,14 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
   }
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
-    // large host-buffer batches: copies of one chunk beside the verification of the previous
-    if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN && !getenv("MV_NO_PIPELINE"))
+    // large host-buffer batches, chunked with the copies of one chunk beside the verification
+    // of the previous: opt-in (MV_PIPELINE=1). Measured on MI355X + EPYC 9575F for 2^20
+    // signatures it is slower than one direct pageable H2D per call (118-127 vs 132 M/s over
+    // 2^18..2^20-signature chunks and 8 or 16 staging threads): host memcpy into pinned
+    // staging runs at ~10 GB/s per thread, and chunks below 2^20 cost the batch path's
+    // fixed per-batch work
+    static const bool pipeline = getenv("MV_PIPELINE") && getenv("MV_PIPELINE")[0] == '1';
+    if (pipeline && !(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN)
       return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {
       uint32_t m = (uint32_t)std::min<uint64_t>(ctx->max_batch, hi - i);
