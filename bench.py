@@ -64,12 +64,16 @@ def slots(field_ops: int, hash_ops: int) -> int:
     return field_ops * FIELD_MACS * MAC_SLOTS + hash_ops
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/), if any."""
+def pmc_traffic(kernel: str, workload: str = "c2"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/<round>/
+    pmc_<workload>_<kernel>.json from tools/profile_r02.sh, or the round-1 pmc_<kernel>.json)."""
     import glob
 
-    files = glob.glob(os.path.join(ROOT, "profiles", "**", f"pmc_{kernel}.json"), recursive=True)
-    for f in sorted(files, key=lambda p: ("final" in p, p), reverse=True):  # newest round summary first
+    files = []
+    for pat in (f"pmc_{workload}_{kernel}.json", f"pmc_{kernel}.json"):
+        files += glob.glob(os.path.join(ROOT, "profiles", "**", pat), recursive=True)
+    rnd = lambda p: os.path.relpath(p, os.path.join(ROOT, "profiles")).split(os.sep)[0]  # r01, r02, ...
+    for f in sorted(files, key=lambda p: (rnd(p), "final" in p, f"pmc_{workload}_" in p), reverse=True):
         try:
             d = json.load(open(f))
             return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)

@@ -327,11 +327,14 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
                    "impl": "oracle/block.c StatementBlock::verify (parse, 2 x BLAKE2b, ZIP-215 verify), gcc -O3 "
                            "-march=native, persistent thread pool"}
     roof = None
+    from bench import pmc_traffic
+
+    traffic, traffic_src = pmc_traffic("k_b2_quad", "c4")
     if hash_ms:
         ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
         roof = {"bound": "valu", "kernel": "k_b2_quad", "kernel_ms": hash_ms,
                 "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
-                "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": None,
+                "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
                                   f"algorithmic) x {W_BLAKE2B_OPS} ops"}
     ok = all_ranks_ok(ok, dist)
