@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     precomp pc;
     if (ca.tab) {  // committee key: R is the only decode
       p3 P;
-      decompress1(P, okR, rw);
+      decompress1_lean(P, okR, rw);
       precomp_from_affine(pc, P);
       if (live) pt_store(pts, gid, pc);
       okA = ca.ok[kid] != 0;
@@ -258,10 +258,11 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     } else {
 #ifdef MV_PREP_SEQ  // experiment: one decode at a time (fewer registers, more waves)
     p3 P;
-    decompress1(P, okR, rw);
+    decompress1_lean(P, okR, rw);
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, gid, pc);
-    decompress1(P, okA, aw);
+    load8(aw, pk + 32 * (size_t)kid);  // reloaded: not held across R's decode
+    decompress1_lean(P, okA, aw);
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, (size_t)n + gid, pc);
 #else

@@ -37,23 +37,45 @@ constexpr uint8_t SIGMA[12][16] = {
     {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
     {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
 
-// The message word lane q adds in round r, slot k (0/1: column step x/y, 2/3: diagonal step
-// x/y) is SIGMA[r][8 (k >> 1) + 2q + (k & 1)]; packed 4 bits per lane.
-constexpr uint32_t msel(int r, int k) {
-  uint32_t c = 0;
-  for (int q = 0; q < 4; q++) c |= (uint32_t)SIGMA[r][8 * (k >> 1) + 2 * q + (k & 1)] << (4 * q);
+// LDS layout of a message block: word w of string j sits at u64 index
+// WH[w] * 16 NS * 4 + 4 j + WG[w] of the buffer ([rank][string][class]). A ds_read_b64 half-wave
+// is 8 quads (strings) x 4 lanes, and lane q of every quad reads the same word SIGMA[r][...];
+// quad j's four reads land on 8-byte bank slots 4 j + WG[w] (mod 32), so they are conflict-
+// free when the four words have distinct classes WG. No class map makes all 40 distinct
+// SIGMA word quadruples rainbow (exhaustive search); this one (local search) costs 1.60 LDS
+// cycles per half-wave read on average, against 2.65 for rows padded to 17 words.
+constexpr uint8_t WG[16] = {0, 0, 2, 0, 1, 0, 3, 3, 1, 3, 2, 1, 3, 1, 2, 2};
+constexpr uint8_t WH[16] = {0, 1, 0, 2, 0, 3, 0, 1, 1, 2, 1, 2, 3, 3, 2, 3};
+template <int NS>
+constexpr uint32_t woff(int w) { return (uint32_t)WH[w] * 64u * NS + WG[w]; }  // u64 units from the string's base
+
+// The u64 offset lane q reads in round r, slot k (0/1: column step x/y, 2/3: diagonal step
+// x/y) is woff(SIGMA[r][8 (k >> 1) + 2q + (k & 1)]); packed 8 bits per lane (NS = 1) or 16
+// bits per lane (NS = 2).
+template <int NS>
+constexpr uint64_t msel(int r, int k) {
+  uint64_t c = 0;
+  for (int q = 0; q < 4; q++) c |= (uint64_t)woff<NS>(SIGMA[r][8 * (k >> 1) + 2 * q + (k & 1)]) << ((NS == 1 ? 8 : 16) * q);
   return c;
 }
+template <int NS>
 struct Sel {
-  uint32_t v[12][4];
+  uint64_t v[12][4];
 };
-constexpr Sel make_sel() {
-  Sel s{};
+template <int NS>
+constexpr Sel<NS> make_sel() {
+  Sel<NS> s{};
   for (int r = 0; r < 12; r++)
-    for (int k = 0; k < 4; k++) s.v[r][k] = msel(r, k);
+    for (int k = 0; k < 4; k++) s.v[r][k] = msel<NS>(r, k);
   return s;
 }
-constexpr Sel SEL = make_sel();
+template <int NS>
+constexpr Sel<NS> SEL = make_sel<NS>();
+template <int NS>
+MV_DEV uint32_t sel_at(int r, int k, uint32_t q) {
+  if (NS == 1) return __builtin_amdgcn_ubfe((uint32_t)SEL<1>.v[r][k], 8 * q, 8);  // one v_bfe_u32
+  return (uint32_t)(SEL<NS>.v[r][k] >> (16 * q)) & 0xffffu;
+}
 
 constexpr uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                             0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
@@ -82,8 +104,8 @@ MV_DEV uint64_t ror63(uint64_t x) {
 template <int K>
 MV_DEV uint64_t qrot(uint64_t x) {
   constexpr int ctrl = ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, ctrl, 0xf, 0xf, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), ctrl, 0xf, 0xf, false);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, ctrl, 0xf, 0xf, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), ctrl, 0xf, 0xf, true);
   return pack(lo, hi);
 }
 
@@ -114,14 +136,19 @@ MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* con
     vd[k] = iv1 ^ (q == 0 ? t[k] : 0ull);        // v[12] ^= t (t_hi = 0: v[13] unchanged)
     vd[k] = (q == 2 && fin[k]) ? ~vd[k] : vd[k];  // v[14] = ~v[14] on the final block
   }
-  const uint32_t sh = 4 * q;
 #pragma unroll
   for (int r = 0; r < 12; r++) {
     // keep each round's message reads in their round: hoisting all 48 ahead of the chain
     // (what the scheduler does unchecked) doubles the VGPRs and halves the waves per SIMD
     asm volatile("" ::: "memory");
-    const uint32_t i0 = (SEL.v[r][0] >> sh) & 15u, i1 = (SEL.v[r][1] >> sh) & 15u;
-    const uint32_t i2 = (SEL.v[r][2] >> sh) & 15u, i3 = (SEL.v[r][3] >> sh) & 15u;
+#ifdef MV_B2Q_NOHOIST
+    uint32_t qq = q;
+    asm volatile("" : "+v"(qq));  // offsets computed in their round, not hoisted (registers)
+#else
+    const uint32_t qq = q;
+#endif
+    const uint32_t i0 = sel_at<NS>(r, 0, qq), i1 = sel_at<NS>(r, 1, qq);
+    const uint32_t i2 = sel_at<NS>(r, 2, qq), i3 = sel_at<NS>(r, 3, qq);
     uint64_t x0[NS], y0[NS], x1[NS], y1[NS];
 #pragma unroll
     for (int k = 0; k < NS; k++) {
@@ -234,12 +261,19 @@ MV_DEV void load_quarter(uint64_t w[4], const uint8_t* p, uint64_t b, uint64_t l
 // 16 * NS strings per 64-lane workgroup: quad qd takes strings 16 k + qd, k < NS. DUAL:
 // out0 = B2(P) (msg), out1 = B2(P || sig) (digest); otherwise out0 = B2(string).
 template <bool DUAL, int NS>
-__global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+#ifdef MV_B2Q_NOHOIST
+#define MV_B2Q_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6)))
+#else
+#define MV_B2Q_BOUNDS __launch_bounds__(64, NS == 1 ? 4 : 3)
+#endif
+__global__ void MV_B2Q_BOUNDS k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                 const uint64_t* __restrict__ len, uint32_t n,
                                                 uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
-  // [buffer][string][word], rows padded to 17 words: the 16 strings' rows start 34 banks
-  // apart, so the lanes of one message-word read (one word per string) hit distinct banks
-  __shared__ uint64_t mbuf[2][16 * NS][17];
+  // [buffer][word rank][string][word class] (WG/WH above)
+  __shared__ uint64_t mbuf[2][4][16 * NS][4];
+  uint32_t wo[4];  // offsets of this lane's quarter (words 4q .. 4q+3) from the string's base
+#pragma unroll
+  for (int j = 0; j < 4; j++) wo[j] = (uint32_t)WH[4 * (threadIdx.x & 3) + j] * 64u * NS + WG[4 * (threadIdx.x & 3) + j];
   const uint32_t lane = threadIdx.x, q = lane & 3, qd = lane >> 2;
   uint32_t idx[NS];
   bool live[NS];
@@ -285,7 +319,7 @@ __global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* 
       load_quarter(w[k], p[k], b, lim, q);
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++) mbuf[0][16 * k + qd][4 * q + j] = w[k][j];
+    for (int j = 0; j < 4; j++) (&mbuf[0][0][16 * k + qd][0])[wo[j]] = w[k][j];
   }
   for (uint32_t s = 0; s < nfull; s++) {
     __syncthreads();
@@ -301,7 +335,7 @@ __global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* 
         pl[k].at(s + 1, b, lim, tt, f, mf);
         load_quarter(w[k], p[k], b, lim, q);
       }
-      mrow[k] = mbuf[s & 1][16 * k + qd];
+      mrow[k] = &mbuf[s & 1][0][16 * k + qd][0];
       t[k] = 128ull * (s + 1);
       fin[k] = false;
     }
@@ -309,7 +343,7 @@ __global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* 
 #pragma unroll
     for (int k = 0; k < NS; k++)
 #pragma unroll
-      for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][16 * k + qd][4 * q + j] = w[k][j];
+      for (int j = 0; j < 4; j++) (&mbuf[(s + 1) & 1][0][16 * k + qd][0])[wo[j]] = w[k][j];
   }
   for (uint32_t s = nfull; s < nmax; s++) {
     __syncthreads();
@@ -322,7 +356,7 @@ __global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* 
       pl[k].at(s + 1, bn, limn, tn, finn, mfinn);
       load_quarter(w[k], p[k], bn, limn, q);  // next block, in flight during this compression
       pl[k].at(s, b, lim, t[k], fin[k], mfin[k]);
-      mrow[k] = mbuf[s & 1][16 * k + qd];
+      mrow[k] = &mbuf[s & 1][0][16 * k + qd][0];
       s0[k] = h0[k];
       s1[k] = h1[k];
     }
@@ -335,7 +369,7 @@ __global__ void __launch_bounds__(64, NS == 1 ? 4 : 3) k_b2_quad(const uint8_t* 
         h1[k] = s1[k];
       }
 #pragma unroll
-      for (int j = 0; j < 4; j++) mbuf[(s + 1) & 1][16 * k + qd][4 * q + j] = w[k][j];
+      for (int j = 0; j < 4; j++) (&mbuf[(s + 1) & 1][0][16 * k + qd][0])[wo[j]] = w[k][j];
     }
   }
 #pragma unroll
