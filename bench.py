@@ -144,10 +144,11 @@ def main():
     ap.add_argument("--path", choices=["batch", "single"], default="batch",
                     help="batch: one combined equation per step (batch.hip) with exact fallback; "
                          "single: every signature verified alone (k_verify)")
-    ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
+    ap.add_argument("--workload", choices=["config2", "config4", "config5", "wal"], default="config2",
                     help="config2 (default, the headline line): 1M independent signatures per GPU; "
                          "config4: HBM-resident 100-validator blocks through the device block pipeline; "
-                         "config5: p50/p99 latency of 64-block batches, GPU vs host cores")
+                         "config5: p50/p99 latency of 64-block batches, GPU vs host cores; "
+                         "wal: WAL replay check (SURVEY.md 8 f4) over an HBM-resident image")
     ap.add_argument("--batches", type=int, default=10000, help="config5: GPU batches timed per shape")
     ap.add_argument("--conc-seconds", type=float, default=3.0, help="config5: seconds of concurrent 1-block callers")
     ap.add_argument("--corrupt", type=int, default=0, help="signatures per batch with a flipped s bit")
@@ -159,6 +160,9 @@ def main():
     ap.add_argument("--no-config4", dest="config4", action="store_false",
                     help="skip the config-4 (100-validator blocks) rate in the default line")
     ap.add_argument("--config4-batch", type=int, default=1 << 20, help="config-4 blocks per GPU per step")
+    ap.add_argument("--no-wal", dest="wal", action="store_false",
+                    help="skip the WAL replay-check rate (row f4) in the default line")
+    ap.add_argument("--wal-entries", type=int, default=1 << 20, help="WAL entries (config-4 blocks) per GPU")
     args = ap.parse_args()
     if args.workload != "config2":
         import bench_blocks
@@ -362,6 +366,15 @@ def main():
                                             cpu=args.cpu_sample > 0)
         ok = ok and cfg4["correct"]
 
+    # f4: the WAL replay check over an HBM-resident WAL of config-4 blocks (bench_wal.wal_measure)
+    walr = None
+    if args.wal and args.path == "batch" and not args.corrupt:
+        import bench_wal
+
+        walr = bench_wal.wal_measure(eng, torch, local_rank, world, dist, n=args.wal_entries,
+                                     steps=max(3, args.steps // 4), warmup=1, cpu=args.cpu_sample > 0)
+        ok = ok and walr["correct"]
+
     out = None
     if rank == 0:
         e2e = None
@@ -421,6 +434,7 @@ def main():
             "sustained": sustained,
             "adversarial": adversarial,
             "config4": cfg4,
+            "wal": walr,
             "end_to_end": e2e,
             "correct": bool(ok),
             "path": args.path,

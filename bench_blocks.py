@@ -98,6 +98,18 @@ def run(args) -> int:
     try:
         if args.workload == "config5":
             return config5(args, eng, rank)
+        if args.workload == "wal":
+            import bench_wal
+
+            res = bench_wal.wal_measure(eng, torch, local_rank, world, dist, n=args.wal_entries, steps=args.steps,
+                                        warmup=args.warmup, cpu=args.cpu_sample > 0)
+            if rank == 0:
+                out = {"metric": "WAL replay check throughput (WalIterator + crc32 per entry)"}
+                out.update(res)
+                out["n_gpus"], out["steps"], out["warmup"] = world, args.steps, args.warmup
+                out["higher_is_better"], out["scaling"], out["vs_baseline"], out["dtype"] = True, "weak", None, "u8"
+                print(json.dumps(out), flush=True)
+            return 0 if res["correct"] else 1
         return config4(args, eng, torch, local_rank, rank, world, dist)
     finally:
         eng.close()

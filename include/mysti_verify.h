@@ -21,6 +21,12 @@
  *                          with VerificationKey::verify) over a whole batch, with an exact
  *                          per-signature fallback: per-item verdicts equal mv_ed25519_verify's
  *   mv_dev_*               the same computations on device-resident buffers (HBM in, HBM out)
+ *   mv_crc32               crc32fast::hash (crc32fast 1.3.2, Cargo.lock:777), as the WAL uses it
+ *                          (mysticeti-core/src/wal.rs:173-177, :250)
+ *   mv_wal_verify          WalReader::iter_until + WalIterator::next over WalReader::try_read
+ *                          (wal.rs:226-346): the entry walk and crc check of the WAL replay in
+ *                          BlockStore::open (block_store.rs:66)
+ *   mv_wal_layout          WalWriter::writev position arithmetic (wal.rs:150-188), host only
  *
  * Conventions
  *   - The caller owns every buffer passed in and out; they must stay valid for the call.
@@ -71,6 +77,12 @@ typedef int32_t mv_status;
 #define MV_BLOCK_THRESHOLD_CLOCK 10        /* types.rs:371-374, threshold_clock.rs:12-35 */
 #define MV_BLOCK_VOTE_RANGE_TOO_LONG 11    /* end - start >= 2^20, "Include is too large ..." :447-453 */
 #define MV_BLOCK_VOTE_RANGE_END_TOO_LARGE 12 /* end >= 2^20, "offset_end_exclusive is too large ..." :454-458 */
+
+/* per-entry WAL verdicts (WalReader::try_read, wal.rs:233-261; the reference panics on all but OK) */
+#define MV_WAL_OK 0
+#define MV_WAL_CRC_MISMATCH 1     /* "Crc mismatch, expected .., found .." wal.rs:250-257 */
+#define MV_WAL_NONZERO_CRC_LEN0 2 /* "Non-zero crc at len 0" wal.rs:240-247 */
+#define MV_WAL_BAD_LENGTH 3       /* len < 16 or the entry runs past its map: Bytes::slice panics, wal.rs:249 */
 
 /* mv_config.flags */
 #define MV_FLAG_NO_BATCH 1u /* host-buffer verify: never use the batch (random linear combination) path */
@@ -137,6 +149,27 @@ mv_status mv_shard_plan(const uint64_t* weights, uint64_t n, uint32_t parts, uin
  * length, or -1 if the bytes do not deserialize. `out` may be NULL to query the length. */
 int64_t mv_block_preimage(const uint8_t* bincode, uint64_t len, uint8_t* out, uint64_t cap);
 
+/* crc32fast::hash (CRC-32/ISO-HDLC) of n byte strings buf[off[i] .. off[i]+len[i]) -> out[i]. */
+mv_status mv_crc32(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                   uint32_t* out /* n */);
+
+/* WAL replay check: iterates the WAL image wal[0 .. size) as WalReader::iter_until does up to the
+ * writer position end_pos (maps of 2^map_bits bytes: 24 in production, 16 under cfg(test),
+ * wal.rs:95-103; 8 <= map_bits <= 30), checking every entry's crc32. Entries come out in
+ * iteration order: pos[i] (WalPosition.start), tag[i], len[i] (payload bytes), status[i]
+ * (MV_WAL_*). The iteration stops after the first entry whose status is not MV_WAL_OK (where
+ * the reference panics). *count = the number of entries; only the first `cap` are written.
+ * Bytes at or past `size` read as zero (the mapping's tail past the end of the file). */
+mv_status mv_wal_verify(mv_ctx* ctx, const uint8_t* wal, uint64_t size, uint64_t end_pos, uint32_t map_bits,
+                        uint64_t* pos, uint32_t* tag, uint32_t* len, uint8_t* status, uint64_t cap,
+                        uint64_t* count);
+
+/* Host-only helper: WalWriter::writev positions of n entries of payload_len[i] bytes written from
+ * writer position `start` (an entry that would straddle a map starts at the next one); returns
+ * the writer position after them. */
+uint64_t mv_wal_layout(const uint64_t* payload_len, uint64_t n, uint32_t map_bits, uint64_t start,
+                       uint64_t* pos /* n */);
+
 /* ---- device-resident variants (inputs already in HBM of `device`) ----
  * Pointers are device pointers, 16-byte aligned; `stream` is a hipStream_t (NULL = the
  * library's stream for that device). They enqueue work and return without synchronising. */
@@ -166,6 +199,16 @@ mv_status mv_dev_verify_blocks(mv_ctx* ctx, int device, const uint8_t* d_buf, ui
                                const uint64_t* d_off, const uint64_t* d_len, uint32_t n, uint8_t* d_status,
                                uint8_t* d_msg_digest, uint8_t* d_block_digest, void* stream);
 
+/* mv_wal_verify on a WAL image already in HBM (d_wal, 4-byte aligned); outputs are device arrays
+ * of `cap` entries and *count is written on the host. Synchronises `stream` (the entry count is
+ * data-dependent: the walk's per-map counts come back to the host before the crc pass). */
+mv_status mv_dev_wal_verify(mv_ctx* ctx, int device, const uint8_t* d_wal, uint64_t size, uint64_t end_pos,
+                            uint32_t map_bits, uint64_t* d_pos, uint32_t* d_tag, uint32_t* d_len, uint8_t* d_status,
+                            uint64_t cap, uint64_t* count, void* stream);
+/* crc32fast::hash of n strings of device buffer d_buf at d_off/d_len (device arrays) -> d_out. Enqueue only. */
+mv_status mv_dev_crc32(mv_ctx* ctx, int device, const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len,
+                       uint32_t n, uint32_t* d_out, void* stream);
+
 /* ---- diagnostics (used by the test-suite) ---- */
 /* Host-buffer batch-path counters since mv_create: batches tried, batches whose combined
  * equation failed (and were re-verified signature by signature). */
@@ -181,10 +224,11 @@ mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out /* 4 */);
 mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups);
 /* Stage timing: when enabled, every call records HIP events on its stream around its
  * stages: batch path 0..5 (prep, sort, bucket, reduce, final, fallback), block pipeline
- * 6..9 (parse, hash, verify = comb/ladder verify when the batch path is not taken, verdict).
+ * 6..9 (parse, hash, verify = comb/ladder verify when the batch path is not taken, verdict),
+ * WAL replay 10..11 (walk = the per-map header walk, crc = the entry crc pass).
  * mv_stage_times waits for the recorded calls and returns the summed device ms per stage and
  * the number of calls measured per stage; reset != 0 clears the sums. */
-#define MV_NSTAGES 10
+#define MV_NSTAGES 12
 mv_status mv_set_stage_timing(mv_ctx* ctx, int enable);
 mv_status mv_stage_times(mv_ctx* ctx, double* ms /* MV_NSTAGES or NULL */, uint64_t* calls /* MV_NSTAGES or NULL */,
                          int reset);

@@ -11,6 +11,11 @@ Reference interfaces mirrored (hrubaanna/mysticeti @ 2025-02-04):
   Engine.ed25519_verify    PublicKey::verify_block -> VerificationKey::verify (crypto.rs:174-189)
   Engine.ed25519_sign      Signer::sign_block (crypto.rs:199-223)
   Engine.blake2b256        BlockHasher (crypto.rs:34)
+  Engine.crc32             crc32fast::hash as the WAL uses it (wal.rs:173-177, :250)
+  Engine.wal_verify        WalReader::iter_until / WalIterator over try_read (wal.rs:226-346)
+  Engine.wal_iter_until    the same as the reference's iterator: (pos, (tag, bytes)), raising
+                           where the reference panics
+  wal_layout               WalWriter::writev positions (wal.rs:150-188)
   crypto.*                 thin reference-named wrappers (BlockDigest, PublicKey, Signer, ...)
 """
 from __future__ import annotations
@@ -41,10 +46,14 @@ EXPORTS = [
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
     "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
-    "mv_queue_stats", "mv_shard_plan",
+    "mv_queue_stats", "mv_shard_plan", "mv_crc32", "mv_wal_verify", "mv_wal_layout", "mv_dev_wal_verify",
+    "mv_dev_crc32",
 ]
-# batch path stages, then the block pipeline's (mv_stage_times order, MV_NSTAGES)
-STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback", "parse", "hash", "verify", "verdict"]
+WAL_OK, WAL_CRC_MISMATCH, WAL_NONZERO_CRC_LEN0, WAL_BAD_LENGTH = range(4)
+WAL_MAP_BITS, WAL_MAP_BITS_TEST = 24, 16  # wal.rs:95-103
+# batch path stages, the block pipeline's, the WAL replay's (mv_stage_times order, MV_NSTAGES)
+STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback", "parse", "hash", "verify", "verdict", "wal_walk",
+          "wal_crc"]
 FLAG_NO_BATCH, FLAG_NO_COMB, FLAG_HOST_PARSE = 1, 2, 4
 BATCH_MIN = 4096
 
@@ -95,6 +104,12 @@ def load_library(path: str = LIB_PATH):
     lib.mv_selftest.argtypes = [vp, ctypes.c_int, vp, u32, vp]
     lib.mv_block_preimage.argtypes = [vp, u64, vp, u64]
     lib.mv_block_preimage.restype = ctypes.c_int64
+    lib.mv_crc32.argtypes = [vp, vp, vp, vp, u32, vp]
+    lib.mv_wal_verify.argtypes = [vp, vp, u64, u64, u32, vp, vp, vp, vp, u64, vp]
+    lib.mv_wal_layout.argtypes = [vp, u64, u32, u64, vp]
+    lib.mv_wal_layout.restype = u64
+    lib.mv_dev_wal_verify.argtypes = [vp, ctypes.c_int, vp, u64, u64, u32, vp, vp, vp, vp, u64, vp, vp]
+    lib.mv_dev_crc32.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
     for name in EXPORTS:
         getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int32
     _lib = lib
@@ -288,6 +303,81 @@ class Engine:
                                                  ctypes.c_void_p(stream_handle or None)),
                     "mv_dev_ed25519_sign")
 
+    # ---- WAL replay (wal.rs) ----
+    def crc32(self, items: Sequence[bytes]) -> np.ndarray:
+        """crc32fast::hash of every item (uint32 array)."""
+        items = [bytes(x) for x in items]
+        lens = np.array([len(x) for x in items], dtype=np.uint64)
+        offs = np.zeros(len(items), dtype=np.uint64)
+        if len(items) > 1:
+            offs[1:] = np.cumsum(lens)[:-1]
+        buf = np.frombuffer(b"".join(items) + b"\0", dtype=np.uint8)
+        return self.crc32_packed(buf, offs, lens)
+
+    def crc32_packed(self, buf: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> np.ndarray:
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        n = len(offs)
+        out = np.zeros(n, dtype=np.uint32)
+        if n:
+            self._check(self.lib.mv_crc32(self.ctx, _p(buf), _p(offs), _p(lens), n, _p(out)), "mv_crc32")
+        return out
+
+    def wal_verify(self, image, end_pos: Optional[int] = None, map_bits: int = WAL_MAP_BITS,
+                   cap: Optional[int] = None):
+        """WalReader::iter_until over a WAL image (bytes / uint8 array) up to the writer position
+        end_pos (default: its length). Returns (pos, tag, len, status) arrays of the entries in
+        iteration order, the last one failing (status != WAL_OK) where the reference panics."""
+        img = np.ascontiguousarray(np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray))
+                                   else np.asarray(image, dtype=np.uint8))
+        size = img.size
+        end = size if end_pos is None else int(end_pos)
+        if cap is None:
+            cap = size // 16 + 1
+        pos = np.zeros(max(cap, 1), dtype=np.uint64)
+        tag = np.zeros(max(cap, 1), dtype=np.uint32)
+        ln = np.zeros(max(cap, 1), dtype=np.uint32)
+        st = np.zeros(max(cap, 1), dtype=np.uint8)
+        cnt = ctypes.c_uint64(0)
+        self._check(self.lib.mv_wal_verify(self.ctx, _p(img) if size else None, size, end, map_bits, _p(pos),
+                                           _p(tag), _p(ln), _p(st), cap, ctypes.byref(cnt)), "mv_wal_verify")
+        n = min(cnt.value, cap)
+        return pos[:n], tag[:n], ln[:n], st[:n]
+
+    def wal_iter_until(self, image, end_pos: Optional[int] = None, map_bits: int = WAL_MAP_BITS):
+        """The reference's iterator (wal.rs:270-346): yields (position, (tag, payload bytes)) and
+        raises MvError with the reference's panic message where it would panic."""
+        img = bytes(image)
+        pos, tag, ln, st = self.wal_verify(img, end_pos, map_bits)
+        for p, t, n, s in zip(pos.tolist(), tag.tolist(), ln.tolist(), st.tolist()):
+            if s == WAL_CRC_MISMATCH:
+                hdr = int.from_bytes(img[p:p + 16].ljust(16, b"\0"), "little")
+                full = (hdr >> 64) & 0xFFFFFFFF
+                found = int(self.crc32([img[p + 16:p + full].ljust(full - 16, b"\0")])[0])
+                raise MvError(f"Crc mismatch, expected {hdr & ((1 << 64) - 1)}, found {found} at position {p}:{full}")
+            if s == WAL_NONZERO_CRC_LEN0:
+                crc = int.from_bytes(img[p:p + 8].ljust(8, b"\0"), "little")
+                raise MvError(f"Non-zero crc at len 0, crc: {crc}, position:{p}")
+            if s == WAL_BAD_LENGTH:
+                raise MvError(f"entry at position {p} runs outside its map (Bytes::slice out of range)")
+            yield p, (t, img[p + 16:p + 16 + n])
+
+    def dev_wal_verify(self, device: int, d_img, size: int, end_pos: int, map_bits: int, d_pos, d_tag, d_len,
+                       d_status, cap: int, stream_handle: int = 0) -> int:
+        """mv_dev_wal_verify on torch device tensors; returns the entry count."""
+        cnt = ctypes.c_uint64(0)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        self._check(self.lib.mv_dev_wal_verify(self.ctx, device, ptr(d_img), size, end_pos, map_bits, ptr(d_pos),
+                                               ptr(d_tag), ptr(d_len), ptr(d_status), cap, ctypes.byref(cnt),
+                                               ctypes.c_void_p(stream_handle or None)), "mv_dev_wal_verify")
+        return cnt.value
+
+    def dev_crc32(self, device: int, d_buf, d_off, d_len, n: int, d_out, stream_handle: int = 0):
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        self._check(self.lib.mv_dev_crc32(self.ctx, device, ptr(d_buf), ptr(d_off), ptr(d_len), n, ptr(d_out),
+                                          ctypes.c_void_p(stream_handle or None)), "mv_dev_crc32")
+
     # ---- diagnostics ----
     def selftest(self, op: int, words: np.ndarray) -> np.ndarray:
         w = np.ascontiguousarray(np.asarray(words, dtype=np.uint32)).reshape(-1, 16)
@@ -317,6 +407,16 @@ def shard_plan(weights, parts: int) -> List[int]:
     if rc != MV_OK:
         raise MvError(f"mv_shard_plan failed ({rc})")
     return [int(c) for c in cut]
+
+
+def wal_layout(payload_lens, map_bits: int = WAL_MAP_BITS, start: int = 0):
+    """Host-only: WalWriter::writev positions of entries with these payload lengths, and the
+    writer position after them."""
+    lib = load_library()
+    pl = np.ascontiguousarray(np.asarray(payload_lens, dtype=np.uint64))
+    pos = np.zeros(max(pl.size, 1), dtype=np.uint64)
+    end = lib.mv_wal_layout(_p(pl) if pl.size else None, pl.size, map_bits, start, _p(pos))
+    return pos[:pl.size], int(end)
 
 
 def version() -> str:

@@ -30,7 +30,8 @@ namespace {
 constexpr int kBlockStage0 = mvk::BATCH_STAGES;  // parse, hash, verify, verdict
 constexpr int kGuardBatches = 64;  // batches cut into sub-batch equations after a failure
 constexpr int kBlockStages = 4;
-static_assert(kBlockStage0 + kBlockStages == MV_NSTAGES, "stage count");
+constexpr int kWalStage0 = kBlockStage0 + kBlockStages;  // walk, crc
+static_assert(kWalStage0 + 2 == MV_NSTAGES, "stage count");
 
 struct DevBuf {
   void* p = nullptr;
@@ -116,6 +117,11 @@ struct Device {
   int blk_next = 0;
   HostBuf h_in, h_out;
   bool committee_loaded = false;
+  // WAL replay (wal.hip): crc tables, walk records, per-map counts / flags / offsets, entries,
+  // the image and outputs of host-buffer calls
+  DevBuf wal_tab, wal_rec, wal_mcount, wal_mflag, wal_moff, wal_ent, wal_ff, wal_img, wal_pos, wal_tag, wal_len,
+      wal_st;
+  int cus = 0;
 };
 
 struct PendingEvents {
@@ -810,7 +816,9 @@ void mv_destroy(mv_ctx* ctx) {
     for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
                       &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
                       &dev.keyok, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0], &dev.vscr[1], &dev.blk[0], &dev.blk[1],
-                      &dev.sscr[0], &dev.sscr[1]})
+                      &dev.sscr[0], &dev.sscr[1], &dev.wal_tab, &dev.wal_rec, &dev.wal_mcount, &dev.wal_mflag,
+                      &dev.wal_moff, &dev.wal_ent, &dev.wal_ff, &dev.wal_img, &dev.wal_pos, &dev.wal_tag, &dev.wal_len,
+                      &dev.wal_st})
       b->release();
     for (hipEvent_t ev : dev.slot_done)
       if (ev) (void)hipEventDestroy(ev);
@@ -1177,6 +1185,211 @@ mv_status mv_dev_ed25519_sign(mv_ctx* ctx, int device, const uint8_t* d_seed, co
   HIPCHK(ctx, hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
   HIPCHK(ctx, mvk::launch_sign(d_seed, d_msg, n, dev->btab.p, d_pk, d_sig, s));
+  return MV_OK;
+}
+
+// ---------------------------------------------------------------- WAL replay
+static mv_status wal_tables(mv_ctx* ctx, Device& dev) {
+  if (dev.wal_tab.p) return MV_OK;
+  std::vector<uint32_t> t(mvk::wal_table_words());
+  mvk::wal_build_tables(t.data());
+  HIPCHK(ctx, dev.wal_tab.ensure(4 * t.size()));
+  HIPCHK(ctx, hipMemcpy(dev.wal_tab.p, t.data(), 4 * t.size(), hipMemcpyHostToDevice));
+  if (!dev.cus) HIPCHK(ctx, hipDeviceGetAttribute(&dev.cus, hipDeviceAttributeMultiprocessorCount, dev.id));
+  return MV_OK;
+}
+
+// Walk (one lane per map), join the maps in iteration order on the host, compact, crc pass.
+static mv_status wal_run(mv_ctx* ctx, Device& dev, const uint8_t* d_img, uint64_t size, uint64_t end_pos,
+                         uint32_t map_bits, uint64_t* d_pos, uint32_t* d_tag, uint32_t* d_len, uint8_t* d_status,
+                         uint64_t cap, uint64_t* count, hipStream_t s) {
+  *count = 0;
+  mv_status st = wal_tables(ctx, dev);
+  if (st != MV_OK) return st;
+  const uint64_t msize = 1ull << map_bits, lim = std::min(size, end_pos);
+  const uint64_t nmaps64 = (lim + msize - 1) >> map_bits;
+  if (nmaps64 == 0) return MV_OK;
+  if (nmaps64 > 0xffffffffull) return set_err(ctx, MV_E_INVALID_ARG, "too many maps");
+  const uint32_t nmaps = (uint32_t)nmaps64;
+  uint32_t cap_pm = (uint32_t)std::min<uint64_t>(msize / 16, 4096);
+  std::vector<uint32_t> mcount(nmaps);
+  std::vector<uint8_t> mflag(nmaps);
+  uint32_t nincl = 0;
+  uint64_t total = 0;
+  std::vector<hipEvent_t> ew, ec;  // stage timing: walk, crc
+  if ((st = make_events(ctx, 1, ew)) != MV_OK || (st = make_events(ctx, 1, ec)) != MV_OK) return st;
+  auto mark = [&](std::vector<hipEvent_t>& e, int i) -> hipError_t {
+    return e.empty() ? hipSuccess : hipEventRecord(e[i], s);
+  };
+  for (;;) {
+    HIPCHK(ctx, dev.wal_rec.ensure(8 * (size_t)nmaps * cap_pm));
+    HIPCHK(ctx, dev.wal_mcount.ensure(4 * (size_t)nmaps));
+    HIPCHK(ctx, dev.wal_mflag.ensure(nmaps));
+    HIPCHK(ctx, mark(ew, 0));
+    HIPCHK(ctx, mvk::launch_wal_walk(d_img, size, end_pos, map_bits, nmaps, cap_pm, dev.wal_rec.as<unsigned long long>(),
+                                     dev.wal_mcount.as<uint32_t>(), dev.wal_mflag.as<uint8_t>(), s));
+    HIPCHK(ctx, mark(ew, 1));
+    HIPCHK(ctx, hipMemcpyAsync(mcount.data(), dev.wal_mcount.p, 4 * (size_t)nmaps, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipMemcpyAsync(mflag.data(), dev.wal_mflag.p, nmaps, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    // WalIterator order: map after map while each one hands over to the next
+    nincl = 0;
+    total = 0;
+    uint32_t maxc = 0;
+    for (uint32_t m = 0; m < nmaps; m++) {
+      if (mflag[m] == mvk::WAL_MAP_EMPTY) break;
+      nincl = m + 1;
+      total += mcount[m];
+      maxc = std::max(maxc, mcount[m]);
+      if (mflag[m] != mvk::WAL_MAP_NEXT) break;
+    }
+    if (maxc <= cap_pm) break;
+    cap_pm = maxc;  // a map held more entries than the first guess: walk again with room for them
+  }
+  keep_events(ctx, dev.id, kWalStage0, ew);
+  if (total == 0) {
+    for (hipEvent_t e : ec) (void)hipEventDestroy(e);
+    return MV_OK;
+  }
+  std::vector<uint64_t> moff(nincl);
+  for (uint64_t m = 0, o = 0; m < nincl; m++) {
+    moff[m] = o;
+    o += mcount[m];
+  }
+  HIPCHK(ctx, dev.wal_moff.ensure(8 * (size_t)nincl));
+  HIPCHK(ctx, dev.wal_ent.ensure(8 * total));
+  HIPCHK(ctx, dev.wal_ff.ensure(8));
+  HIPCHK(ctx, hipMemcpyAsync(dev.wal_moff.p, moff.data(), 8 * (size_t)nincl, hipMemcpyHostToDevice, s));
+  HIPCHK(ctx, mvk::launch_wal_compact(dev.wal_rec.as<unsigned long long>(), cap_pm, dev.wal_mcount.as<uint32_t>(),
+                                      dev.wal_moff.as<uint64_t>(), nincl, dev.wal_ent.as<unsigned long long>(), s));
+  HIPCHK(ctx, hipMemsetAsync(dev.wal_ff.p, 0xff, 8, s));
+  HIPCHK(ctx, mark(ec, 0));
+  HIPCHK(ctx, mvk::launch_wal_crc(d_img, size, dev.wal_ent.as<unsigned long long>(), total, dev.wal_tab.as<uint32_t>(),
+                                  d_pos, d_tag, d_len, d_status, cap, dev.wal_ff.as<unsigned long long>(), dev.cus, s));
+  HIPCHK(ctx, mark(ec, 1));
+  keep_events(ctx, dev.id, kWalStage0 + 1, ec);
+  uint64_t ff = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&ff, dev.wal_ff.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipStreamSynchronize(s));
+  *count = ff < total ? ff + 1 : total;
+  return MV_OK;
+}
+
+static bool wal_args_ok(uint32_t map_bits) { return map_bits >= 8 && map_bits <= 30; }
+
+mv_status mv_wal_verify(mv_ctx* ctx, const uint8_t* wal, uint64_t size, uint64_t end_pos, uint32_t map_bits,
+                        uint64_t* pos, uint32_t* tag, uint32_t* len, uint8_t* status, uint64_t cap,
+                        uint64_t* count) {
+  if (!ctx || !count || (size && !wal) || (cap && (!pos || !tag || !len || !status)) || !wal_args_ok(map_bits))
+    return set_err(ctx, MV_E_INVALID_ARG, "bad wal args");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  Device& dev = ctx->devs[0];  // one image, one device
+  HIPCHK(ctx, hipSetDevice(dev.id));
+  hipStream_t s = dev.stream;
+  HIPCHK(ctx, dev.wal_img.ensure(size + 16));
+  if (size) HIPCHK(ctx, hipMemcpyAsync(dev.wal_img.p, wal, size, hipMemcpyHostToDevice, s));
+  // outputs: device arrays of up to cap entries; the walk bounds the entry count by size / 16
+  const uint64_t ocap = std::min<uint64_t>(cap, size / 16 + 1);
+  HIPCHK(ctx, dev.wal_pos.ensure(8 * ocap + 8));
+  HIPCHK(ctx, dev.wal_tag.ensure(4 * ocap + 4));
+  HIPCHK(ctx, dev.wal_len.ensure(4 * ocap + 4));
+  HIPCHK(ctx, dev.wal_st.ensure(ocap + 1));
+  uint64_t n = 0;
+  mv_status st = wal_run(ctx, dev, dev.wal_img.as<uint8_t>(), size, end_pos, map_bits, dev.wal_pos.as<uint64_t>(),
+                         dev.wal_tag.as<uint32_t>(), dev.wal_len.as<uint32_t>(), dev.wal_st.as<uint8_t>(), ocap, &n, s);
+  if (st != MV_OK) return st;
+  const uint64_t w = std::min(n, ocap);
+  if (w) {
+    HIPCHK(ctx, hipMemcpyAsync(pos, dev.wal_pos.p, 8 * w, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipMemcpyAsync(tag, dev.wal_tag.p, 4 * w, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipMemcpyAsync(len, dev.wal_len.p, 4 * w, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipMemcpyAsync(status, dev.wal_st.p, w, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+  }
+  *count = n;
+  return MV_OK;
+}
+
+mv_status mv_dev_wal_verify(mv_ctx* ctx, int device, const uint8_t* d_wal, uint64_t size, uint64_t end_pos,
+                            uint32_t map_bits, uint64_t* d_pos, uint32_t* d_tag, uint32_t* d_len, uint8_t* d_status,
+                            uint64_t cap, uint64_t* count, void* stream) {
+  if (!ctx || !count || (size && !d_wal) || (cap && (!d_pos || !d_tag || !d_len || !d_status)) ||
+      !wal_args_ok(map_bits))
+    return set_err(ctx, MV_E_INVALID_ARG, "bad wal args");
+  if (((uintptr_t)d_wal) & 3) return set_err(ctx, MV_E_INVALID_ARG, "d_wal must be 4-byte aligned");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  Device* dev = find_dev(ctx, device);
+  if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
+  HIPCHK(ctx, hipSetDevice(dev->id));
+  hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
+  return wal_run(ctx, *dev, d_wal, size, end_pos, map_bits, d_pos, d_tag, d_len, d_status, cap, count, s);
+}
+
+uint64_t mv_wal_layout(const uint64_t* payload_len, uint64_t n, uint32_t map_bits, uint64_t start, uint64_t* pos) {
+  if (!wal_args_ok(map_bits) || (n && (!payload_len || !pos))) return start;
+  const uint64_t mask = ~((1ull << map_bits) - 1);
+  uint64_t p = start;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t len = payload_len[i] + 16;  // header + payload (wal.rs:152)
+    if ((p & mask) != ((p + len - 1) & mask)) p = (p + len - 1) & mask;  // zero padding (wal.rs:163-167)
+    pos[i] = p;
+    p += len;
+  }
+  return p;
+}
+
+mv_status mv_crc32(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                   uint32_t* out) {
+  if (!ctx || (n && (!buf || !off || !len || !out))) return set_err(ctx, MV_E_INVALID_ARG, "bad crc32 args");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
+    HIPCHK(ctx, hipSetDevice(dev.id));
+    mv_status st = wal_tables(ctx, dev);
+    if (st != MV_OK) return st;
+    uint64_t i = lo;
+    while (i < hi) {
+      uint64_t j = i, bytes = 0;  // chunks of <= max_batch strings and <= 1 GiB
+      while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += len[j++];
+      const uint32_t m = (uint32_t)(j - i);
+      HIPCHK(ctx, dev.h_in.ensure(bytes + 16));
+      uint8_t* stg = dev.h_in.as<uint8_t>();
+      std::vector<uint64_t> soff(m), slen(m);
+      uint64_t p = 0;
+      for (uint32_t k = 0; k < m; k++) {
+        soff[k] = p;
+        slen[k] = len[i + k];
+        memcpy(stg + p, buf + off[i + k], slen[k]);
+        p += slen[k];
+      }
+      HIPCHK(ctx, dev.bytes.ensure(p + 16));
+      HIPCHK(ctx, dev.off.ensure(8 * (size_t)m));
+      HIPCHK(ctx, dev.len.ensure(8 * (size_t)m));
+      HIPCHK(ctx, dev.out2.ensure(4 * (size_t)m));
+      if (p) HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, stg, p, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(dev.off.p, soff.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(dev.len.p, slen.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
+      HIPCHK(ctx, mvk::launch_crc32(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
+                                    dev.wal_tab.as<uint32_t>(), dev.out2.as<uint32_t>(), dev.cus, dev.stream));
+      HIPCHK(ctx, hipMemcpyAsync(out + i, dev.out2.p, 4 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
+      HIPCHK(ctx, hipStreamSynchronize(dev.stream));
+      i = j;
+    }
+    return MV_OK;
+  });
+}
+
+mv_status mv_dev_crc32(mv_ctx* ctx, int device, const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len,
+                       uint32_t n, uint32_t* d_out, void* stream) {
+  if (!ctx || (n && (!d_buf || !d_off || !d_len || !d_out))) return set_err(ctx, MV_E_INVALID_ARG, "bad args");
+  if (((uintptr_t)d_buf) & 3) return set_err(ctx, MV_E_INVALID_ARG, "d_buf must be 4-byte aligned");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  Device* dev = find_dev(ctx, device);
+  if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
+  HIPCHK(ctx, hipSetDevice(dev->id));
+  mv_status st = wal_tables(ctx, *dev);
+  if (st != MV_OK) return st;
+  hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
+  HIPCHK(ctx, mvk::launch_crc32(d_buf, d_off, d_len, n, dev->wal_tab.as<uint32_t>(), d_out, dev->cus, s));
   return MV_OK;
 }
 

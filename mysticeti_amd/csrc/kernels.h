@@ -70,4 +70,22 @@ hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* diges
 // status in the types.rs order; zeroes both digests of blocks that do not deserialize
 hipError_t launch_block_verdict(const uint32_t* facts, const uint8_t* claimed, uint8_t* msg_digest, uint8_t* digest,
                                 const uint8_t* sig_status, uint32_t n, uint8_t* status, hipStream_t s);
+// wal.hip: crc32fast::hash on the GPU and the WAL replay walk. `tables`
+// (wal_table_words() words, built by wal_build_tables on the host) stay resident per device.
+// cus = compute units (sizes the persistent crc grids).
+size_t wal_table_words();
+void wal_build_tables(uint32_t* out);
+hipError_t launch_crc32(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                        const uint32_t* tables, uint32_t* out, int cus, hipStream_t s);
+// one lane per map: records (position | walk status << 60) of map m at rec[m * cap_pm ..], the
+// record count (may exceed cap_pm: nothing past it is stored) and how the iteration leaves the map
+constexpr uint8_t WAL_MAP_EMPTY = 0, WAL_MAP_NEXT = 1, WAL_MAP_END = 2, WAL_MAP_BAD = 3;
+hipError_t launch_wal_walk(const uint8_t* img, uint64_t size, uint64_t end_pos, uint32_t map_bits, uint32_t nmaps,
+                           uint32_t cap_pm, unsigned long long* rec, uint32_t* mcount, uint8_t* mflag, hipStream_t s);
+hipError_t launch_wal_compact(const unsigned long long* rec, uint32_t cap_pm, const uint32_t* mcount,
+                              const uint64_t* moff, uint32_t nmaps, unsigned long long* ent, hipStream_t s);
+// one wave per entry: header, payload crc, verdict (MV_WAL_*); *first_fail = min failing index
+hipError_t launch_wal_crc(const uint8_t* img, uint64_t size, const unsigned long long* ent, uint64_t total,
+                          const uint32_t* tables, uint64_t* out_pos, uint32_t* out_tag, uint32_t* out_len,
+                          uint8_t* out_status, uint64_t cap, unsigned long long* first_fail, int cus, hipStream_t s);
 }  // namespace mvk

@@ -86,6 +86,22 @@ void orc_block_verify_batch(const uint8_t* buf, const uint64_t* off, const uint6
                             const uint8_t* committee_pks, const uint64_t* stakes, uint32_t n_auth, uint64_t epoch,
                             uint8_t* status, uint8_t* msg_digests, uint8_t* block_digests, int threads);
 
+/* ---- WAL replay check (wal.c) ---- */
+enum { ORC_WAL_OK = 0, ORC_WAL_CRC_MISMATCH = 1, ORC_WAL_NONZERO_CRC_LEN0 = 2, ORC_WAL_BAD_LENGTH = 3 };
+/* crc32fast::hash (CRC-32/ISO-HDLC): orc_crc32 folds with PCLMULQDQ where the CPU has it (as
+ * crc32fast does on x86_64), orc_crc32_table is the byte-at-a-time table form */
+uint32_t orc_crc32(const uint8_t* p, size_t n);
+uint32_t orc_crc32_table(const uint8_t* p, size_t n);
+void orc_crc32_batch(const uint8_t* buf, const uint64_t* off, const uint64_t* len, size_t n, uint32_t* out);
+/* WalWriter::writev positions of n entries of payload_len bytes from writer position `start`;
+ * returns the writer position after them. */
+uint64_t orc_wal_layout(const uint64_t* payload_len, size_t n, uint32_t map_bits, uint64_t start, uint64_t* pos);
+/* WalReader::iter_until over img[0, size) up to end_pos: entries (position, tag, payload length,
+ * ORC_WAL_* status) in order, stopping after the first failing one; returns the entry count
+ * (entries past cap are counted, not written). */
+uint64_t orc_wal_iter(const uint8_t* img, uint64_t size, uint64_t end_pos, uint32_t map_bits, uint64_t* pos,
+                      uint32_t* tag, uint32_t* len, uint8_t* status, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

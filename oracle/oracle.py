@@ -57,6 +57,16 @@ def lib():
         _lib.orc_block_verify.restype = ctypes.c_int
         _lib.orc_block_verify_batch.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_uint32,
                                                 ctypes.c_uint64, u8p, u8p, u8p, ctypes.c_int]
+        _lib.orc_crc32.argtypes = [u8p, ctypes.c_size_t]
+        _lib.orc_crc32.restype = ctypes.c_uint32
+        _lib.orc_crc32_table.argtypes = [u8p, ctypes.c_size_t]
+        _lib.orc_crc32_table.restype = ctypes.c_uint32
+        _lib.orc_crc32_batch.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p]
+        _lib.orc_wal_layout.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, u8p]
+        _lib.orc_wal_layout.restype = ctypes.c_uint64
+        _lib.orc_wal_iter.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p, u8p, u8p, u8p,
+                                      ctypes.c_uint64]
+        _lib.orc_wal_iter.restype = ctypes.c_uint64
     return _lib
 
 
@@ -155,3 +165,51 @@ def block_verify_batch(buf: np.ndarray, off: np.ndarray, lens: np.ndarray, pks: 
     lib().orc_block_verify_batch(_ptr(buf), _ptr(off), _ptr(lens), n, _ptr(pks), _ptr(stakes), pks.shape[0], epoch,
                                  _ptr(status), _ptr(md), _ptr(bd), threads)
     return status, md, bd
+
+
+WAL_OK, WAL_CRC_MISMATCH, WAL_NONZERO_CRC_LEN0, WAL_BAD_LENGTH = range(4)
+
+
+def crc32(data: bytes) -> int:
+    """crc32fast::hash (oracle/wal.c)."""
+    b = np.frombuffer(bytes(data) or b"\0", dtype=np.uint8)
+    return int(lib().orc_crc32(_ptr(b), len(data)))
+
+
+def crc32_table(data: bytes) -> int:
+    """The byte-at-a-time table form (oracle/wal.c), to cross-check the folded one."""
+    b = np.frombuffer(bytes(data) or b"\0", dtype=np.uint8)
+    return int(lib().orc_crc32_table(_ptr(b), len(data)))
+
+
+def crc32_batch(buf: np.ndarray, off: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    out = np.zeros(len(off), dtype=np.uint32)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    lib().orc_crc32_batch(_ptr(buf), _ptr(off), _ptr(lens), len(off), _ptr(out))
+    return out
+
+
+def wal_layout(payload_len, map_bits: int, start: int = 0):
+    """WalWriter::writev positions (oracle/wal.c) -> (positions, writer position after)."""
+    pl = np.ascontiguousarray(payload_len, dtype=np.uint64)
+    pos = np.zeros(max(len(pl), 1), dtype=np.uint64)
+    end = lib().orc_wal_layout(_ptr(pl), len(pl), map_bits, start, _ptr(pos))
+    return pos[:len(pl)], int(end)
+
+
+def wal_iter(img: np.ndarray, end_pos: int, map_bits: int, cap: int | None = None):
+    """WalReader::iter_until (oracle/wal.c) -> (pos, tag, len, status) arrays of the entries read,
+    the last one failing if the reference would panic there."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    if cap is None:
+        cap = len(img) // 16 + 2
+    pos = np.zeros(cap, dtype=np.uint64)
+    tag = np.zeros(cap, dtype=np.uint32)
+    ln = np.zeros(cap, dtype=np.uint32)
+    st = np.zeros(cap, dtype=np.uint8)
+    n = lib().orc_wal_iter(_ptr(img) if len(img) else None, len(img), end_pos, map_bits, _ptr(pos), _ptr(tag),
+                           _ptr(ln), _ptr(st), cap)
+    n = min(int(n), cap)
+    return pos[:n], tag[:n], ln[:n], st[:n]
