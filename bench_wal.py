@@ -83,7 +83,7 @@ def wal_measure(eng, torch, local_rank, world, dist, n: int, steps: int, warmup:
 
     dev = torch.device("cuda", local_rank)
     base = MB.config4(eng, rounds=41)  # 4,100 distinct config-4 blocks (signed on the GPU)
-    payloads = [b.bincode() for b in base]
+    payloads = [bytes(b) for b in base]
     t0 = time.perf_counter()
     img, pos, lens, end = build_image(payloads, n, map_bits)
     build_s = time.perf_counter() - t0

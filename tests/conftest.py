@@ -8,6 +8,19 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))  # tests use the oracle as the checker
 
 
+def pytest_sessionstart(session):
+    # torch ships its own HIP runtime, and it must see the device before libmysti_verify.so's
+    # runtime is loaded (a CPU test that loads the library first would leave torch -- and then
+    # mv_create -- without devices): on a GPU box, initialise torch before any test runs
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built HIP library")
     config.addinivalue_line("markers", "slow: large-batch case")
