@@ -122,6 +122,14 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg /* n x 32 */, const 
                             const uint8_t* pk /* n x 32 or NULL */, const uint32_t* key_idx /* n or NULL */,
                             uint32_t n, uint8_t* status /* n, MV_SIG_* */);
 
+/* Page-locked host memory for verify inputs (hipHostMalloc, portable across the context's
+ * devices). mv_ed25519_verify on inputs that are pinned (these, or any hipHostMalloc /
+ * hipHostRegister memory) streams them in chunks whose H2D copies run beside the verification
+ * of the previous chunk, instead of one pageable copy before the whole batch. Free with
+ * mv_host_free. The Rust caller would receive network payloads into such buffers. */
+mv_status mv_host_alloc(mv_ctx* ctx, uint64_t bytes, void** out);
+void mv_host_free(mv_ctx* ctx, void* p);
+
 /* RFC 8032 signing of n 32-byte messages with n 32-byte seeds -> pk (n x 32), sig (n x 64). */
 mv_status mv_ed25519_sign(mv_ctx* ctx, const uint8_t* seed, const uint8_t* msg, uint32_t n, uint8_t* pk,
                           uint8_t* sig);

@@ -47,7 +47,7 @@ EXPORTS = [
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
     "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
     "mv_queue_stats", "mv_shard_plan", "mv_crc32", "mv_wal_verify", "mv_wal_layout", "mv_dev_wal_verify",
-    "mv_dev_crc32",
+    "mv_dev_crc32", "mv_host_alloc", "mv_host_free",
 ]
 WAL_OK, WAL_CRC_MISMATCH, WAL_NONZERO_CRC_LEN0, WAL_BAD_LENGTH = range(4)
 WAL_MAP_BITS, WAL_MAP_BITS_TEST = 24, 16  # wal.rs:95-103
@@ -110,6 +110,9 @@ def load_library(path: str = LIB_PATH):
     lib.mv_wal_layout.restype = u64
     lib.mv_dev_wal_verify.argtypes = [vp, ctypes.c_int, vp, u64, u64, u32, vp, vp, vp, vp, u64, vp, vp]
     lib.mv_dev_crc32.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
+    lib.mv_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
+    lib.mv_host_free.argtypes = [vp, vp]
+    lib.mv_host_free.restype = None
     for name in EXPORTS:
         getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int32
     _lib = lib
@@ -150,8 +153,23 @@ class Engine:
 
     def close(self):
         if getattr(self, "ctx", None):
+            for ptr in getattr(self, "_pinned", {}).values():
+                self.lib.mv_host_free(self.ctx, ptr)
+            self._pinned = {}
             self.lib.mv_destroy(self.ctx)
             self.ctx = None
+
+    def host_empty(self, shape, dtype=np.uint8) -> np.ndarray:
+        """A numpy array in page-locked host memory (mv_host_alloc), valid until close(): verify
+        inputs held in such arrays are streamed to the GPU beside the verification."""
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        ptr = ctypes.c_void_p()
+        self._check(self.lib.mv_host_alloc(self.ctx, max(nbytes, 1), ctypes.byref(ptr)), "mv_host_alloc")
+        if not hasattr(self, "_pinned"):
+            self._pinned = {}
+        self._pinned[ptr.value] = ptr
+        raw = (ctypes.c_uint8 * max(nbytes, 1)).from_address(ptr.value)
+        return np.frombuffer(raw, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
 
     def __del__(self):
         try:

@@ -658,14 +658,27 @@ void par_memcpy(void* dst, const void* src, size_t bytes, unsigned threads) {
   for (auto& t : th) t.join();
 }
 
-// mv_ed25519_verify's batch path over [lo, hi) of the caller's (pageable) arrays, in chunks
-// of >= 8 x MV_BATCH_MIN signatures, three stages deep: the host packs chunk c + 1 into
-// pinned staging (several threads; pageable H2D copies run at a fraction of PCIe) while the
-// device copies chunk c in from pinned memory and verifies it on compute stream c % 2
-// (double-buffered device inputs, stream-ordered reuse); statuses return by one D2H per
-// chunk into pinned staging. pk rows by item, or committee keys by key_idx.
+// True if p is page-locked host memory the DMA engines can read directly (mv_host_alloc,
+// hipHostMalloc, hipHostRegister, torch pin_memory).
+bool host_pinned(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: the query fails; do not leave the error set
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// mv_ed25519_verify's batch path over [lo, hi) of the caller's arrays, in chunks of
+// >= MV_BATCH_MIN signatures on two streams, so the H2D copy of chunk c + 1 runs beside the
+// verification of chunk c (double-buffered device inputs, stream-ordered reuse); statuses
+// return by one D2H per chunk into pinned staging. pk rows by item, or committee keys by
+// key_idx. direct = true: the DMA engines read the caller's arrays themselves (pinned inputs,
+// or MV_PIPELINE=2 on pageable ones); false: the host first packs chunk c + 1 into pinned
+// staging with several threads (MV_PIPELINE=1, pageable inputs).
 mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
-                                const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status) {
+                                const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status, bool direct) {
   const uint64_t m = hi - lo;
   static const int chunk_log2 = [] {  // MV_PIPE_CHUNK_LOG2 (experiments): signatures per chunk
     const char* e = getenv("MV_PIPE_CHUNK_LOG2");
@@ -684,7 +697,7 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
     HIPCHK(ctx, dev.pin_sig[k].ensure(64 * cs));
     HIPCHK(ctx, dev.pin_pk[k].ensure((pk ? 32 : 4) * cs));
     HIPCHK(ctx, dev.pin_st[k].ensure(cs));
-    HIPCHK(ctx, dev.h_stage[k].ensure(rowb * cs));
+    if (!direct) HIPCHK(ctx, dev.h_stage[k].ensure(rowb * cs));
   }
   HIPCHK(ctx, dev.h_out.ensure(m));
   uint8_t* hst = dev.h_out.as<uint8_t>();
@@ -708,16 +721,22 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
     const double ta = now();
     if (staged_used[b]) HIPCHK(ctx, hipEventSynchronize(dev.pin_free[b]));
     const double tb = now();
-    uint8_t* hs = dev.h_stage[b].as<uint8_t>();
-    par_memcpy(hs, msg + 32 * i, 32 * (size_t)k, threads);
-    par_memcpy(hs + 32 * cs, sig + 64 * i, 64 * (size_t)k, threads);
-    if (pk) par_memcpy(hs + 96 * cs, pk + 32 * i, 32 * (size_t)k, threads);
-    else par_memcpy(hs + 96 * cs, key_idx + i, 4 * (size_t)k, threads);
-    HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, hs, 32 * (size_t)k, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, hs + 32 * cs, 64 * (size_t)k, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, hs + 96 * cs, (pk ? 32 : 4) * (size_t)k, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipEventRecord(dev.pin_free[b], st));
-    staged_used[b] = true;
+    const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);
+    if (direct) {
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, msg + 32 * i, 32 * (size_t)k, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, sig + 64 * i, 64 * (size_t)k, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, src_pk, (pk ? 32 : 4) * (size_t)k, hipMemcpyHostToDevice, st));
+    } else {
+      uint8_t* hs = dev.h_stage[b].as<uint8_t>();
+      par_memcpy(hs, msg + 32 * i, 32 * (size_t)k, threads);
+      par_memcpy(hs + 32 * cs, sig + 64 * i, 64 * (size_t)k, threads);
+      par_memcpy(hs + 96 * cs, src_pk, (pk ? 32 : 4) * (size_t)k, threads);
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, hs, 32 * (size_t)k, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, hs + 32 * cs, 64 * (size_t)k, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, hs + 96 * cs, (pk ? 32 : 4) * (size_t)k, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipEventRecord(dev.pin_free[b], st));
+      staged_used[b] = true;
+    }
     mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dpk_com,
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), st,
@@ -740,6 +759,24 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
 extern "C" {
 
 const char* mv_version(void) { return "mysti_verify 0.2 gfx950"; }
+
+mv_status mv_host_alloc(mv_ctx* ctx, uint64_t bytes, void** out) {
+  if (!ctx || !out) return set_err(ctx, MV_E_INVALID_ARG, "bad host_alloc args");
+  *out = nullptr;
+  if (bytes == 0) return MV_OK;
+  HIPCHK(ctx, hipSetDevice(ctx->devs[0].id));
+  if (hipHostMalloc(out, bytes, hipHostMallocPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return set_err(ctx, MV_E_ALLOC, "hipHostMalloc failed");
+  }
+  return MV_OK;
+}
+
+void mv_host_free(mv_ctx* ctx, void* p) {
+  (void)ctx;
+  if (p) (void)hipHostFree(p);
+}
 
 int64_t mv_block_preimage(const uint8_t* bincode, uint64_t len, uint8_t* out, uint64_t cap) {
   if (!bincode && len) return -1;
@@ -933,6 +970,7 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
     for (uint32_t i = 0; i < n; i++)
       if (key_idx[i] >= ctx->committee.size()) return set_err(ctx, MV_E_INVALID_ARG, "key_idx out of range");
   }
+  const bool pinned = n && host_pinned(msg) && host_pinned(sig) && host_pinned(pk ? (const void*)pk : key_idx);
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
     // large host-buffer batches, chunked with the copies of one chunk beside the verification
@@ -941,9 +979,12 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
     // 2^18..2^20-signature chunks and 8 or 16 staging threads): host memcpy into pinned
     // staging runs at ~10 GB/s per thread, and chunks below 2^20 cost the batch path's
     // fixed per-batch work
-    static const bool pipeline = getenv("MV_PIPELINE") && getenv("MV_PIPELINE")[0] == '1';
-    if (pipeline && !(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN)
-      return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
+    // Pinned inputs (mv_host_alloc) always take the chunked pipeline with direct DMA reads.
+    static const int pipeline = getenv("MV_PIPELINE") ? atoi(getenv("MV_PIPELINE")) : 0;
+    if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN) {
+      if (pinned) return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, true);
+      if (pipeline) return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, pipeline == 2);
+    }
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {
       uint32_t m = (uint32_t)std::min<uint64_t>(ctx->max_batch, hi - i);
       HIPCHK(ctx, dev.msg.ensure(32 * (size_t)m));

@@ -244,11 +244,12 @@ def test_adaptive_guard_after_a_failed_batch():
         assert (st == 0).all() and d == (1, 0, 8, 0)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("committee", [False, True])
-def test_pipelined_host_batches(engine, committee):
-    """Large host-buffer calls (here through the default direct path, and through the
-    opt-in chunked copy/compute pipeline in test_pipeline_opt_in): ragged sizes, committee-key
-    rows and bad signatures far apart keep exact verdicts."""
+def test_pipelined_host_batches(engine, committee, pinned):
+    """Large host-buffer calls, through the default direct path (pageable arrays) and through
+    the chunked copy-beside-verify pipeline that pinned inputs (mv_host_alloc) take: ragged
+    sizes, committee-key rows and bad signatures far apart keep exact verdicts."""
     rng = np.random.default_rng(41 + committee)
     n = 9 * M.BATCH_MIN + 333
     msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
@@ -262,5 +263,13 @@ def test_pipelined_host_batches(engine, committee):
     sig = sig.copy()
     bad = [3, n // 3, n - 2]
     sig[bad, 45] ^= 0x20
+    if pinned:
+        def pin(a):
+            h = engine.host_empty(a.shape, a.dtype)
+            h[...] = a
+            return h
+        msg, sig, pk = pin(msg), pin(sig), pin(pk)
+        if committee:
+            ki = pin(ki)
     st = engine.ed25519_verify(msg, sig, key_idx=ki) if committee else engine.ed25519_verify(msg, sig, pk)
     assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
