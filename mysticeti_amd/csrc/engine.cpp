@@ -93,27 +93,27 @@ struct Device {
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
   DevBuf committee_pk, stakes, combA, keyok;
-  // scratch rings: consecutive calls alternate between two slots, so a call on one stream
-  // can run while the previous one (on another stream) finishes its latency-bound tail; an
+  // scratch rings: consecutive calls rotate over kSlots slots, so a call on one stream can
+  // run while the previous ones (on other streams) finish their latency-bound tails; an
   // event per slot orders reuse across streams. Batch path: bscr/vscr; blocks: blk.
-  static constexpr int kSlots = 2;
+  static constexpr int kSlots = 3;
   static constexpr int kFlagWords = 1 + mvk::BATCH_MAX_GROUPS;
   DevBuf bscr[kSlots], vscr[kSlots];
-  hipEvent_t slot_done[kSlots] = {nullptr, nullptr};
-  bool slot_used[kSlots] = {false, false};
+  hipEvent_t slot_done[kSlots] = {};
+  bool slot_used[kSlots] = {};
   int next_slot = 0;
   // the batch flags of each slot's last call, copied to pinned host words behind it; read
   // (without blocking) once slot_done has completed: flag_groups[slot] groups pending
   uint32_t* h_flags = nullptr;  // kSlots x kFlagWords, pinned
-  uint32_t flag_groups[kSlots] = {0, 0};
-  // single-verify scratch (k_verify's per-wave tables), same two-slot ring
+  uint32_t flag_groups[kSlots] = {};
+  // single-verify scratch (k_verify's per-wave tables), same ring
   DevBuf sscr[kSlots];
-  hipEvent_t sscr_done[kSlots] = {nullptr, nullptr};
-  bool sscr_used[kSlots] = {false, false};
+  hipEvent_t sscr_done[kSlots] = {};
+  bool sscr_used[kSlots] = {};
   int sscr_next = 0;
   DevBuf blk[kSlots];
-  hipEvent_t blk_done[kSlots] = {nullptr, nullptr};
-  bool blk_used[kSlots] = {false, false};
+  hipEvent_t blk_done[kSlots] = {};
+  bool blk_used[kSlots] = {};
   int blk_next = 0;
   HostBuf h_in, h_out;
   bool committee_loaded = false;
@@ -852,11 +852,12 @@ void mv_destroy(mv_ctx* ctx) {
     (void)hipDeviceSynchronize();  // device-API calls may have run on the caller's streams
     for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
                       &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
-                      &dev.keyok, &dev.bscr[0], &dev.bscr[1], &dev.vscr[0], &dev.vscr[1], &dev.blk[0], &dev.blk[1],
-                      &dev.sscr[0], &dev.sscr[1], &dev.wal_tab, &dev.wal_rec, &dev.wal_mcount, &dev.wal_mflag,
+                      &dev.keyok, &dev.wal_tab, &dev.wal_rec, &dev.wal_mcount, &dev.wal_mflag,
                       &dev.wal_moff, &dev.wal_ent, &dev.wal_ff, &dev.wal_img, &dev.wal_pos, &dev.wal_tag, &dev.wal_len,
                       &dev.wal_st})
       b->release();
+    for (int k = 0; k < Device::kSlots; k++)
+      for (DevBuf* b : {&dev.bscr[k], &dev.vscr[k], &dev.blk[k], &dev.sscr[k]}) b->release();
     for (hipEvent_t ev : dev.slot_done)
       if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.sscr_done)
