@@ -40,6 +40,10 @@ constexpr int S_WORDS = S_LEVELS * 4 * 256;  // [k][byte t][value e]
 constexpr int T_WORDS = 256;                 // the byte table (1-byte shift), global only
 constexpr uint32_t PREFIX = 0x9226f562u;     // crc_raw(0, PREFIX as 4 LE bytes) = 0xFFFFFFFF
 constexpr int WG = 1024;                     // threads per crc workgroup
+#ifndef MV_WAL_ROWS
+#define MV_WAL_ROWS 8
+#endif
+constexpr int WAL_ROWS = MV_WAL_ROWS;        // 256-B rows in flight per wave
 
 // a wave-uniform 64-bit value from lane 0
 MV_DEV uint64_t bcast64(uint64_t x) {
@@ -98,18 +102,19 @@ MV_DEV uint32_t crc_raw_wave(const uint8_t* __restrict__ base, uint64_t a, uint6
     }
     u = adv256(L, u, c) ^ w;
   }
-  // rows 2 .. R-1: whole rows of D, four in flight
+  // rows 2 .. R-1: whole rows of D, WAL_ROWS in flight (the kernel is bound by HBM latency:
+  // ~1 us per round trip, so each lane keeps several rows' loads outstanding)
   uint64_t j = jm;
   const uint8_t* pr = base + (int64_t)b - 256 * (int64_t)(R - j) + 4 * (int64_t)lane - sh;
-  for (; j + 4 <= R; j += 4, pr += 1024) {
-    uint32_t A[4], B[4];
+  for (; j + WAL_ROWS <= R; j += WAL_ROWS, pr += 256 * WAL_ROWS) {
+    uint32_t A[WAL_ROWS], B[WAL_ROWS];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < WAL_ROWS; k++) {
       A[k] = ld32(pr + 256 * k);
       B[k] = sh ? ld32(pr + 256 * k + 4) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) u = adv256(L, u, c) ^ (sh ? __builtin_amdgcn_alignbyte(B[k], A[k], sh) : A[k]);
+    for (int k = 0; k < WAL_ROWS; k++) u = adv256(L, u, c) ^ (sh ? __builtin_amdgcn_alignbyte(B[k], A[k], sh) : A[k]);
   }
   for (; j < R; j++, pr += 256) {
     const uint32_t A = ld32(pr), B = sh ? ld32(pr + 4) : 0u;
