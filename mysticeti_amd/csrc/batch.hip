@@ -178,11 +178,13 @@ struct CommitteeA {
 __global__ void __launch_bounds__(256, MV_PREP_OCC)
     k_bv_prep(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ pk,
               const uint32_t* __restrict__ key_idx, uint32_t n, BvKey key, CommitteeA ca, uint4* __restrict__ pts,
-              uint4* __restrict__ scal, unsigned long long* __restrict__ bsum_part, uint8_t* __restrict__ status) {
+              uint4* __restrict__ scal, unsigned long long* __restrict__ bsum, uint8_t* __restrict__ status,
+              uint32_t blk0, uint32_t group_sigs) {
   __shared__ unsigned long long sbsum[BSUM_WORDS];
   if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t blk = blockIdx.x + blk0;  // launches may cover a chunk of the batch
+  const uint32_t gid = blk * blockDim.x + threadIdx.x;
   const bool live = gid < n;
   const uint32_t idx = live ? gid : n - 1;
 
@@ -311,7 +313,10 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     atomicAdd(&sbsum[11], (unsigned long long)(uint32_t)acc);
   }
   __syncthreads();
-  if (threadIdx.x < BSUM_WORDS) bsum_part[(size_t)blockIdx.x * BSUM_WORDS + threadIdx.x] = sbsum[threadIdx.x];
+  // the workgroup's column sums into its group's (zeroed before the first prep launch); the
+  // final check then reads 12 words per group instead of reducing a per-workgroup array
+  if (threadIdx.x < BSUM_WORDS)
+    atomicAdd(&bsum[(size_t)(blk * 256u / group_sigs) * BSUM_WORDS + threadIdx.x], sbsum[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------- bucket sort
@@ -377,18 +382,21 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_count(const uint4* __restri
   __syncthreads();
   for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) pcount[(size_t)blockIdx.x * BV_NPG + i] = hist[i];
 }
-// block b: group b / 32, its partitions [64 (b % 32), + 64), 4 chunk subgroups of the
-// group's chunks; row reads are 256-B coalesced. poff[c][p] = entries of partition (g, p)
-// in the group's chunks before c; ptot[g * BV_NPG + p] = partition size.
-__global__ void __launch_bounds__(256) k_part_scan(const uint32_t* __restrict__ pcount, uint32_t nchunk, BvGroups G,
-                                                   uint32_t* __restrict__ poff, uint32_t* __restrict__ ptot) {
-  __shared__ uint32_t gsum[4][64];
+// block b: group b / 32, its partitions [64 (b % 32), + 64), SCAN_SUB chunk subgroups of the
+// group's chunks (one group of 1,024 chunks: 64 chunks per thread, not 256); row reads are
+// 256-B coalesced. poff[c][p] = entries of partition (g, p) in the group's chunks before c;
+// ptot[g * BV_NPG + p] = partition size.
+constexpr int SCAN_SUB = 16;
+__global__ void __launch_bounds__(64 * SCAN_SUB) k_part_scan(const uint32_t* __restrict__ pcount, uint32_t nchunk,
+                                                             BvGroups G, uint32_t* __restrict__ poff,
+                                                             uint32_t* __restrict__ ptot) {
+  __shared__ uint32_t gsum[SCAN_SUB][64];
   constexpr uint32_t BPG = BV_NPG / 64;
   const uint32_t pl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const uint32_t g = blockIdx.x / BPG;
   const uint32_t p = (blockIdx.x % BPG) * 64 + pl;
   const uint32_t cg0 = g * G.cpg, cg1 = min(nchunk, cg0 + G.cpg);
-  const uint32_t per = (cg1 - cg0 + 3) / 4;
+  const uint32_t per = (cg1 - cg0 + SCAN_SUB - 1) / SCAN_SUB;
   const uint32_t c0 = min(cg1, cg0 + q * per), c1 = min(cg1, c0 + per);
   uint32_t sum = 0;
   for (uint32_t c = c0; c < c1; c++) sum += pcount[(size_t)c * BV_NPG + p];
@@ -401,7 +409,7 @@ __global__ void __launch_bounds__(256) k_part_scan(const uint32_t* __restrict__ 
     poff[(size_t)c * BV_NPG + p] = run;
     run += v;
   }
-  if (q == 3) ptot[g * BV_NPG + p] = run;
+  if (q == SCAN_SUB - 1) ptot[g * BV_NPG + p] = run;
 }
 // exclusive scan of the partition totals (all groups) -> pstart[0..total]
 __global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ ptot, uint32_t total,
@@ -448,33 +456,51 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __rest
   }
 }
 // block -> partition P: the partition's entries sorted by bucket into ents; offs[key] for
-// its 256 keys. One thread per bin; a partition's output window is ~64 KB, so the ranked
-// stores of the blocks in flight merge in L2. The biggest partitions (window 15's, whose
-// digits stop at 2^13) of every group are scheduled first.
+// its 256 keys. FINE_NT threads over 256 bins (a partition holds ~8K entries, window 15's
+// ~32K: digits stop at 2^13), so the ranked stores of the blocks in flight merge in L2. The
+// biggest partitions (window 15's) of every group are scheduled first.
 constexpr uint32_t BV_PPW = BV_NB >> BV_FINE_BITS;  // partitions per window (128)
-__global__ void __launch_bounds__(1 << BV_FINE_BITS) k_fine_sort(const unsigned long long* __restrict__ tmp,
-                                                    const uint32_t* __restrict__ pstart, uint32_t ngroups,
-                                                    uint32_t* __restrict__ ents, uint32_t* __restrict__ offs) {
+constexpr int FINE_NT = 1024;
+__global__ void __launch_bounds__(FINE_NT) k_fine_sort(const unsigned long long* __restrict__ tmp,
+                                                       const uint32_t* __restrict__ pstart, uint32_t ngroups,
+                                                       uint32_t* __restrict__ ents, uint32_t* __restrict__ offs) {
   constexpr int NF = 1 << BV_FINE_BITS;
   __shared__ uint32_t cnt[NF];
-  __shared__ uint32_t sm[NF];
   const uint32_t span = ngroups * BV_PPW;
   const uint32_t w = BV_NW - 1 - blockIdx.x / span;
   const uint32_t g = (blockIdx.x % span) / BV_PPW;
   const uint32_t p = g * BV_NPG + w * BV_PPW + blockIdx.x % BV_PPW;
   const uint32_t s = pstart[p], e = pstart[p + 1];
-  cnt[threadIdx.x] = 0;
+  if (threadIdx.x < NF) cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (uint32_t i = s + threadIdx.x; i < e; i += NF) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
+  for (uint32_t i = s + threadIdx.x; i < e; i += FINE_NT) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
   __syncthreads();
-  const uint32_t c = cnt[threadIdx.x];
-  uint32_t total;
-  const uint32_t ex = block_excl_scan256<NF>(c, sm, total);
-  offs[(size_t)p * NF + threadIdx.x] = s + ex;
-  if (p == ngroups * BV_NPG - 1 && threadIdx.x == 0) offs[(size_t)ngroups * BV_NKG] = e;
-  cnt[threadIdx.x] = ex;
+  static_assert(NF == 256, "wave 0 scans four bins per lane");
+  if (threadIdx.x < 64) {  // wave 0 alone (no barrier inside): exclusive scan of the bins
+    const uint32_t l = threadIdx.x;
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = cnt[4 * l + k];
+      sum += c[k];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)incl, o);
+      if (l >= (uint32_t)o) incl += x;
+    }
+    uint32_t ex = incl - sum;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      offs[(size_t)p * NF + 4 * l + k] = s + ex;
+      cnt[4 * l + k] = ex;
+      ex += c[k];
+    }
+    if (p == ngroups * BV_NPG - 1 && l == 0) offs[(size_t)ngroups * BV_NKG] = e;
+  }
   __syncthreads();
-  for (uint32_t i = s + threadIdx.x; i < e; i += NF) {
+  for (uint32_t i = s + threadIdx.x; i < e; i += FINE_NT) {
     const unsigned long long v = tmp[i];
     const uint32_t r = atomicAdd(&cnt[(uint32_t)(v >> 32) & (NF - 1)], 1u);
     ents[s + r] = (uint32_t)v;
@@ -728,31 +754,15 @@ __global__ void __launch_bounds__(256) k_bv_reduce_q(const uint4* __restrict__ i
 
 // ---------------------------------------------------------------- final check
 // One 128-thread block. Quad g of wave 0: Horner over group g's window sums (V of the last
-// reduction level, one per window), four lanes per point. Lane g of wave 1: -[sum z s mod l]B
-// of group g on the comb table of B. flags[1 + g] = group g's equation held; flags[0] = all.
+// reduction level, one per window), four lanes per point. Lane g of wave 1, meanwhile:
+// -[sum z s mod l]B of group g from its column sums (k_bv_prep) on the comb table of B.
+// flags[1 + g] = group g's equation held; flags[0] = all.
 __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV, uint32_t nw,
                                                   const uint4* __restrict__ asum,
-                                                  const unsigned long long* __restrict__ bsum_part, uint32_t nparts,
-                                                  uint32_t parts_per_group, uint32_t ngroups,
+                                                  const unsigned long long* __restrict__ bsum, uint32_t ngroups,
                                                   const uint4* __restrict__ combB, uint32_t* __restrict__ flags) {
-  __shared__ unsigned long long sb[BV_MAXG][BSUM_WORDS];
   __shared__ uint4 sbp[BV_MAXG][P3_QUADS];
   __shared__ uint32_t sflag[BV_MAXG];
-  for (uint32_t i = threadIdx.x; i < BV_MAXG * BSUM_WORDS; i += blockDim.x) (&sb[0][0])[i] = 0;
-  __syncthreads();
-  for (uint32_t g = 0; g < ngroups; g++) {
-    unsigned long long acc[BSUM_WORDS];
-#pragma unroll
-    for (int c = 0; c < BSUM_WORDS; c++) acc[c] = 0;
-    const uint32_t i1 = min(nparts, (g + 1) * parts_per_group);
-    for (uint32_t i = g * parts_per_group + threadIdx.x; i < i1; i += blockDim.x) {
-#pragma unroll
-      for (int c = 0; c < BSUM_WORDS; c++) acc[c] += bsum_part[(size_t)i * BSUM_WORDS + c];
-    }
-#pragma unroll
-    for (int c = 0; c < BSUM_WORDS; c++) atomicAdd(&sb[g][c], acc[c]);
-  }
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   if (threadIdx.x >= 64) {
     if (lane < ngroups) {
@@ -761,7 +771,7 @@ __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV
       unsigned long long carry = 0;
 #pragma unroll
       for (int c = 0; c < BSUM_WORDS; c++) {
-        const unsigned long long v = sb[lane][c];
+        const unsigned long long v = bsum[(size_t)lane * BSUM_WORDS + c];
         const unsigned long long lo = (v & 0xffffffffull) + (carry & 0xffffffffull);
         x[c] = (uint32_t)lo;
         carry = (v >> 32) + (carry >> 32) + (lo >> 32);
@@ -856,7 +866,7 @@ struct BatchLayout {
     segT = take((size_t)groups * BV_NKG * P3_QUADS * 16);
     const size_t lv = (size_t)groups * (BV_NKG / BV_FAN) * P3_QUADS * 16;
     rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
-    bsum = take(nblk * BSUM_WORDS * 8);
+    bsum = take((size_t)BV_MAXG * BSUM_WORDS * 8);  // per group
     kpart = take(nchunk * BV_MAXKEYS * 8 * 8);
     asum = take((size_t)BV_MAXG * P3_QUADS * 16);
     flag = take((1 + BV_MAXG) * 4);
@@ -912,7 +922,8 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok,
-                               uint32_t n_keys, const void* comb_b) {
+                               uint32_t n_keys, const void* comb_b, const hipEvent_t* chunk_ready,
+                               uint32_t nchunks, const uint32_t* chunk_end) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
@@ -951,15 +962,29 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   CommitteeA ca{com ? static_cast<const uint4*>(comb_a) : nullptr, key_ok,
                 (uint32_t)(comb_table_bytes(1) / sizeof(uint4)), agg ? 1u : 0u};
   const uint32_t nw = agg ? BV_NWR : BV_NW;  // windows with bucket entries
-  hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,
-                     status);
+  e = hipMemsetAsync(bsum, 0, (size_t)BV_MAXG * BSUM_WORDS * 8, s);  // k_bv_prep accumulates per group
+  if (e != hipSuccess) return e;
+  if (chunk_ready && nchunks) {
+    if (chunk_end[nchunks - 1] != n) return hipErrorInvalidValue;
+    for (uint32_t c = 0, lo = 0; c < nchunks; lo = chunk_end[c++]) {
+      const uint32_t hi = chunk_end[c];
+      if (hi <= lo || lo % 256 || (hi % 256 && hi != n)) return hipErrorInvalidValue;
+      e = hipStreamWaitEvent(s, chunk_ready[c], 0);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_bv_prep, dim3((hi - lo + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca,
+                         pts, scal, bsum, status, lo / 256, G.cpg * PART_CHUNK);
+    }
+  } else {
+    hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,
+                       status, 0u, G.cpg * PART_CHUNK);
+  }
   mark(1);
   hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, agg ? 1u : 0u, pcount);
-  hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(256), 0, s, pcount, nchunk, G, poff, ptot);
+  hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(64 * SCAN_SUB), 0, s, pcount, nchunk, G, poff, ptot);
   hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, nparts, pstart);
   hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
                      agg ? 1u : 0u, tmp);
-  hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(1 << BV_FINE_BITS), 0, s, tmp, pstart, G.count, ents, offs);
+  hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
   mark(2);
   // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
   // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
@@ -996,8 +1021,8 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     cnt = out;
   }
   mark(4);
-  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, nw, agg ? (const uint4*)asum : nullptr, bsum, nblk,
-                     G.cpg * (PART_CHUNK / 256), G.count, static_cast<const uint4*>(comb_b), flag);
+  hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, nw, agg ? (const uint4*)asum : nullptr, bsum,
+                     G.count, static_cast<const uint4*>(comb_b), flag);
   mark(5);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

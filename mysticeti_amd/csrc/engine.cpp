@@ -87,9 +87,13 @@ struct Device {
   // host-buffer batch verifies: two compute streams and double-buffered device inputs, so
   // the (pageable) H2D of one chunk runs beside the previous chunk's verification
   hipStream_t pstream[2] = {nullptr, nullptr};
+  hipStream_t xstream = nullptr;  // H2D copies of pinned inputs (verify_host_streamed)
   DevBuf pin_msg[2], pin_sig[2], pin_pk[2], pin_st[2];
   HostBuf h_stage[2];
   hipEvent_t pin_free[2] = {nullptr, nullptr};
+  // pinned inputs: per-chunk "copied" events of the two input buffers (verify_host_streamed)
+  static constexpr int kMaxChunks = 64;
+  hipEvent_t chunk_ev[2][kMaxChunks] = {};
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
   DevBuf committee_pk, stakes, combA, keyok;
@@ -142,11 +146,12 @@ struct mv_ctx {
   std::atomic<uint64_t> calls{0};   // batch calls, the PRF's per-call input
   std::atomic<uint64_t> batches{0}, fallbacks{0}, groups_run{0}, groups_failed{0};
   // sub-batch equations per batch: groups_fixed != 0 forces that many; 0 = adaptive:
-  // base_groups equations (4 cost nothing measurable over 1: the sort runs on 4x more, 4x
-  // smaller partitions), and after a batch whose equation failed, the next kGuardBatches
-  // batches are cut into guard_groups (a failure then re-verifies 1/8 of the batch).
+  // base_groups equations (one: every group adds 16 x 2^15 buckets to the bucket and reduce
+  // kernels; config 2 measured 267 M/s at one group against 241 M/s at four), and after a
+  // batch whose equation failed, the next kGuardBatches batches are cut into guard_groups
+  // (a failure then re-verifies 1/8 of the batch).
   uint32_t groups_fixed = 0;
-  uint32_t base_groups = 4;
+  uint32_t base_groups = 1;
   uint32_t guard_groups = 8;
   std::atomic<int> guard_left{0};
   // stage timing (mv_set_stage_timing): event sets of calls not yet read back
@@ -283,7 +288,8 @@ uint32_t pick_groups(mv_ctx* ctx) {
 // device) receives the all-groups flag word.
 mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
                         const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s,
-                        uint32_t* flag_dst) {
+                        uint32_t* flag_dst, const hipEvent_t* chunk_ready = nullptr, uint32_t nchunks = 0,
+                        const uint32_t* chunk_end = nullptr) {
   poll_flags(ctx, dev);
   const int slot = dev.next_slot;
   dev.next_slot = (slot + 1) % Device::kSlots;
@@ -319,7 +325,8 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
                                        com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr,
-                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p));
+                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p, chunk_ready,
+                                       nchunks, chunk_end));
   keep_events(ctx, dev.id, 0, evs);
   if (flag_dst) HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, hipMemcpyDeviceToDevice, s));
   const uint32_t ng = (n + mvk::batch_group_size(n, groups) - 1) / mvk::batch_group_size(n, groups);
@@ -754,6 +761,97 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
   return MV_OK;
 }
 
+// mv_ed25519_verify's batch path over [lo, hi) of pinned caller arrays, in a few large
+// batches (two by default) on two compute streams. The DMA engines copy a batch's inputs
+// chunk by chunk on a copy stream, and k_bv_prep of chunk c starts as soon as chunk c has
+// landed, so the PCIe copy overlaps the preparation; batch t + 1's copy and preparation run
+// beside batch t's sort, buckets and tail (two input buffers, reuse ordered by events).
+mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
+                               const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status) {
+  static const int chunk_log2 = [] {  // MV_STREAM_CHUNK_LOG2 (experiments): signatures per copy chunk
+    const char* e = getenv("MV_STREAM_CHUNK_LOG2");
+    const int v = e ? atoi(e) : 17;
+    return v < 8 ? 8 : (v > 24 ? 24 : v);
+  }();
+  static const uint64_t min_batches = [] {  // MV_STREAM_BATCHES (experiments): batches per call, at least
+    const char* e = getenv("MV_STREAM_BATCHES");
+    const int v = e ? atoi(e) : 2;
+    return (uint64_t)(v < 1 ? 1 : v);
+  }();
+  const uint64_t m = hi - lo;
+  // at least two batches, on alternating compute streams: batch t's sort, buckets and tail
+  // run beside batch t + 1's copy and preparation
+  uint64_t nb = std::max<uint64_t>(min_batches, (m + ctx->max_batch - 1) / ctx->max_batch);
+  uint64_t bs64 = ((m + nb - 1) / nb + 1023) & ~1023ull;
+  if (bs64 < MV_BATCH_MIN) bs64 = MV_BATCH_MIN;
+  if (bs64 > ctx->max_batch) bs64 = ctx->max_batch;
+  const uint32_t bs = (uint32_t)bs64;
+  uint32_t chunk = 1u << chunk_log2;
+  while ((bs + chunk - 1) / chunk > (uint32_t)Device::kMaxChunks / 2) chunk <<= 1;
+  // chunk schedule: the first batch starts with small chunks (2^14, 2^15, ... signatures), so
+  // the chip starts preparing after ~40 us of copying instead of a whole chunk's
+  std::vector<uint32_t> sched[2];
+  for (int b = 0; b < 2; b++) {
+    uint32_t o = 0, c = b == 0 ? std::min<uint32_t>(chunk, 1u << 14) : chunk;
+    while (o < bs) {
+      sched[b].push_back(o);
+      o += c;
+      if (c < chunk) c *= 2;
+    }
+    sched[b].push_back(bs);
+  }
+  const size_t kb = pk ? 32 : 4;  // pk rows or committee key indices
+  if (!dev.xstream) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.xstream, hipStreamNonBlocking));
+  for (int b = 0; b < 2; b++) {
+    if (!dev.pstream[b]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[b], hipStreamNonBlocking));
+    if (!dev.pin_free[b]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[b], hipEventDisableTiming));
+    for (int c = 0; c < Device::kMaxChunks; c++)
+      if (!dev.chunk_ev[b][c]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.chunk_ev[b][c], hipEventDisableTiming));
+    HIPCHK(ctx, dev.pin_msg[b].ensure(32 * (size_t)bs));
+    HIPCHK(ctx, dev.pin_sig[b].ensure(64 * (size_t)bs));
+    HIPCHK(ctx, dev.pin_pk[b].ensure(kb * bs));
+    HIPCHK(ctx, dev.pin_st[b].ensure(bs));
+  }
+  HIPCHK(ctx, dev.h_out.ensure(m));
+  uint8_t* hst = dev.h_out.as<uint8_t>();
+  hipStream_t xs = dev.xstream;  // copies; batch t computes on pstream[t & 1]
+  uint64_t t = 0;
+  for (uint64_t i = lo; i < hi; i += bs, t++) {
+    const int b = (int)(t & 1);
+    hipStream_t cs = dev.pstream[b];
+    const uint32_t k = (uint32_t)std::min<uint64_t>(bs, hi - i);
+    // buffer b is free once batch t - 2 (or the previous call's last batch on it) is done
+    HIPCHK(ctx, hipStreamWaitEvent(xs, dev.pin_free[b], 0));
+    const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);
+    const std::vector<uint32_t>& cut = sched[t == 0 ? 0 : 1];
+    std::vector<uint32_t> marks;  // chunk ends, signatures
+    for (uint32_t c = 0; c + 1 < cut.size() && cut[c] < k; c++) {
+      const uint32_t o = cut[c];
+      const size_t r = std::min(cut[c + 1], k) - o;
+      marks.push_back(o + (uint32_t)r);
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].as<uint8_t>() + 32 * (size_t)o, msg + 32 * (i + o), 32 * r,
+                                 hipMemcpyHostToDevice, xs));
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].as<uint8_t>() + 64 * (size_t)o, sig + 64 * (i + o), 64 * r,
+                                 hipMemcpyHostToDevice, xs));
+      HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].as<uint8_t>() + kb * o, src_pk + kb * o, kb * r,
+                                 hipMemcpyHostToDevice, xs));
+      HIPCHK(ctx, hipEventRecord(dev.chunk_ev[b][c], xs));
+    }
+    mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
+                                 pk ? dev.pin_pk[b].as<uint8_t>() : dev.committee_pk.as<uint8_t>(),
+                                 pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), cs,
+                                 nullptr, dev.chunk_ev[b], (uint32_t)marks.size(), marks.data());
+    if (rc != MV_OK) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, cs));
+    HIPCHK(ctx, hipEventRecord(dev.pin_free[b], cs));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[0]));
+  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[1]));
+  poll_flags(ctx, dev);
+  memcpy(status + lo, hst, m);
+  return MV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -866,8 +964,11 @@ void mv_destroy(mv_ctx* ctx) {
       for (DevBuf* b : {&dev.pin_msg[k], &dev.pin_sig[k], &dev.pin_pk[k], &dev.pin_st[k]}) b->release();
       dev.h_stage[k].release();
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
+      for (hipEvent_t ev : dev.chunk_ev[k])
+        if (ev) (void)hipEventDestroy(ev);
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
+    if (dev.xstream) (void)hipStreamDestroy(dev.xstream);
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);
     for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
@@ -980,10 +1081,10 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
     // 2^18..2^20-signature chunks and 8 or 16 staging threads): host memcpy into pinned
     // staging runs at ~10 GB/s per thread, and chunks below 2^20 cost the batch path's
     // fixed per-batch work
-    // Pinned inputs (mv_host_alloc) always take the chunked pipeline with direct DMA reads.
+    // Pinned inputs (mv_host_alloc) stream: chunked DMA copies gate k_bv_prep chunk by chunk.
     static const int pipeline = getenv("MV_PIPELINE") ? atoi(getenv("MV_PIPELINE")) : 0;
     if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN) {
-      if (pinned) return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, true);
+      if (pinned) return verify_host_streamed(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
       if (pipeline) return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, pipeline == 2);
     }
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {

@@ -44,7 +44,13 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
-                               const uint8_t* key_ok = nullptr, uint32_t n_keys = 0, const void* comb_b = nullptr);
+                               const uint8_t* key_ok = nullptr, uint32_t n_keys = 0, const void* comb_b = nullptr,
+                               const hipEvent_t* chunk_ready = nullptr, uint32_t nchunks = 0,
+                               const uint32_t* chunk_end = nullptr);
+// chunk_ready (optional): nchunks events; chunk c = signatures [chunk_end[c - 1], chunk_end[c])
+// (ends multiples of 256 except the last = n). k_bv_prep runs chunk by chunk, each launch after
+// hipStreamWaitEvent on its chunk's event, so the inputs' H2D copies (another stream) overlap
+// the preparation of the chunks already copied.
 // comb_b (required): the comb table of B (mv_create), for the -[sum z s]B term.
 // comb_a / key_ok (optional, with key_idx): the committee's comb tables (comb.hip, tables of
 // -A) and per-key decode flags; k_bv_prep then reads each signature's A from entry [0][1]

@@ -227,7 +227,7 @@ def test_sub_batch_equations_reverify_only_failing_groups(engine, n, groups, wan
 
 
 def test_adaptive_guard_after_a_failed_batch():
-    """Default policy: 4 sub-batch equations per batch; a failed equation arms the guard, and
+    """Default policy: one batch equation per batch; a failed equation arms the guard, and
     the next batches are cut into 8 (a bad signature then re-verifies one group)."""
     with M.Engine(devices=(0,)) as eng:
         n = 16384
@@ -236,7 +236,7 @@ def test_adaptive_guard_after_a_failed_batch():
         s2[100, 40] ^= 0x10
         st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, s2, pk))
         assert st[100] == 1 and (np.delete(st, 100) == 0).all()
-        assert d == (1, 1, 4, 1)
+        assert d == (1, 1, 1, 1)
         st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, s2, pk))
         assert st[100] == 1 and (np.delete(st, 100) == 0).all()
         assert d == (1, 1, 8, 1)

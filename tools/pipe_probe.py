@@ -1,5 +1,5 @@
 """Diagnostics: host-buffer verify timing, pageable arrays vs pinned ones (mv_host_alloc; the
-chunked copy-beside-verify path). MV_PIPE_CHUNK_LOG2 sets the pinned path's chunk size."""
+streamed path: chunked DMA copies gate k_bv_prep). MV_STREAM_CHUNK_LOG2 sets its chunk size."""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -26,7 +26,7 @@ def rate(m, s, p, label):
 rate(msg, sig, pk, "pageable")
 pm, ps, pp = eng.host_empty(msg.shape), eng.host_empty(sig.shape), eng.host_empty(pk.shape)
 pm[:], ps[:], pp[:] = msg, sig, pk
-rate(pm, ps, pp, f"pinned chunk_log2={os.environ.get('MV_PIPE_CHUNK_LOG2', '18')}")
+rate(pm, ps, pp, f"pinned chunk_log2={os.environ.get('MV_STREAM_CHUNK_LOG2', '17')}")
 d = torch.empty(sig.shape, dtype=torch.uint8, device="cuda")
 hp = torch.from_numpy(sig).pin_memory()
 for _ in range(2):
