@@ -922,8 +922,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok,
-                               uint32_t n_keys, const void* comb_b, const hipEvent_t* chunk_ready,
-                               uint32_t nchunks, const uint32_t* chunk_end) {
+                               uint32_t n_keys, const void* comb_b, const ChunkGate* gate) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
@@ -964,15 +963,24 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   const uint32_t nw = agg ? BV_NWR : BV_NW;  // windows with bucket entries
   e = hipMemsetAsync(bsum, 0, (size_t)BV_MAXG * BSUM_WORDS * 8, s);  // k_bv_prep accumulates per group
   if (e != hipSuccess) return e;
-  if (chunk_ready && nchunks) {
-    if (chunk_end[nchunks - 1] != n) return hipErrorInvalidValue;
-    for (uint32_t c = 0, lo = 0; c < nchunks; lo = chunk_end[c++]) {
-      const uint32_t hi = chunk_end[c];
+  if (gate && gate->n) {
+    const uint32_t* end = gate->end;
+    if (end[gate->n - 1] != n) return hipErrorInvalidValue;
+    if (gate->aux) {
+      if ((e = hipEventRecord(gate->fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(gate->aux, gate->fork, 0)) != hipSuccess) return e;
+    }
+    for (uint32_t c = 0, lo = 0; c < gate->n; lo = end[c++]) {
+      const uint32_t hi = end[c];
       if (hi <= lo || lo % 256 || (hi % 256 && hi != n)) return hipErrorInvalidValue;
-      e = hipStreamWaitEvent(s, chunk_ready[c], 0);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_bv_prep, dim3((hi - lo + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca,
+      hipStream_t ps = gate->aux && (c & 1) ? gate->aux : s;
+      if ((e = hipStreamWaitEvent(ps, gate->ready[c], 0)) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_bv_prep, dim3((hi - lo + 255) / 256), dim3(256), 0, ps, msg, sig, pk, key_idx, n, k, ca,
                          pts, scal, bsum, status, lo / 256, G.cpg * PART_CHUNK);
+    }
+    if (gate->aux) {
+      if ((e = hipEventRecord(gate->join, gate->aux)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(s, gate->join, 0)) != hipSuccess) return e;
     }
   } else {
     hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,

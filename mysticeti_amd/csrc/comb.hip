@@ -36,6 +36,7 @@
 #include "scalar25519.h"
 #include "tables.h"
 #include "comb.h"
+#include "blake2b_quad.h"
 
 namespace mv {
 
@@ -186,6 +187,143 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* __restrict__
   }
 }
 
+// The same predicate split in two, for small batches of long blocks (config 5, 8-KB
+// pre-images), where k_b2_quad's serial chain of ~65 compressions is the latency path. The
+// terms that need only the signature run in the same launch as the hash, on workgroups of
+// their own (no cross-stream events: each costs ~10 us of queue drain on this path):
+//   k_hash_comb_pre  workgroups [0, nh): quad BLAKE2b of 16 blocks each (blake2b_quad.h);
+//                    [nh, nh + np): s < l and the ZIP-215 decode of R, 64 signatures each;
+//                    [nh + np, nh + 2 np): -[s]B on C_B, 64 signatures each
+//   k_comb_post (8 waves): k = SHA-512(R || A || M) mod l on every wave; wave w: the A-table
+//                    entries of k's digits 4w .. 4w + 3 (4 additions), wave 7 also R - [s]B;
+//                    a 3-level tree over the waves' sums; wave 0: R - [s]B - sum (the tables
+//                    hold -A), [8], identity test.
+// k_comb_post's latency is a SHA-512 and 4 + 5 additions instead of the R decode.
+__global__ void __launch_bounds__(64) k_hash_comb_pre(const uint8_t* __restrict__ stage,
+                                                      const uint64_t* __restrict__ poff,
+                                                      const uint64_t* __restrict__ plen, uint8_t* __restrict__ md,
+                                                      uint8_t* __restrict__ bd, const uint8_t* __restrict__ sig,
+                                                      uint32_t n, uint32_t nh, uint32_t np,
+                                                      const uint4* __restrict__ combB, uint4* __restrict__ rbuf,
+                                                      uint4* __restrict__ sbuf, uint8_t* __restrict__ qflags) {
+  const uint32_t blk = blockIdx.x;
+  if (blk < nh) {
+    b2q::quad_hash<true, 1>(blk, stage, poff, plen, n, md, bd);
+    return;
+  }
+  const bool role_r = blk < nh + np;
+  const uint32_t gid = (blk - nh - (role_r ? 0 : np)) * 64 + threadIdx.x;
+  const uint32_t idx = gid < n ? gid : n - 1;
+  uint4 q[9];
+  if (role_r) {
+    uint32_t rw[8], sw[8];
+    load8(rw, sig + 64 * (size_t)idx);
+    load8(sw, sig + 64 * (size_t)idx + 32);
+    const bool s_ok = sc_is_canonical(sw);
+    p3 R;
+    bool okR;
+    decompress1(R, okR, rw);
+    p3_to_quads(q, R);
+    if (gid < n) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) rbuf[(size_t)gid * 9 + k] = q[k];
+      qflags[gid] = (s_ok ? 1 : 0) | (okR ? 2 : 0);
+    }
+  } else {
+    uint32_t sw[8], sd[8];
+    load8(sw, sig + 64 * (size_t)idx + 32);
+    sc_recode256(sd, sw);
+    p3 acc;
+    ct_sum(acc, combB, sd, 0, CT_ROWS);
+    p3_neg(acc, acc);
+    p3_to_quads(q, acc);
+    if (gid < n) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) sbuf[(size_t)gid * 9 + k] = q[k];
+    }
+  }
+}
+
+constexpr int POST_WAVES = 8;
+__global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __restrict__ msg,
+                                                              const uint8_t* __restrict__ sig,
+                                                              const uint8_t* __restrict__ pk,
+                                                              const uint32_t* __restrict__ key_idx, uint32_t n,
+                                                              const uint4* __restrict__ combA,
+                                                              const uint8_t* __restrict__ key_ok,
+                                                              const uint4* __restrict__ rbuf,
+                                                              const uint4* __restrict__ sbuf,
+                                                              const uint8_t* __restrict__ qflags,
+                                                              uint8_t* __restrict__ status) {
+  __shared__ uint4 part[POST_WAVES][9][64];  // per-wave partial sums, [quad][lane]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t gid = blockIdx.x * 64 + lane;
+  const uint32_t idx = gid < n ? gid : n - 1;
+  const uint32_t key = key_idx[idx];
+  uint4 q[9];
+  p3 acc, X;
+  {
+    uint32_t kin[24], h[16], k[8], kd[8];
+    load8(kin, sig + 64 * (size_t)idx);
+    load8(kin + 8, pk + 32 * (size_t)key);
+    load8(kin + 16, msg + 32 * (size_t)idx);
+    sha512_short(h, kin, 96);
+    sc_reduce512(k, h);
+    sc_recode256(kd, k);
+    const int r0 = wave * (CT_ROWS / POST_WAVES);
+    ct_sum(acc, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / POST_WAVES);  // -[k_w]A
+  }
+  if (wave == POST_WAVES - 1) {  // also R - [s]B (k_hash_comb_pre), into the spare slot 0
+    p3 R;
+#pragma unroll
+    for (int k = 0; k < 9; k++) q[k] = rbuf[(size_t)idx * 9 + k];
+    quads_to_p3(R, q);
+#pragma unroll
+    for (int k = 0; k < 9; k++) q[k] = sbuf[(size_t)idx * 9 + k];
+    quads_to_p3(X, q);
+    ct_acc(R, X);
+    p3_to_quads(q, R);
+#pragma unroll
+    for (int k = 0; k < 9; k++) part[0][k][lane] = q[k];
+  }
+  // tree over the waves' partial sums: wave w < h adds wave w + h's
+  for (int h = POST_WAVES / 2; h >= 1; h >>= 1) {
+    if (wave >= h && wave < 2 * h) {
+      p3_to_quads(q, acc);
+#pragma unroll
+      for (int k = 0; k < 9; k++) part[wave][k][lane] = q[k];
+    }
+    __syncthreads();
+    if (wave < h) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) q[k] = part[wave + h][k][lane];
+      quads_to_p3(X, q);
+      ct_acc(acc, X);
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    p3_neg(acc, acc);  // +[k]A
+#pragma unroll
+    for (int k = 0; k < 9; k++) q[k] = part[0][k][lane];
+    quads_to_p3(X, q);
+    ct_acc(acc, X);  // R - [s]B + [k]A = R - R'
+    p2 P;
+    p1p1 t;
+    P.X = acc.X;
+    P.Y = acc.Y;
+    P.Z = acc.Z;
+#pragma unroll 1
+    for (int d = 0; d < 3; d++) {  // cofactor
+      p2_dbl(t, P);
+      p1p1_to_p2(P, t);
+    }
+    const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
+    const uint8_t f = qflags[idx];
+    if (gid < n) status[gid] = !key_ok[key] ? 2 : (((f & 3) == 3 && ident) ? 0 : 1);
+  }
+}
+
 }  // namespace mv
 
 // ---------------------------------------------------------------- launchers
@@ -206,6 +344,25 @@ hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                      (const uint4*)combB, (const uint4*)combA, key_ok, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_hash_comb_pre(const uint8_t* stage, const uint64_t* poff, const uint64_t* plen, uint32_t n,
+                                uint8_t* md, uint8_t* bd, const uint8_t* sig, const void* combB, void* rbuf,
+                                void* sbuf, uint8_t* qflags, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nh = (n + 15) / 16, np = (n + 63) / 64;
+  hipLaunchKernelGGL(mv::k_hash_comb_pre, dim3(nh + 2 * np), dim3(64), 0, s, stage, poff, plen, md, bd, sig, n, nh,
+                     np, (const uint4*)combB, (uint4*)rbuf, (uint4*)sbuf, qflags);
+  return hipGetLastError();
+}
+
+hipError_t launch_comb_post(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                            uint32_t n, const void* combA, const uint8_t* key_ok, const void* rbuf,
+                            const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mv::k_comb_post, dim3((n + 63) / 64), dim3(64 * mv::POST_WAVES), 0, s, msg, sig, pk, key_idx, n,
+                     (const uint4*)combA, key_ok, (const uint4*)rbuf, (const uint4*)sbuf, qflags, status);
   return hipGetLastError();
 }
 

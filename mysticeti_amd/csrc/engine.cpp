@@ -288,8 +288,7 @@ uint32_t pick_groups(mv_ctx* ctx) {
 // device) receives the all-groups flag word.
 mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
                         const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s,
-                        uint32_t* flag_dst, const hipEvent_t* chunk_ready = nullptr, uint32_t nchunks = 0,
-                        const uint32_t* chunk_end = nullptr) {
+                        uint32_t* flag_dst, const mvk::ChunkGate* gate = nullptr) {
   poll_flags(ctx, dev);
   const int slot = dev.next_slot;
   dev.next_slot = (slot + 1) % Device::kSlots;
@@ -325,8 +324,7 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
                                        com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr,
-                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p, chunk_ready,
-                                       nchunks, chunk_end));
+                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p, gate));
   keep_events(ctx, dev.id, 0, evs);
   if (flag_dst) HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, hipMemcpyDeviceToDevice, s));
   const uint32_t ng = (n + mvk::batch_group_size(n, groups) - 1) / mvk::batch_group_size(n, groups);
@@ -405,6 +403,14 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   o += al(32 * nn);
   const size_t o_bd = o;
   o += al(32 * nn);
+  // small batches of long blocks: the comb verify's signature-only half beside the hash
+  // bytes per block from which the split pays (MV_COMB_SPLIT_BYTES: tests and experiments; 0 = never)
+  const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
+  const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
+  const bool batch = !(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN;
+  const bool split = !batch && !(ctx->flags & MV_FLAG_NO_COMB) && split_bytes && buf_bytes >= split_bytes * nn;
+  const size_t o_q = o;
+  if (split) o += 2 * al(144 * nn) + al(nn);
   HIPCHK(ctx, dev.blk[slot].ensure(o));
   char* b = dev.blk[slot].as<char>();
   uint8_t* stage = (uint8_t*)(b + o_stage);
@@ -425,13 +431,23 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                       com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
   HIPCHK(ctx, mark(1));
-  HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
+  uint8_t* rbuf = (uint8_t*)(b + o_q);
+  uint8_t* sbuf = rbuf + al(144 * nn);
+  uint8_t* qflags = sbuf + al(144 * nn);
+  if (split)  // the hash, and beside it on workgroups of their own the signature-only terms
+    HIPCHK(ctx, mvk::launch_hash_comb_pre(stage, poff, plen, n, md, bd, sig, dev.combB.p, rbuf, sbuf, qflags, s));
+  else
+    HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
   // a block whose digest does not match is rejected ahead of its signature (types.rs:327-332):
-  // s >= l takes it out of the batch equation, so a tampered block never fails the batch
-  HIPCHK(ctx, mvk::launch_block_digest_gate(claimed, bd, facts, n, sig, s));
+  // s >= l takes it out of the batch equation, so a tampered block never fails the batch (the
+  // per-signature paths need no gate: the verdict puts the digest first)
+  if (batch) HIPCHK(ctx, mvk::launch_block_digest_gate(claimed, bd, facts, n, sig, s));
   HIPCHK(ctx, mark(2));
-  if (!(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN) {
+  if (batch) {
     st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, nullptr);
+  } else if (split) {
+    HIPCHK(ctx, mvk::launch_comb_post(md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, dev.combA.p,
+                                      dev.keyok.as<uint8_t>(), rbuf, sbuf, qflags, sst, s));
   } else {
     st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s);
   }
@@ -837,10 +853,13 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
                                  hipMemcpyHostToDevice, xs));
       HIPCHK(ctx, hipEventRecord(dev.chunk_ev[b][c], xs));
     }
+    // every chunk's prep on cs (a second prep stream per compute stream measured slower:
+    // 163-167 vs 175-180 M/s; more streams than the 4 hardware queues share queues)
+    const mvk::ChunkGate gate{dev.chunk_ev[b], (uint32_t)marks.size(), marks.data(), nullptr, nullptr, nullptr};
     mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dev.committee_pk.as<uint8_t>(),
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), cs,
-                                 nullptr, dev.chunk_ev[b], (uint32_t)marks.size(), marks.data());
+                                 nullptr, &gate);
     if (rc != MV_OK) return rc;
     HIPCHK(ctx, hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, cs));
     HIPCHK(ctx, hipEventRecord(dev.pin_free[b], cs));

@@ -36,6 +36,13 @@ hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* b
 // device address of the flag words: [0] = 1 if every group's equation held, [1 + g] = 1
 // if group g's held. ev (optional): BATCH_STAGES + 1 events, recorded before the first
 // stage and after each stage.
+struct ChunkGate {
+  const hipEvent_t* ready;
+  uint32_t n;
+  const uint32_t* end;
+  hipStream_t aux;  // may be null: every chunk on s
+  hipEvent_t fork, join;
+};
 constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
 constexpr int BATCH_MAX_GROUPS = 16;
 size_t batch_scratch_bytes(uint32_t n, uint32_t groups);
@@ -45,12 +52,12 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
                                const uint8_t* key_ok = nullptr, uint32_t n_keys = 0, const void* comb_b = nullptr,
-                               const hipEvent_t* chunk_ready = nullptr, uint32_t nchunks = 0,
-                               const uint32_t* chunk_end = nullptr);
-// chunk_ready (optional): nchunks events; chunk c = signatures [chunk_end[c - 1], chunk_end[c])
-// (ends multiples of 256 except the last = n). k_bv_prep runs chunk by chunk, each launch after
-// hipStreamWaitEvent on its chunk's event, so the inputs' H2D copies (another stream) overlap
-// the preparation of the chunks already copied.
+                               const struct ChunkGate* gate = nullptr);
+// gate (optional): the inputs arrive in chunks (H2D copies on another stream). Chunk c =
+// signatures [end[c - 1], end[c]) (ends multiples of 256 except the last = n); k_bv_prep runs
+// chunk by chunk, each launch after hipStreamWaitEvent on ready[c], alternating between s and
+// aux (when set) so one chunk's latency-bound preparation overlaps the next's; fork / join
+// order aux after s's earlier work and s's later stages after aux's preparations.
 // comb_b (required): the comb table of B (mv_create), for the -[sum z s]B term.
 // comb_a / key_ok (optional, with key_idx): the committee's comb tables (comb.hip, tables of
 // -A) and per-key decode flags; k_bv_prep then reads each signature's A from entry [0][1]
@@ -64,6 +71,16 @@ hipError_t launch_comb_init(const uint8_t* enc, uint32_t nb, int negate, void* t
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
                               uint8_t* status, hipStream_t s);
+// the comb verify split in two, for small batches of long blocks: k_hash_comb_pre is
+// launch_block_hash plus, on workgroups of their own, the signature-only terms (R decoded ->
+// rbuf, -[s]B -> sbuf, 144 B per signature each, flags: bit 0 s < l, bit 1 R decodes);
+// k_comb_post adds the message-dependent [k]A and tests [8](R - R') = O
+hipError_t launch_hash_comb_pre(const uint8_t* stage, const uint64_t* poff, const uint64_t* plen, uint32_t n,
+                                uint8_t* md, uint8_t* bd, const uint8_t* sig, const void* combB, void* rbuf,
+                                void* sbuf, uint8_t* qflags, hipStream_t s);
+hipError_t launch_comb_post(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+                            uint32_t n, const void* combA, const uint8_t* key_ok, const void* rbuf,
+                            const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s);
 // ingest.hip: device-side bincode parse + pre-image staging, and the final block verdict
 hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,

@@ -178,3 +178,33 @@ def test_config4_shape_4100_blocks_through_the_batch_path(engine):
     for i in sample:
         ost, omd, obd = O.block_verify(bins[i], pks, stakes, 0)
         assert int(st[i]) == ost and md[i].tobytes() == omd and bd[i].tobytes() == obd, i
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_comb_split_and_fused_paths_agree(engine, golden, monkeypatch, split):
+    """Batches under MV_BATCH_MIN take the committee comb verify. Long blocks run it split
+    (k_comb_pre -- s < l, R decode, R - [s]B -- on a second stream beside the hash, k_comb_post
+    after it); MV_COMB_SPLIT_BYTES=1 forces the split for every block, 0 the fused kernel: the
+    edge cases, ragged lengths and config-4-shaped blocks with bad signatures keep the oracle's
+    verdicts and digests either way."""
+    import hashlib as H
+
+    import mysticeti_amd as M
+    import mysticeti_amd.blocks as MB
+
+    monkeypatch.setenv("MV_COMB_SPLIT_BYTES", split)
+    test_block_edge_cases(engine, golden)
+    test_mixed_lengths_and_failures(engine)
+    bins = list(MB.config4(engine, rounds=1))[:64]
+    pks, stakes = MB.committee(engine, 100, distinct=True)
+    engine.set_committee(pks, stakes, 0)
+    for i, flip in ((5, -20), (33, -50)):  # s bit (s < l), R bit; digest recomputed: SIG_INVALID
+        b = bytearray(bins[i])
+        b[flip] ^= 0x10
+        b[24:56] = H.blake2b(M.block_preimage(bytes(b)) + bytes(b[-64:]), digest_size=32).digest()
+        bins[i] = bytes(b)
+    st, md, bd = engine.verify_blocks(bins)
+    assert st[5] == 6 and st[33] == 6 and (np.delete(st, [5, 33]) == 0).all()
+    for i in (0, 5, 33, 63):
+        ost, omd, obd = O.block_verify(bins[i], pks, stakes, 0)
+        assert int(st[i]) == ost and md[i].tobytes() == omd and bd[i].tobytes() == obd, i
