@@ -228,7 +228,8 @@ mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out /* 4 */);
 /* Sub-batch equations per batch-path call: the batch is cut into groups of whole 1024-signature
  * chunks, each with its own combined equation, and a failed equation re-verifies only its group.
  * groups = 0 (default): adaptive -- 1 group per batch; after a batch whose equation failed,
- * the next 64 batches are cut into 8. groups = 1..16 fixes the count. Verdicts never depend on it. */
+ * the next 64 batches are cut into 8. groups = 1..16 fixes the count. Every call clears the guard.
+ * Verdicts never depend on it. */
 mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups);
 /* Stage timing: when enabled, every call records HIP events on its stream around its
  * stages: batch path 0..5 (prep, sort, bucket, reduce, final, fallback), block pipeline

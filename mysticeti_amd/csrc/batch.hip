@@ -514,7 +514,12 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort(const unsigned long long*
 // window's sum (k_bv_reduce). seg = 1: T only (V = T). Windows are laid out high-first in the
 // grid (window 15's buckets hold four times the entries), every group's windows side by side,
 // and each point is loaded one add ahead.
-__global__ void __launch_bounds__(256) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
+// 3 workgroups per CU (168 VGPRs, 16 spilled) beat 2 (175 VGPRs, no spill): the gathers
+// need the third wave per SIMD (config 2: bucket 1.71 -> 1.44-1.50 ms as run, +0.8% step rate)
+#ifndef MV_BUCKET_OCC
+#define MV_BUCKET_OCC 3
+#endif
+__global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ ents, uint32_t ngroups, uint32_t seg,
                                                    uint32_t nw, uint4* __restrict__ segV, uint4* __restrict__ segT) {
   const uint32_t nsw = BV_NB / seg;  // segments per (group, window) row

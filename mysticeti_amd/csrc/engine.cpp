@@ -87,7 +87,6 @@ struct Device {
   // host-buffer batch verifies: two compute streams and double-buffered device inputs, so
   // the (pageable) H2D of one chunk runs beside the previous chunk's verification
   hipStream_t pstream[2] = {nullptr, nullptr};
-  hipStream_t xstream = nullptr;  // H2D copies of pinned inputs (verify_host_streamed)
   DevBuf pin_msg[2], pin_sig[2], pin_pk[2], pin_st[2];
   HostBuf h_stage[2];
   hipEvent_t pin_free[2] = {nullptr, nullptr};
@@ -817,7 +816,6 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     sched[b].push_back(bs);
   }
   const size_t kb = pk ? 32 : 4;  // pk rows or committee key indices
-  if (!dev.xstream) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.xstream, hipStreamNonBlocking));
   for (int b = 0; b < 2; b++) {
     if (!dev.pstream[b]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[b], hipStreamNonBlocking));
     if (!dev.pin_free[b]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[b], hipEventDisableTiming));
@@ -830,7 +828,11 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   }
   HIPCHK(ctx, dev.h_out.ensure(m));
   uint8_t* hst = dev.h_out.as<uint8_t>();
-  hipStream_t xs = dev.xstream;  // copies; batch t computes on pstream[t & 1]
+  // copies on the device stream (idle here: calls are serialised by ctx->mu); batch t computes on
+  // pstream[t & 1]. mv_create makes these three streams first, so they sit on three distinct
+  // hardware queues (GPU_MAX_HW_QUEUES = 4; later streams share queues round-robin, and a copy
+  // queued behind another stream's kernels would serialise the pipeline)
+  hipStream_t xs = dev.stream;
   uint64_t t = 0;
   for (uint64_t i = lo; i < hi; i += bs, t++) {
     const int b = (int)(t & 1);
@@ -946,6 +948,7 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   for (auto& dev : ctx->devs) {
     hipError_t e = hipSetDevice(dev.id);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking);
+    for (int k = 0; k < 2 && e == hipSuccess; k++) e = hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking);
     if (e == hipSuccess) e = dev.btab.ensure(mvk::btable_bytes());
     if (e == hipSuccess) e = mvk::launch_btable_init(dev.btab.p, dev.stream);
     if (e == hipSuccess) e = dev.combB.ensure(mvk::comb_table_bytes(1));
@@ -987,7 +990,6 @@ void mv_destroy(mv_ctx* ctx) {
         if (ev) (void)hipEventDestroy(ev);
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
-    if (dev.xstream) (void)hipStreamDestroy(dev.xstream);
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);
     for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
@@ -1285,6 +1287,7 @@ mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups) {
   if (!ctx || groups > (uint32_t)mvk::BATCH_MAX_GROUPS) return set_err(ctx, MV_E_INVALID_ARG, "groups > 16");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->groups_fixed = groups;
+  ctx->guard_left = 0;  // a new policy starts unguarded
   return MV_OK;
 }
 
