@@ -173,12 +173,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    # one GPU per rank; a rehearsal with more ranks than GPUs (e.g. 2 ranks on a 1-GPU box) shares
+    # devices round-robin (device_count does not initialise the GPU)
+    local_rank %= max(1, torch.cuda.device_count())
 
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")
+        from mysticeti_amd.dist import init_gloo
+
+        init_gloo(dist)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     import mysticeti_amd as M

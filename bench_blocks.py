@@ -84,12 +84,17 @@ def run(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    # one GPU per rank; a rehearsal with more ranks than GPUs (e.g. 2 ranks on a 1-GPU box) shares
+    # devices round-robin (device_count does not initialise the GPU)
+    local_rank %= max(1, torch.cuda.device_count())
 
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")
+        from mysticeti_amd.dist import init_gloo
+
+        init_gloo(dist)
     torch.cuda.set_device(local_rank)
     sys.path.insert(0, ROOT)
     import mysticeti_amd as M
@@ -319,7 +324,7 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     comp_alg = -(-pre_len // 128) + -(-(pre_len + 64) // 128)
     hash_ms = stage_ms.get("hash")
     cpu_res = None
-    if cpu:
+    if cpu and int(os.environ.get("RANK", "0")) == 0:  # the CPU baseline: rank 0 at any N
         lib = _oracle_native()
         threads, share_src = _cpu_threads()
         res = {}

@@ -145,7 +145,7 @@ def wal_measure(eng, torch, local_rank, world, dist, n: int, steps: int, warmup:
                       "entries_per_gpu": n, "image_bytes": image_bytes, "map_bits": map_bits,
                       "parallelism": f"shard-per-gpu x{world} (one WAL image per rank), no collective"},
            "stage_ms": stage_ms, "roofline": roof, "correct": bool(ok)}
-    if cpu and local_rank == 0:
+    if cpu and int(os.environ.get("RANK", "0")) == 0:
         out["cpu_baseline"] = cpu_baseline(img, end, map_bits)
         out["speedup_vs_cpu"] = round(value / world / 1e9 / out["cpu_baseline"]["value"], 1)
     del d_img

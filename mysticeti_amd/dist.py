@@ -11,6 +11,23 @@ import time
 from typing import Callable, Optional, Tuple
 
 
+def init_gloo(dist) -> None:
+    """dist.init_process_group("gloo") with the C++ library's stdout chatter ("[Gloo] Rank r is
+    connected to ...") sent to stderr: stdout carries only rank 0's JSON line."""
+    import os
+    import sys
+
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        dist.init_process_group("gloo")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def shard_range(rank: int, world: int, per_rank: int) -> Tuple[int, int]:
     """Corpus indices owned by `rank` (weak scaling: `per_rank` items each)."""
     assert 0 <= rank < world and per_rank >= 0

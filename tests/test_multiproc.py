@@ -55,3 +55,32 @@ def test_shard_ranges_cover_without_overlap():
             lo, hi = shard_range(r, world, 1000)
             seen.extend(range(lo, hi))
         assert seen == list(range(world * 1000))
+
+
+def test_torchrun_stdout_is_one_json_line(tmp_path):
+    """bench.py's launch shape (torch.distributed.run, 2 ranks, gloo): the gloo library's own
+    stdout chatter goes to stderr during init (init_gloo), so stdout holds only rank 0's line."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "line.py"
+    script.write_text(
+        "import json, os, sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import torch.distributed as dist\n"
+        "from mysticeti_amd.dist import all_ranks_ok, init_gloo\n"
+        "init_gloo(dist)\n"
+        "ok = all_ranks_ok(True, dist)\n"
+        "if dist.get_rank() == 0:\n"
+        "    print(json.dumps({'world': dist.get_world_size(), 'ok': ok}), flush=True)\n"
+        "dist.destroy_process_group()\n")
+    port = 29000 + os.getpid() % 900
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    assert json.loads(lines[0]) == {"world": 2, "ok": True}
