@@ -159,7 +159,8 @@ def main():
                     help="skip the 1-bad-signature and config-3 (1%% corrupted) rates")
     ap.add_argument("--no-config4", dest="config4", action="store_false",
                     help="skip the config-4 (100-validator blocks) rate in the default line")
-    ap.add_argument("--config4-batch", type=int, default=1 << 20, help="config-4 blocks per GPU per step")
+    ap.add_argument("--config4-batch", type=int, default=1 << 21,
+                    help="config-4 blocks per GPU per step (2^21: BASELINE config 4's 16M blocks over 8 GPUs)")
     ap.add_argument("--no-wal", dest="wal", action="store_false",
                     help="skip the WAL replay-check rate (row f4) in the default line")
     ap.add_argument("--wal-entries", type=int, default=1 << 20, help="WAL entries (config-4 blocks) per GPU")

@@ -360,6 +360,7 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
            "data": f"synthetic config-4 blocks ({nb} distinct, signed on the GPU, replicated in HBM)",
            "config": {"workload": "config4: 100-validator blocks, 67 includes, 512-B tx, 66 VoteRanges, "
                                   "HBM-resident bincode, device parse + verify", "blocks_per_gpu": n,
+                      "global_blocks": n * world,
                       "bincode_bytes_per_block": L, "preimage_bytes": pre_len,
                       "parallelism": f"shard-per-gpu x{world}, no collective"},
            "roofline": roof,
