@@ -140,7 +140,10 @@ mv_status mv_ed25519_sign(mv_ctx* ctx, const uint8_t* seed, const uint8_t* msg, 
  * Requires mv_set_committee. Concurrent callers are coalesced: a call joins a submission
  * queue, and a caller that finds no device pass running takes every queued call into one
  * pass (the online path: n - 1 peer tasks each with a block or two share a GPU round trip).
- * Several devices: the merged blocks are split into contiguous shards of about equal bytes. */
+ * Several devices: the merged blocks are split into contiguous shards of about equal bytes.
+ * Parameter order: status comes before the two (optional) digest arrays, unlike the draft in
+ * SURVEY.md 8(b), so that the required outputs precede the NULL-able ones; `len` is u64 (blocks
+ * are not bounded by 4 GiB in the type, and off/len share one type). */
 mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                            uint8_t* status, uint8_t* msg_digest, uint8_t* block_digest);
 
