@@ -273,3 +273,38 @@ def test_pipelined_host_batches(engine, committee, pinned):
             ki = pin(ki)
     st = engine.ed25519_verify(msg, sig, key_idx=ki) if committee else engine.ed25519_verify(msg, sig, pk)
     assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
+
+
+@pytest.mark.parametrize("committee", [False, True])
+def test_streamed_pinned_inputs_many_batches(committee):
+    """Pinned inputs with max_batch = 8,192: a call of 5 batches + a ragged tail on the streamed
+    path (two input buffers reused across batches, copy chunks gating k_bv_prep chunk by
+    chunk, two compute streams), twice in a row, with bad signatures in the first, a middle
+    and the last batch: exact verdicts, the same as pageable inputs."""
+    rng = np.random.default_rng(77 + committee)
+    n = 5 * 8192 + 77
+    with M.Engine(devices=(0,), max_batch=8192) as eng:
+        msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        if committee:
+            seeds = rng.integers(0, 256, size=(5, 32), dtype=np.uint8)
+            ki = rng.integers(0, 5, size=n).astype(np.uint32)
+            pk, sig = eng.ed25519_sign(seeds[ki], msg)
+            eng.set_committee(pk[[int(np.nonzero(ki == a)[0][0]) for a in range(5)]], np.ones(5, np.uint64))
+        else:
+            pk, sig = eng.ed25519_sign(rng.integers(0, 256, size=(n, 32), dtype=np.uint8), msg)
+        sig = sig.copy()
+        bad = [0, 8191, 8192, 3 * 8192 + 5, n - 1]
+        sig[bad, 40] ^= 0x10
+
+        def pin(a):
+            h = eng.host_empty(a.shape, a.dtype)
+            h[...] = a
+            return h
+
+        pm, ps, pp = pin(msg), pin(sig), pin(pk)
+        pki = pin(ki) if committee else None
+        for _ in range(2):
+            st = eng.ed25519_verify(pm, ps, key_idx=pki) if committee else eng.ed25519_verify(pm, ps, pp)
+            assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
+        st2 = eng.ed25519_verify(msg, sig, key_idx=ki) if committee else eng.ed25519_verify(msg, sig, pk)
+        assert (st2 == st).all()

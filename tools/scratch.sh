@@ -1,2 +1,2 @@
 set -o pipefail
-bash tools/ab.sh orig main o3 orig main o3
+timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py -m gpu -x -q --timeout 200 --timeout-method thread 2>&1 | tail -3
