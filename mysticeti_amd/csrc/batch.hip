@@ -181,6 +181,13 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
               uint4* __restrict__ scal, unsigned long long* __restrict__ bsum, uint8_t* __restrict__ status,
               uint32_t blk0, uint32_t group_sigs) {
   __shared__ unsigned long long sbsum[BSUM_WORDS];
+  // A, s and z wait in LDS across the decodes ([word][thread]: no bank conflicts), so each
+  // input byte is read from HBM once and none of them holds registers during the chains. A
+  // compiler memory barrier before each read-back keeps the compiler from forwarding the
+  // thread's own stores (which would keep the values live in registers after all); volatile
+  // would not do: it turns the accesses into 64-bit-addressed flat ones
+  __shared__ uint32_t va[8][256], vs[8][256], vz[4][256];
+  const uint32_t t = threadIdx.x;
   if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t blk = blockIdx.x + blk0;  // launches may cover a chunk of the batch
@@ -195,6 +202,11 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
   load8(sw, sig + 64 * (size_t)idx + 32);
   load8(mw, msg + 32 * (size_t)idx);
   const bool s_ok = sc_is_canonical(sw);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    va[i][t] = aw[i];
+    vs[i][t] = sw[i];
+  }
   // scalars first (cheap, and their inputs die before the long decode):
   // k = SHA-512(R || A || M) mod l, z = BLAKE2b(secret || call || i) < 2^127, z k mod l
   uint32_t z[4], zk[8];
@@ -232,6 +244,8 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     sc_muladd(zk, z8, k, zero);
   }
   uint4* sc = scal + (size_t)idx * SC_QUADS;
+#pragma unroll
+  for (int i = 0; i < 4; i++) vz[i][t] = z[i];
   if (live) {
     sc[0] = make_uint4(z[0], z[1], z[2], z[3]);
     sc[1] = make_uint4(zk[0], zk[1], zk[2], zk[3]);
@@ -263,7 +277,9 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     decompress1_lean(P, okR, rw);
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, gid, pc);
-    load8(aw, pk + 32 * (size_t)kid);  // reloaded: not held across R's decode
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; i++) aw[i] = va[i][t];  // from LDS: not held across R's decode
     decompress1_lean(P, okA, aw);
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, (size_t)n + gid, pc);
@@ -287,16 +303,12 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     }
     status[gid] = !okA ? 2 : (ok ? 0 : 1);
   }
-  // z and s were stored / are in HBM: reload them rather than hold 12 registers
-  // across the decode
-  {
-    const uint4 q = sc[0];
-    z[0] = ok ? q.x : 0u;
-    z[1] = ok ? q.y : 0u;
-    z[2] = ok ? q.z : 0u;
-    z[3] = ok ? q.w : 0u;
-    load8(sw, sig + 64 * (size_t)idx + 32);
-  }
+  // z and s from LDS rather than 12 registers held across the decodes
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 4; i++) z[i] = ok ? vz[i][t] : 0u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) sw[i] = vs[i][t];
   // z * s (12 words, not reduced), summed per workgroup
   {
     uint64_t acc = 0;
