@@ -583,8 +583,11 @@ struct BlockItem {
 
 mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint64_t lo, uint64_t hi) {
   HIPCHK(ctx, hipSetDevice(dev.id));
+  static const bool trace = getenv("MV_BLK_TRACE") != nullptr;  // diagnostics: host-side times
+  auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   uint64_t i = lo;
   while (i < hi) {
+    const double t0 = trace ? now() : 0;
     uint64_t j = i, bytes = 0;
     while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += (it[j++].len + 7) & ~7ull;
     const uint32_t m = (uint32_t)(j - i);
@@ -608,15 +611,22 @@ mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint
     HIPCHK(ctx, dev.bytes.ensure(total));
     HIPCHK(ctx, dev.out2.ensure(65 * (size_t)m + 256));
     HIPCHK(ctx, dev.h_out.ensure(65 * (size_t)m));
+    const double t1 = trace ? now() : 0;
     HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
+    const double t2 = trace ? now() : 0;
     uint8_t* dout = dev.out2.as<uint8_t>();
     const uint8_t* dbuf = dev.bytes.as<uint8_t>();
     mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
                                   (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
                                   dout + 32 * (size_t)m, dev.stream);
     if (st != MV_OK) return st;
+    const double t3 = trace ? now() : 0;
     HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
+    const double t4 = trace ? now() : 0;
     HIPCHK(ctx, hipStreamSynchronize(dev.stream));
+    if (trace)
+      fprintf(stderr, "[blk] %u blocks: pack %.1f, h2d %.1f, kernels %.1f, d2h %.1f, wait %.1f us\n", m, t1 - t0,
+              t2 - t1, t3 - t2, t4 - t3, now() - t4);
     poll_flags(ctx, dev);
     const uint8_t* ho = dev.h_out.as<uint8_t>();
     for (uint32_t k = 0; k < m; k++) {
