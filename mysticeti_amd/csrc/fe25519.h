@@ -116,7 +116,15 @@ MV_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
     return c;
   });
 }
-MV_DEV void fe_sq(fe& r, const fe& a) {
+MV_DEV void fe_sq(fe& r, const fe& a_in) {
+  // opaque limbs: otherwise the compiler rebuilds 2a from the producer's unmasked column
+  // ((c << 1) & 0x3ffffffe beside c & 0x1fffffff: one extra instruction per limb)
+  fe a;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    a.v[i] = a_in.v[i];
+    asm("" : "+v"(a.v[i]));
+  }
   uint32_t a2[9];
 #pragma unroll
   for (int i = 0; i < 9; i++) a2[i] = a.v[i] << 1;  // < 2^31.01
