@@ -135,8 +135,9 @@ def cpu_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, sample: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # default timed region >= 2 s (600 steps of ~3.5 ms; BASELINE.md 2: DVFS settles)
+    ap.add_argument("--steps", type=int, default=600)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20, help="0 disables the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true")
@@ -233,9 +234,6 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if args.path == "batch":
-        eng.stage_times(reset=True)
-        eng.set_stage_timing(True)  # HIP events around every stage, on the launch streams
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev_side = [torch.cuda.Event() for _ in range(nstreams)]
 
@@ -258,6 +256,13 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # device time per step on the launch streams
     stage_ms = {}
     if args.path == "batch":
+        # the as-run stage table: HIP events around every stage of a few more steps on the same
+        # alternating streams, after the timed region (the events stay out of `value`)
+        eng.stage_times(reset=True)
+        eng.set_stage_timing(True)
+        for _ in range(max(2 * nstreams, min(args.steps, 20))):
+            step()
+        torch.cuda.synchronize(dev)
         tot, calls = eng.stage_times()
         eng.set_stage_timing(False)
         stage_ms = {k: v / calls[k] for k, v in tot.items() if calls[k]}
@@ -345,7 +350,7 @@ def main():
             for _ in range(3):
                 adv_step()
             c0 = eng.batch_counters()
-            k = max(4, args.steps // 2)
+            k = max(4, min(args.steps // 2, 200))
             e = timed_region(adv_step, k, lambda: torch.cuda.synchronize(dev), dist)
             c1 = eng.batch_counters()
             good = all((x.cpu().numpy() == want).all() for x in d_status)
@@ -397,7 +402,8 @@ def main():
         import bench_blocks
 
         cfg4 = bench_blocks.config4_measure(eng, torch, local_rank, world, dist, n=args.config4_batch,
-                                            steps=args.steps, warmup=args.warmup, nstreams=nstreams,
+                                            steps=max(3, min(args.steps, 100)), warmup=max(1, min(args.warmup, 3)),
+                                            nstreams=nstreams,
                                             cpu=args.cpu_sample > 0)
         ok = ok and cfg4["correct"]
 
@@ -407,7 +413,7 @@ def main():
         import bench_wal
 
         walr = bench_wal.wal_measure(eng, torch, local_rank, world, dist, n=args.wal_entries,
-                                     steps=max(3, args.steps // 4), warmup=1, cpu=args.cpu_sample > 0)
+                                     steps=max(3, min(args.steps // 4, 50)), warmup=1, cpu=args.cpu_sample > 0)
         ok = ok and walr["correct"]
 
     out = None

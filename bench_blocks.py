@@ -293,9 +293,13 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    elapsed = timed_region(step, steps, lambda: torch.cuda.synchronize(dev), dist)
+    # the as-run stage table: stage events on a few more alternating steps (kept out of `value`)
     eng.stage_times(reset=True)
     eng.set_stage_timing(True)
-    elapsed = timed_region(step, steps, lambda: torch.cuda.synchronize(dev), dist)
+    for _ in range(max(2 * nstreams, min(steps, 6))):
+        step()
+    torch.cuda.synchronize(dev)
     tot, calls = eng.stage_times()
     eng.set_stage_timing(False)
     stage_ms = {k: round(v / calls[k], 4) for k, v in tot.items() if calls[k]}

@@ -103,9 +103,13 @@ def wal_measure(eng, torch, local_rank, world, dist, n: int, steps: int, warmup:
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    elapsed = timed_region(step, steps, lambda: torch.cuda.synchronize(dev), dist)
+    # stage events on a few more steps (kept out of `value`)
     eng.stage_times(reset=True)
     eng.set_stage_timing(True)
-    elapsed = timed_region(step, steps, lambda: torch.cuda.synchronize(dev), dist)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
     tot, calls = eng.stage_times()
     eng.set_stage_timing(False)
     stage_ms = {k: round(tot[k] / calls[k], 4) for k in ("wal_walk", "wal_crc") if calls[k]}
