@@ -866,7 +866,6 @@ struct BatchLayout {
       flag, total;
   BatchLayout(uint32_t n, uint32_t groups) {
     using namespace mv;
-    const size_t nblk = (n + 255) / 256;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += align256(bytes); return r; };
     pts = take((size_t)2 * n * PT_QUADS * 16);
