@@ -872,9 +872,17 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dev.committee_pk.as<uint8_t>(),
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), cs,
                                  nullptr, &gate);
-    if (rc != MV_OK) return rc;
-    HIPCHK(ctx, hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, cs));
-    HIPCHK(ctx, hipEventRecord(dev.pin_free[b], cs));
+    hipError_t e = rc == MV_OK ? hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, cs)
+                               : hipSuccess;
+    if (e == hipSuccess && rc == MV_OK) e = hipEventRecord(dev.pin_free[b], cs);
+    if (rc != MV_OK || e != hipSuccess) {
+      // drain what was queued (it reads the input buffers and writes h_out) before returning
+      (void)hipStreamSynchronize(xs);
+      (void)hipStreamSynchronize(dev.pstream[0]);
+      (void)hipStreamSynchronize(dev.pstream[1]);
+      if (rc != MV_OK) return rc;
+      return set_err(ctx, MV_E_HIP, std::string("streamed verify: ") + hipGetErrorString(e));
+    }
   }
   HIPCHK(ctx, hipStreamSynchronize(dev.pstream[0]));
   HIPCHK(ctx, hipStreamSynchronize(dev.pstream[1]));
