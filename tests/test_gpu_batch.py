@@ -242,6 +242,9 @@ def test_adaptive_guard_after_a_failed_batch():
         assert d == (1, 1, 8, 1)
         st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, sig, pk))
         assert (st == 0).all() and d == (1, 0, 8, 0)
+        eng.set_batch_groups(0)  # setting the policy clears the guard: one equation again
+        st, d = counters_delta(eng, lambda: eng.ed25519_verify(msg, sig, pk))
+        assert (st == 0).all() and d == (1, 0, 1, 0)
 
 
 @pytest.mark.parametrize("pinned", [False, True])
