@@ -194,8 +194,9 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* __restrict__
 //   k_hash_comb_pre  workgroups [0, nh): quad BLAKE2b of 16 blocks each (blake2b_quad.h);
 //                    [nh, nh + np): s < l and the ZIP-215 decode of R, 64 signatures each;
 //                    [nh + np, nh + 2 np): -[s]B on C_B, 64 signatures each
-//   k_comb_post (8 waves): k = SHA-512(R || A || M) mod l on every wave; wave w: the A-table
-//                    entries of k's digits 4w .. 4w + 3 (4 additions), wave 7 also R - [s]B;
+//   k_comb_post (8 waves): k = SHA-512(R || A || M) mod l on wave 0 (alone on its SIMD; wave 7
+//                    meanwhile R - [s]B), digits through LDS; wave w: the A-table entries of
+//                    k's digits 4w .. 4w + 3 (4 additions);
 //                    a 3-level tree over the waves' sums; wave 0: R - [s]B - sum (the tables
 //                    hold -A), [8], identity test.
 // k_comb_post's latency is a SHA-512 and 4 + 5 additions instead of the R decode.
@@ -256,13 +257,14 @@ __global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __
                                                               const uint8_t* __restrict__ qflags,
                                                               uint8_t* __restrict__ status) {
   __shared__ uint4 part[POST_WAVES][9][64];  // per-wave partial sums, [quad][lane]
+  __shared__ uint32_t skd[8][64];            // k's signed radix-256 digits, [word][lane]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t gid = blockIdx.x * 64 + lane;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
   uint4 q[9];
   p3 acc, X;
-  {
+  if (wave == 0) {  // k = SHA-512(R || A || M) mod l once, alone on its SIMD
     uint32_t kin[24], h[16], k[8], kd[8];
     load8(kin, sig + 64 * (size_t)idx);
     load8(kin + 8, pk + 32 * (size_t)key);
@@ -270,10 +272,9 @@ __global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __
     sha512_short(h, kin, 96);
     sc_reduce512(k, h);
     sc_recode256(kd, k);
-    const int r0 = wave * (CT_ROWS / POST_WAVES);
-    ct_sum(acc, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / POST_WAVES);  // -[k_w]A
-  }
-  if (wave == POST_WAVES - 1) {  // also R - [s]B (k_hash_comb_pre), into the spare slot 0
+#pragma unroll
+    for (int i = 0; i < 8; i++) skd[i][lane] = kd[i];
+  } else if (wave == POST_WAVES - 1) {  // meanwhile R - [s]B (k_hash_comb_pre), into the spare slot 0
     p3 R;
 #pragma unroll
     for (int k = 0; k < 9; k++) q[k] = rbuf[(size_t)idx * 9 + k];
@@ -285,6 +286,14 @@ __global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __
     p3_to_quads(q, R);
 #pragma unroll
     for (int k = 0; k < 9; k++) part[0][k][lane] = q[k];
+  }
+  __syncthreads();
+  {
+    uint32_t kd[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) kd[i] = skd[i][lane];
+    const int r0 = wave * (CT_ROWS / POST_WAVES);
+    ct_sum(acc, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / POST_WAVES);  // -[k_w]A
   }
   // tree over the waves' partial sums: wave w < h adds wave w + h's
   for (int h = POST_WAVES / 2; h >= 1; h >>= 1) {
