@@ -612,10 +612,24 @@ mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint
     HIPCHK(ctx, dev.out2.ensure(65 * (size_t)m + 256));
     HIPCHK(ctx, dev.h_out.ensure(65 * (size_t)m));
     const double t1 = trace ? now() : 0;
-    HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
+    // small passes (the online path): the ingest kernel reads the pinned staging over PCIe
+    // itself (zero-copy) instead of waiting for an H2D copy and the launch behind it
+    static const uint64_t zc_max = [] {  // MV_BLK_ZEROCOPY=<bytes> (experiments; 0 = always copy)
+      const char* e = getenv("MV_BLK_ZEROCOPY");
+      return e ? (uint64_t)atoll(e) : (uint64_t)(1u << 20);
+    }();
+    const uint8_t* dbuf = nullptr;
+    if (total <= zc_max) {
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess && dp) dbuf = static_cast<const uint8_t*>(dp);
+      else (void)hipGetLastError();
+    }
+    if (!dbuf) {
+      HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
+      dbuf = dev.bytes.as<uint8_t>();
+    }
     const double t2 = trace ? now() : 0;
     uint8_t* dout = dev.out2.as<uint8_t>();
-    const uint8_t* dbuf = dev.bytes.as<uint8_t>();
     mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
                                   (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
                                   dout + 32 * (size_t)m, dev.stream);
