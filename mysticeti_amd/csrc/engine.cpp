@@ -619,23 +619,32 @@ mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint
       return e ? (uint64_t)atoll(e) : (uint64_t)(1u << 20);
     }();
     const uint8_t* dbuf = nullptr;
+    uint8_t* hout_dev = nullptr;  // zero-copy outputs too: the kernels write the pinned h_out
     if (total <= zc_max) {
       void* dp = nullptr;
-      if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess && dp) dbuf = static_cast<const uint8_t*>(dp);
-      else (void)hipGetLastError();
+      void* dq = nullptr;
+      // outputs only under the comb path: the batch path re-reads the digests many times
+      const bool zc_out = m < MV_BATCH_MIN;
+      if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess && dp &&
+          (!zc_out || (hipHostGetDevicePointer(&dq, dev.h_out.p, 0) == hipSuccess && dq))) {
+        dbuf = static_cast<const uint8_t*>(dp);
+        hout_dev = static_cast<uint8_t*>(dq);
+      } else {
+        (void)hipGetLastError();
+      }
     }
     if (!dbuf) {
       HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
       dbuf = dev.bytes.as<uint8_t>();
     }
     const double t2 = trace ? now() : 0;
-    uint8_t* dout = dev.out2.as<uint8_t>();
+    uint8_t* dout = hout_dev ? hout_dev : dev.out2.as<uint8_t>();
     mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
                                   (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
                                   dout + 32 * (size_t)m, dev.stream);
     if (st != MV_OK) return st;
     const double t3 = trace ? now() : 0;
-    HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
+    if (!hout_dev) HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
     const double t4 = trace ? now() : 0;
     HIPCHK(ctx, hipStreamSynchronize(dev.stream));
     if (trace)
