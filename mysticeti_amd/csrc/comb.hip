@@ -37,6 +37,7 @@
 #include "tables.h"
 #include "comb.h"
 #include "blake2b_quad.h"
+#include "block_verdict.h"
 
 namespace mv {
 
@@ -112,11 +113,20 @@ MV_DEV void ct_acc(p3& P, const p3& Q) {
   p1p1_to_p3(P, t);
 }
 
-__global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* __restrict__ msg, const uint8_t* __restrict__ sig,
+// the signature status of block gid, or its block verdict when the kernel carries it
+MV_DEV void put_status(uint8_t* status, const mvk::BlockVerdictOut& bv, uint32_t gid, uint8_t sig_status) {
+  if (bv.status)
+    bv.status[gid] = block_verdict(bv.facts, bv.claimed, bv.msg_digest, bv.digest, sig_status, gid);
+  else
+    status[gid] = sig_status;
+}
+
+__global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* msg, const uint8_t* __restrict__ sig,
                                                      const uint8_t* __restrict__ pk, const uint32_t* __restrict__ key_idx,
                                                      uint32_t n, const uint4* __restrict__ combB,
                                                      const uint4* __restrict__ combA,
-                                                     const uint8_t* __restrict__ key_ok, uint8_t* __restrict__ status) {
+                                                     const uint8_t* __restrict__ key_ok, uint8_t* __restrict__ status,
+                                                     const mvk::BlockVerdictOut bv) {
   __shared__ uint4 part[3][9][64];  // partial sums of waves 1..3, [quad][lane]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t gid = blockIdx.x * 64 + lane;
@@ -183,7 +193,7 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* __restrict__
       p1p1_to_p2(P, t);
     }
     const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
-    if (gid < n) status[gid] = !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1);
+    if (gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
   }
 }
 
@@ -246,7 +256,7 @@ __global__ void __launch_bounds__(64) k_hash_comb_pre(const uint8_t* __restrict_
 }
 
 constexpr int POST_WAVES = 8;
-__global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __restrict__ msg,
+__global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* msg,  // not restrict: bv writes it
                                                               const uint8_t* __restrict__ sig,
                                                               const uint8_t* __restrict__ pk,
                                                               const uint32_t* __restrict__ key_idx, uint32_t n,
@@ -255,7 +265,8 @@ __global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __
                                                               const uint4* __restrict__ rbuf,
                                                               const uint4* __restrict__ sbuf,
                                                               const uint8_t* __restrict__ qflags,
-                                                              uint8_t* __restrict__ status) {
+                                                              uint8_t* __restrict__ status,
+                                                              const mvk::BlockVerdictOut bv) {
   __shared__ uint4 part[POST_WAVES][9][64];  // per-wave partial sums, [quad][lane]
   __shared__ uint32_t skd[8][64];            // k's signed radix-256 digits, [word][lane]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -329,7 +340,7 @@ __global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* __
     }
     const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
     const uint8_t f = qflags[idx];
-    if (gid < n) status[gid] = !key_ok[key] ? 2 : (((f & 3) == 3 && ident) ? 0 : 1);
+    if (gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : (((f & 3) == 3 && ident) ? 0 : 1));
   }
 }
 
@@ -349,10 +360,11 @@ hipError_t launch_comb_init(const uint8_t* enc, uint32_t nb, int negate, void* t
 
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
-                              uint8_t* status, hipStream_t s) {
+                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv) {
   if (n == 0) return hipSuccess;
+  const BlockVerdictOut none{};
   hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                     (const uint4*)combB, (const uint4*)combA, key_ok, status);
+                     (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);
   return hipGetLastError();
 }
 
@@ -368,10 +380,12 @@ hipError_t launch_hash_comb_pre(const uint8_t* stage, const uint64_t* poff, cons
 
 hipError_t launch_comb_post(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                             uint32_t n, const void* combA, const uint8_t* key_ok, const void* rbuf,
-                            const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s) {
+                            const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s,
+                            const BlockVerdictOut* bv) {
   if (n == 0) return hipSuccess;
+  const BlockVerdictOut none{};
   hipLaunchKernelGGL(mv::k_comb_post, dim3((n + 63) / 64), dim3(64 * mv::POST_WAVES), 0, s, msg, sig, pk, key_idx, n,
-                     (const uint4*)combA, key_ok, (const uint4*)rbuf, (const uint4*)sbuf, qflags, status);
+                     (const uint4*)combA, key_ok, (const uint4*)rbuf, (const uint4*)sbuf, qflags, status, bv ? *bv : none);
   return hipGetLastError();
 }
 

@@ -355,11 +355,13 @@ mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const u
 
 // Committee-key signatures one by one: comb tables (comb.hip) or, with MV_FLAG_NO_COMB,
 // the per-signature ladder (k_verify).
+// bv: the block verdict fused into the comb kernel (the block path); null otherwise.
 mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig,
-                                   const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s) {
+                                   const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s,
+                                   const mvk::BlockVerdictOut* bv = nullptr) {
   if (!(ctx->flags & MV_FLAG_NO_COMB)) {
     HIPCHK(ctx, mvk::launch_verify_comb(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
-                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s));
+                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv));
   } else {
     return enqueue_verify(ctx, dev, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, d_status, s);
   }
@@ -442,17 +444,25 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   // per-signature paths need no gate: the verdict puts the digest first)
   if (batch) HIPCHK(ctx, mvk::launch_block_digest_gate(claimed, bd, facts, n, sig, s));
   HIPCHK(ctx, mark(2));
+  // the comb kernels write the block verdict themselves (one launch less on the online path);
+  // the batch path and the MV_FLAG_NO_COMB ladder leave it to k_block_verdict
+  static const bool fuse_env = [] {  // MV_VERDICT_FUSED=0: the separate k_block_verdict (A/B)
+    const char* e = getenv("MV_VERDICT_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  const bool fused = fuse_env && !batch && !(ctx->flags & MV_FLAG_NO_COMB);
+  const mvk::BlockVerdictOut bv{facts, claimed, md, bd, d_status};
   if (batch) {
     st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, nullptr);
   } else if (split) {
     HIPCHK(ctx, mvk::launch_comb_post(md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, dev.combA.p,
-                                      dev.keyok.as<uint8_t>(), rbuf, sbuf, qflags, sst, s));
+                                      dev.keyok.as<uint8_t>(), rbuf, sbuf, qflags, sst, s, fused ? &bv : nullptr));
   } else {
-    st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s);
+    st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s, fused ? &bv : nullptr);
   }
   if (st != MV_OK) return st;
   HIPCHK(ctx, mark(3));
-  HIPCHK(ctx, mvk::launch_block_verdict(facts, claimed, md, bd, sst, n, d_status, s));
+  if (!fused) HIPCHK(ctx, mvk::launch_block_verdict(facts, claimed, md, bd, sst, n, d_status, s));
   HIPCHK(ctx, mark(4));
   keep_events(ctx, dev.id, kBlockStage0, evs);
   HIPCHK(ctx, hipEventRecord(dev.blk_done[slot], s));

@@ -21,13 +21,11 @@
 
 #include "../../include/mysti_verify.h"
 #include "hash_dev.h"
+#include "block_verdict.h"
 #include "kernels.h"
 
 namespace mv {
 
-constexpr uint32_t BF_PARSED = 1u, BF_EPOCH_OK = 2u, BF_AUTHOR_OK = 4u, BF_GENESIS = 8u, BF_QUORUM = 32u;
-constexpr int BF_INC_SHIFT = 8;               // first failing include: MV_BLOCK_INCLUDE_* or 0
-constexpr int BF_VR_SHIFT = 16;               // first failing VoteRange: vr_code() or 0
 constexpr uint64_t VR_MAX_LEN = 1024 * 1024;  // VoteRange::verify MAX_LEN (types.rs:448)
 
 // VoteRange::verify (types.rs:440-460), its checks in order: 1 = end < start, 2 = length
@@ -683,14 +681,6 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
   }
 }
 
-MV_DEV bool digest_same(const uint8_t* claimed, const uint8_t* digest, uint32_t i) {
-  const uint4* a = reinterpret_cast<const uint4*>(claimed + 32 * (size_t)i);
-  const uint4* b = reinterpret_cast<const uint4*>(digest + 32 * (size_t)i);
-  const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
-  return ((a0.x ^ b0.x) | (a0.y ^ b0.y) | (a0.z ^ b0.z) | (a0.w ^ b0.w) | (a1.x ^ b1.x) | (a1.y ^ b1.y) |
-          (a1.z ^ b1.z) | (a1.w ^ b1.w)) == 0;
-}
-
 // Between the hashes and the signature check: a parsed block whose digest differs from the
 // claimed one gets DIGEST_MISMATCH whatever its signature (types.rs:327-332 comes before the
 // signature check at :346-348), so its s is set to 2^256 - 1 (>= l): it is then excluded
@@ -706,8 +696,7 @@ __global__ void __launch_bounds__(256) k_block_digest_gate(const uint8_t* __rest
   s4[1] = make_uint4(~0u, ~0u, ~0u, ~0u);
 }
 
-// status[i] in the order of StatementBlock::verify (types.rs:315-376). A block that does not
-// deserialize has no pre-image: its two digests are zeroed, so every output is deterministic.
+// status[i] in the order of StatementBlock::verify (types.rs:315-376), block_verdict.h
 __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restrict__ facts,
                                                        const uint8_t* __restrict__ claimed,
                                                        uint8_t* __restrict__ msg_digest,
@@ -716,34 +705,7 @@ __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restric
                                                        uint8_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t f = facts[i];
-  uint8_t st;
-  if (!(f & BF_PARSED)) {
-    st = MV_BLOCK_PARSE_ERROR;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    uint4* m4 = reinterpret_cast<uint4*>(msg_digest + 32 * (size_t)i);
-    uint4* d4 = reinterpret_cast<uint4*>(digest + 32 * (size_t)i);
-    m4[0] = z;
-    m4[1] = z;
-    d4[0] = z;
-    d4[1] = z;
-  } else {
-    const bool same = digest_same(claimed, digest, i);
-    const uint32_t inc = (f >> BF_INC_SHIFT) & 0xffu;
-    const uint32_t vr = (f >> BF_VR_SHIFT) & 3u;
-    st = !same                      ? MV_BLOCK_DIGEST_MISMATCH
-         : !(f & BF_EPOCH_OK)       ? MV_BLOCK_EPOCH_MISMATCH
-         : !(f & BF_AUTHOR_OK)      ? MV_BLOCK_UNKNOWN_AUTHOR
-         : (f & BF_GENESIS)         ? MV_BLOCK_GENESIS
-         : sig_status[i] != MV_SIG_OK ? MV_BLOCK_SIG_INVALID
-         : inc                      ? (uint8_t)inc
-         : vr == 1                  ? MV_BLOCK_VOTE_RANGE
-         : vr == 2                  ? MV_BLOCK_VOTE_RANGE_TOO_LONG
-         : vr == 3                  ? MV_BLOCK_VOTE_RANGE_END_TOO_LARGE
-         : !(f & BF_QUORUM)         ? MV_BLOCK_THRESHOLD_CLOCK
-                                    : MV_BLOCK_OK;
-  }
-  status[i] = st;
+  status[i] = block_verdict(facts, claimed, msg_digest, digest, sig_status[i], i);
 }
 
 }  // namespace mv

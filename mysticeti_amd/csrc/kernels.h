@@ -68,9 +68,19 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
 // enc == nullptr builds the table of B; negate = 1 stores -P (committee keys).
 size_t comb_table_bytes(uint32_t nbases);
 hipError_t launch_comb_init(const uint8_t* enc, uint32_t nb, int negate, void* tab, uint8_t* ok, hipStream_t s);
+// the block verdict (block_verdict.h) fused into a committee signature kernel's last step on
+// the online block path, which then writes status[] instead of the signature status: one
+// launch less. Null: signature status only.
+struct BlockVerdictOut {
+  const uint32_t* facts;
+  const uint8_t* claimed;
+  uint8_t* msg_digest;
+  uint8_t* digest;
+  uint8_t* status;
+};
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
-                              uint8_t* status, hipStream_t s);
+                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr);
 // the comb verify split in two, for small batches of long blocks: k_hash_comb_pre is
 // launch_block_hash plus, on workgroups of their own, the signature-only terms (R decoded ->
 // rbuf, -[s]B -> sbuf, 144 B per signature each, flags: bit 0 s < l, bit 1 R decodes);
@@ -80,7 +90,8 @@ hipError_t launch_hash_comb_pre(const uint8_t* stage, const uint64_t* poff, cons
                                 void* sbuf, uint8_t* qflags, hipStream_t s);
 hipError_t launch_comb_post(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                             uint32_t n, const void* combA, const uint8_t* key_ok, const void* rbuf,
-                            const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s);
+                            const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s,
+                            const BlockVerdictOut* bv = nullptr);
 // ingest.hip: device-side bincode parse + pre-image staging, and the final block verdict
 hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
