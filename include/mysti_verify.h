@@ -33,7 +33,9 @@
  *     The library copies host inputs into its own pinned staging and device memory.
  *   - Return value: MV_OK (0) or a negative MV_E_* code; mv_last_error() gives text.
  *     Per-item verdicts go to caller arrays: a rejected signature is not an error.
- *   - All calls are synchronous and thread-safe on one context (serialised internally).
+ *   - Host-buffer calls are synchronous and thread-safe on one context. mv_verify_blocks callers
+ *     are coalesced (a submission queue merges concurrent calls into shared device passes);
+ *     the other host-buffer calls take the context in turn.
  *   - A context spans the devices in mv_config.device_mask; host-buffer calls shard
  *     their items across them (no collective: each device returns its slice of verdicts).
  */
@@ -188,9 +190,10 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
                                 const uint8_t* d_pk, uint32_t n, uint8_t* d_status, void* stream);
 /* Batch path on device buffers: verdicts identical to mv_dev_ed25519_verify. The combined
  * equation [8](-[sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i) == O with secret random
- * 127-bit z_i (BLAKE2b PRF keyed per context and call) is checked first; if it fails, every
- * signature is re-verified individually on the same stream, so each verdict is exact (an
- * invalid signature survives a passing combination with probability <= 2^-127).
+ * 127-bit z_i (BLAKE2b PRF keyed per context and call) is checked first, per sub-batch group
+ * (mv_set_batch_groups); the signatures of every group whose equation fails are re-verified
+ * individually on the same stream, so each verdict is exact (an invalid signature survives a
+ * passing combination with probability <= 2^-127).
  * `d_pk` rows are indexed by item, or by `d_key_idx` (device array) when it is non-NULL; every
  * d_key_idx[i] must then be a row of d_pk (the library cannot bound-check device arrays).
  * Enqueues only; `d_batch_ok` (optional, device, 4 bytes) receives 1 if the combination held. */

@@ -22,6 +22,7 @@ pub const MV_E_INVALID_ARG: i32 = -1;
 pub const MV_E_HIP: i32 = -2;
 pub const MV_E_NO_DEVICE: i32 = -3;
 pub const MV_E_NO_COMMITTEE: i32 = -4;
+pub const MV_E_ALLOC: i32 = -5;
 
 pub const MV_SIG_OK: u8 = 0;
 pub const MV_SIG_INVALID: u8 = 1;
@@ -41,11 +42,16 @@ pub const MV_BLOCK_THRESHOLD_CLOCK: u8 = 10;
 pub const MV_BLOCK_VOTE_RANGE_TOO_LONG: u8 = 11;
 pub const MV_BLOCK_VOTE_RANGE_END_TOO_LARGE: u8 = 12;
 
+pub const MV_WAL_OK: u8 = 0;
+pub const MV_WAL_CRC_MISMATCH: u8 = 1;
+pub const MV_WAL_NONZERO_CRC_LEN0: u8 = 2;
+pub const MV_WAL_BAD_LENGTH: u8 = 3;
+
 pub const MV_FLAG_NO_BATCH: u32 = 1;
 pub const MV_FLAG_NO_COMB: u32 = 2;
 pub const MV_FLAG_HOST_PARSE: u32 = 4;
 pub const MV_BATCH_MIN: u32 = 4096;
-pub const MV_NSTAGES: usize = 10;
+pub const MV_NSTAGES: usize = 12;
 
 extern "C" {
     pub fn mv_create(cfg: *const mv_config, out: *mut *mut mv_ctx) -> i32;
@@ -58,6 +64,8 @@ extern "C" {
                          out: *mut u8) -> i32;
     pub fn mv_ed25519_verify(ctx: *mut mv_ctx, msg: *const u8, sig: *const u8, pk: *const u8,
                              key_idx: *const u32, n: u32, status: *mut u8) -> i32;
+    pub fn mv_host_alloc(ctx: *mut mv_ctx, bytes: u64, out: *mut *mut c_void) -> i32;
+    pub fn mv_host_free(ctx: *mut mv_ctx, p: *mut c_void);
     pub fn mv_ed25519_sign(ctx: *mut mv_ctx, seed: *const u8, msg: *const u8, n: u32, pk: *mut u8,
                            sig: *mut u8) -> i32;
     pub fn mv_verify_blocks(ctx: *mut mv_ctx, buf: *const u8, off: *const u64, len: *const u64, n: u32,
@@ -65,6 +73,12 @@ extern "C" {
     pub fn mv_block_preimage(bincode: *const u8, len: u64, out: *mut u8, cap: u64) -> i64;
     pub fn mv_queue_stats(ctx: *mut mv_ctx, calls: *mut u64, passes: *mut u64) -> i32;
     pub fn mv_shard_plan(weights: *const u64, n: u64, parts: u32, cut: *mut u64) -> i32;
+    pub fn mv_crc32(ctx: *mut mv_ctx, buf: *const u8, off: *const u64, len: *const u64, n: u32,
+                    out: *mut u32) -> i32;
+    pub fn mv_wal_verify(ctx: *mut mv_ctx, wal: *const u8, size: u64, end_pos: u64, map_bits: u32,
+                         pos: *mut u64, tag: *mut u32, len: *mut u32, status: *mut u8, cap: u64,
+                         count: *mut u64) -> i32;
+    pub fn mv_wal_layout(payload_len: *const u64, n: u64, map_bits: u32, start: u64, pos: *mut u64) -> u64;
     pub fn mv_dev_ed25519_verify(ctx: *mut mv_ctx, device: i32, d_msg: *const u8, d_sig: *const u8,
                                  d_pk: *const u8, n: u32, d_status: *mut u8, stream: *mut c_void) -> i32;
     pub fn mv_dev_ed25519_verify_batch(ctx: *mut mv_ctx, device: i32, d_msg: *const u8, d_sig: *const u8,
@@ -75,6 +89,11 @@ extern "C" {
     pub fn mv_dev_verify_blocks(ctx: *mut mv_ctx, device: i32, d_buf: *const u8, buf_bytes: u64,
                                 d_off: *const u64, d_len: *const u64, n: u32, d_status: *mut u8,
                                 d_msg_digest: *mut u8, d_block_digest: *mut u8, stream: *mut c_void) -> i32;
+    pub fn mv_dev_wal_verify(ctx: *mut mv_ctx, device: i32, d_wal: *const u8, size: u64, end_pos: u64,
+                             map_bits: u32, d_pos: *mut u64, d_tag: *mut u32, d_len: *mut u32,
+                             d_status: *mut u8, cap: u64, count: *mut u64, stream: *mut c_void) -> i32;
+    pub fn mv_dev_crc32(ctx: *mut mv_ctx, device: i32, d_buf: *const u8, d_off: *const u64, d_len: *const u64,
+                        n: u32, d_out: *mut u32, stream: *mut c_void) -> i32;
     pub fn mv_batch_stats(ctx: *mut mv_ctx, batches: *mut u64, fallbacks: *mut u64) -> i32;
     pub fn mv_batch_counters(ctx: *mut mv_ctx, out: *mut u64) -> i32;
     pub fn mv_set_batch_groups(ctx: *mut mv_ctx, groups: u32) -> i32;
