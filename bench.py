@@ -10,9 +10,12 @@ reported separately as `end_to_end`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S]
 
-N > 1: launched by torch.distributed.run, one rank per GPU; each rank verifies its
-own shard (weak scaling, no data-path collective); barrier + synchronize around the
-timed region, max time over ranks (gloo), value = all ranks' signatures / that time.
+N > 1: one rank per GPU under torch.distributed.run. Launched bare (`bench.py --gpus N`,
+no WORLD_SIZE), the script starts that launcher itself as a child process before any
+GPU call and exits with its code; under an external launcher WORLD_SIZE must equal N.
+Each rank verifies its own shard (weak scaling, no data-path collective); barrier +
+synchronize around the timed region, max time over ranks (gloo), value = all ranks'
+signatures / that time.
 """
 from __future__ import annotations
 
@@ -166,6 +169,15 @@ def main():
                     help="skip the WAL replay-check rate (row f4) in the default line")
     ap.add_argument("--wal-entries", type=int, default=1 << 20, help="WAL entries (config-4 blocks) per GPU")
     args = ap.parse_args()
+    from mysticeti_amd.dist import launch_ranks, needs_launch
+
+    if needs_launch(args.gpus):
+        # `bench.py --gpus N` without an external launcher: start the N ranks as a child
+        # torch.distributed.run (nothing here has touched the GPU) and exit with its code
+        return launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     if args.workload != "config2":
         import bench_blocks
 

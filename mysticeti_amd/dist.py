@@ -28,6 +28,39 @@ def init_gloo(dist) -> None:
         os.close(saved)
 
 
+def needs_launch(gpus: int, env=None) -> bool:
+    """True when `--gpus N` (N > 1) was asked for but this process is not a rank of a launched
+    job (no WORLD_SIZE): the bench must start its N ranks itself."""
+    import os
+
+    env = os.environ if env is None else env
+    return gpus > 1 and "WORLD_SIZE" not in env
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(script: str, argv, nproc: int, timeout: Optional[float] = None) -> int:
+    """Runs `script argv` as `nproc` ranks under torch.distributed.run (one process per GPU,
+    rendezvous on 127.0.0.1) as a CHILD process and returns its exit code. The caller must not
+    have touched the GPU: the ranks own the devices. stdout/stderr are inherited, so rank 0's
+    JSON line (the only stdout line: gloo's chatter goes to stderr, init_gloo) reaches the
+    caller's stdout as it is printed."""
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), script] + list(argv)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    return subprocess.run(cmd, timeout=timeout).returncode
+
+
 def shard_range(rank: int, world: int, per_rank: int) -> Tuple[int, int]:
     """Corpus indices owned by `rank` (weak scaling: `per_rank` items each)."""
     assert 0 <= rank < world and per_rank >= 0

@@ -84,3 +84,64 @@ def test_torchrun_stdout_is_one_json_line(tmp_path):
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
     assert json.loads(lines[0]) == {"world": 2, "ok": True}
+
+
+def test_needs_launch():
+    from mysticeti_amd.dist import needs_launch
+
+    assert not needs_launch(1, {})
+    assert needs_launch(2, {})
+    assert not needs_launch(8, {"WORLD_SIZE": "8"})
+
+
+def test_launch_ranks_starts_n_ranks_and_relays_rank0_line(tmp_path):
+    """bench.py --gpus N without an external launcher: dist.launch_ranks starts N ranks of the
+    script as a child torch.distributed.run (argv passed through) and returns its exit code;
+    the caller's stdout gets exactly rank 0's JSON line."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stub = tmp_path / "stub.py"
+    stub.write_text(
+        "import json, os, sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import torch.distributed as dist\n"
+        "from mysticeti_amd.dist import all_ranks_ok, init_gloo\n"
+        "init_gloo(dist)\n"
+        "ok = all_ranks_ok(True, dist)\n"
+        "if dist.get_rank() == 0:\n"
+        "    print(json.dumps({'n_gpus': dist.get_world_size(), 'argv': sys.argv[1:], 'ok': ok}), flush=True)\n"
+        "dist.destroy_process_group()\n"
+        "sys.exit(3 if '--fail' in sys.argv else 0)\n")
+    parent = tmp_path / "parent.py"
+    parent.write_text(
+        "import sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from mysticeti_amd.dist import launch_ranks, needs_launch\n"
+        "n = int(sys.argv[1])\n"
+        "assert needs_launch(n)\n"
+        f"sys.exit(launch_ranks({str(stub)!r}, ['--gpus', str(n)] + sys.argv[2:], n))\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(parent), "2", "--steps", "3"], capture_output=True, text=True,
+                       timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    assert json.loads(lines[0]) == {"n_gpus": 2, "argv": ["--gpus", "2", "--steps", "3"], "ok": True}
+    r = subprocess.run([sys.executable, str(parent), "2", "--fail"], capture_output=True, text=True,
+                       timeout=180, env=env)
+    assert r.returncode != 0
+
+
+def test_bench_refuses_a_world_that_differs_from_gpus():
+    """A launched rank whose WORLD_SIZE differs from --gpus stops before touching a device."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
