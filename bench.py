@@ -165,6 +165,12 @@ def main():
                     help="skip the config-4 (100-validator blocks) rate in the default line")
     ap.add_argument("--config4-batch", type=int, default=1 << 21,
                     help="config-4 blocks per GPU per step (2^21: BASELINE config 4's 16M blocks over 8 GPUs)")
+    ap.add_argument("--no-config5", dest="config5", action="store_false",
+                    help="skip the config-5 (online latency) key of the default line")
+    ap.add_argument("--config5-batches", type=int, default=2000,
+                    help="default line's config-5 leg: 64-block calls timed per shape")
+    ap.add_argument("--config5-seconds", type=float, default=2.0,
+                    help="default line's config-5 leg: seconds of concurrent 1-block callers per shape")
     ap.add_argument("--no-wal", dest="wal", action="store_false",
                     help="skip the WAL replay-check rate (row f4) in the default line")
     ap.add_argument("--wal-entries", type=int, default=1 << 20, help="WAL entries (config-4 blocks) per GPU")
@@ -428,6 +434,18 @@ def main():
                                      steps=max(3, min(args.steps // 4, 50)), warmup=1, cpu=args.cpu_sample > 0)
         ok = ok and walr["correct"]
 
+    # config 5 (the online path): latency of 64-block calls and concurrent 1-block callers through
+    # mv_verify_blocks on host buffers, GPU and CPU in the same run (bench_blocks.config5_measure);
+    # rank 0 only (the host CPU legs would otherwise compete across ranks)
+    cfg5 = None
+    if args.config5 and args.path == "batch" and not args.corrupt and rank == 0:
+        import bench_blocks
+
+        eng.set_batch_groups(args.groups)
+        cfg5 = bench_blocks.config5_measure(eng, batches=args.config5_batches, conc_seconds=args.config5_seconds,
+                                            cpu=args.cpu_sample > 0)
+        ok = ok and cfg5["correct"]
+
     out = None
     if rank == 0:
         cpu = None
@@ -477,6 +495,7 @@ def main():
             "sustained": sustained,
             "adversarial": adversarial,
             "config4": cfg4,
+            "config5": cfg5,
             "wal": walr,
             "end_to_end": e2e,
             "correct": bool(ok),

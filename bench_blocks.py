@@ -46,6 +46,7 @@ def _oracle_native():
     vp = ctypes.c_void_p
     lib.orc_block_verify_batch.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_uint32, ctypes.c_uint64,
                                            vp, vp, vp, ctypes.c_int]
+    lib.orc_block_verify_batch_c.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, vp, vp, ctypes.c_int]
     return lib
 
 
@@ -53,10 +54,11 @@ def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
 
 
-def _cpu_blocks(lib, buf, off, ln, pks, stakes, threads):
+def _cpu_blocks(comm, buf, off, ln, threads):
+    """oracle StatementBlock::verify of the blocks on `threads` host threads (committee keys
+    decoded once: `comm` is a _Committee)."""
     st = np.zeros(off.shape[0], dtype=np.uint8)
-    lib.orc_block_verify_batch(_p(buf), _p(off), _p(ln), off.shape[0], _p(pks), _p(stakes), pks.shape[0], 0,
-                               _p(st), None, None, threads)
+    comm.lib.orc_block_verify_batch_c(comm.ptr, _p(buf), _p(off), _p(ln), off.shape[0], _p(st), None, None, threads)
     return st
 
 
@@ -123,13 +125,74 @@ def run(args) -> int:
 
 
 # ------------------------------------------------------------------ config 5 (latency)
-def config5(args, eng, rank) -> int:
+def _native_driver():
+    """bench_native/concurrent.c (built here with gcc): N pthreads calling a verify function."""
+    src = os.path.join(ROOT, "bench_native", "concurrent.c")
+    out_dir = os.path.join(ROOT, "bench_native", "build")
+    so = os.path.join(out_dir, "libmv_conc.so")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        os.makedirs(out_dir, exist_ok=True)
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-pthread", "-o", so, src], check=True)
+    lib = ctypes.CDLL(so)
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    lib.mvb_concurrent.restype = u64
+    lib.mvb_concurrent.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, u32, u32, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_double, u64, vp, u64, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    return lib
+
+
+class _Committee:
+    """orc_committee of the native oracle: committee keys decoded once, as the reference's
+    Committee holds them (committee.rs:83-87)."""
+
+    def __init__(self, lib, pks, stakes):
+        vp = ctypes.c_void_p
+        lib.orc_committee_new.restype = vp
+        lib.orc_committee_new.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint64]
+        lib.orc_committee_free.argtypes = [vp]
+        self.lib, self._pks, self._stakes = lib, np.ascontiguousarray(pks), np.ascontiguousarray(stakes)
+        self.ptr = lib.orc_committee_new(_p(self._pks), _p(self._stakes), pks.shape[0], 0)
+        self.fn = ctypes.cast(lib.orc_block_verify_batch_c, vp).value
+
+    def close(self):
+        if self.ptr:
+            self.lib.orc_committee_free(self.ptr)
+            self.ptr = None
+
+
+def _drive(drv, kind, fn, ctx, packed, per_call, callers, inner_threads=1, seconds=0.0, max_calls=0):
+    """One mvb_concurrent run: latency summary, blocks/s, and whether every block was accepted."""
+    buf, off, ln = packed
+    cap = max(1, int(max_calls * callers) if max_calls else int(callers * seconds * 40000) + 1024)
+    lat = np.zeros(cap, dtype=np.float64)
+    wall, bad, err = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+    calls = drv.mvb_concurrent(kind, fn, ctx, _p(buf), _p(off), _p(ln), off.shape[0], per_call, callers,
+                               inner_threads, seconds, max_calls, _p(lat), cap, ctypes.byref(wall), ctypes.byref(bad),
+                               ctypes.byref(err))
+    r = _lat_summary(lat[:min(calls, cap)])
+    r["blocks_per_s"] = round(calls * per_call / wall.value, 1)
+    return r, bool(calls) and bad.value == 0 and err.value == 0
+
+
+def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None) -> dict:
+    """Config 5 on this rank's GPU: for config-1 and config-4 shaped blocks,
+      - 64-block calls of mv_verify_blocks one after another (host buffers, PCIe both ways):
+        p50/p99 over `batches` calls, beside the oracle's StatementBlock::verify of the same
+        64 blocks on one host core (the reference's sequential loop) and on the CPU share;
+      - `callers` concurrent 1-block callers for `conc_seconds` (one tokio task per peer,
+        net_sync.rs:214-221, 314-386): the GPU queue merges them; the CPU leg verifies each
+        block on the caller's own core (no pool).
+    Every caller is a pthread of bench_native/concurrent.c, so Python caps neither side."""
     import mysticeti_amd.blocks as MB
 
-    lib = _oracle_native() if args.cpu_sample > 0 else None
-    out = {"metric": "config5: 64-block batch verify latency, submit -> verdicts (mv_verify_blocks, host buffers)",
-           "unit": "us", "higher_is_better": False, "n_gpus": 1, "data": "synthetic (blocks signed on the GPU)",
-           "host_cpu": _host_cpu(), "shapes": {}}
+    drv = _native_driver()
+    olib = _oracle_native() if cpu else None
+    threads, share_src = _cpu_threads()
+    callers = callers or threads
+    mv_fn = ctypes.cast(eng.lib.mv_verify_blocks, ctypes.c_void_p).value
+    out = {"unit": "us", "host_cpu": _host_cpu(), "cpu_threads": threads, "cpu_threads_source": share_src,
+           "shapes": {}}
     ok = True
     for shape in ("config1", "config4"):
         if shape == "config1":
@@ -139,95 +202,55 @@ def config5(args, eng, rank) -> int:
             blocks = MB.config4(eng, rounds=4)
             pks, stakes = MB.committee(eng, 100, distinct=True)
         eng.set_committee(pks, stakes, 0)
-        batches = [MB.pack(blocks[i:i + 64]) for i in range(0, len(blocks) - 63, 64)]
-        for b in batches:  # warm-up + correctness
-            st, _, _ = eng.verify_blocks_packed(*b)
-            ok &= bool((st == 0).all())
-        lat = []
-        for it in range(args.batches):
-            b = batches[it % len(batches)]
-            t0 = time.perf_counter()
-            eng.verify_blocks_packed(*b)
-            lat.append(time.perf_counter() - t0)
-        res = {"gpu": _lat_summary(lat), "bincode_bytes_per_block": int(batches[0][2].mean())}
-        cpu_threads, share_src = _cpu_threads()
-        if lib is not None:
-            for threads, nb in ((1, 100 if shape == "config4" else 300), (cpu_threads, 1500)):
-                clat = []
-                for it in range(nb):
-                    buf, off, ln = batches[it % len(batches)]
-                    t0 = time.perf_counter()
-                    st = _cpu_blocks(lib, buf, off, ln, pks, stakes, threads)
-                    clat.append(time.perf_counter() - t0)
-                    ok &= bool((st == 0).all())
-                res[f"cpu_{threads}t"] = _lat_summary(clat)
-            res["cpu_threads_source"] = share_src
-            res["gpu_vs_cpu_p50"] = {k: round(res[k]["p50_us"] / res["gpu"]["p50_us"], 2)
-                                     for k in res if k.startswith("cpu_") and isinstance(res[k], dict)}
-        # the online path as the reference has it: one tokio task per peer verifying the ~1
-        # block each message carries (net_sync.rs:214-221, 314-386). N concurrent callers each
-        # submit one block at a time; the GPU queue merges them (mv_verify_blocks), the CPU
-        # leg verifies each block on the caller's own core.
-        conc = _concurrent(eng, lib, blocks, pks, stakes, callers=cpu_threads, seconds=args.conc_seconds)
-        ok &= conc.pop("ok")
+        nb = (len(blocks) // 64) * 64
+        packed = MB.pack(blocks[:nb])
+        res = {"bincode_bytes_per_block": int(packed[2].mean())}
+        _drive(drv, 0, mv_fn, eng.ctx, packed, 64, 1, max_calls=max(8, nb // 64))  # warm-up
+        res["gpu"], g = _drive(drv, 0, mv_fn, eng.ctx, packed, 64, 1, max_calls=batches)
+        ok &= g
+        comm = _Committee(olib, pks, stakes) if olib is not None else None
+        if comm is not None:
+            n1 = 100 if shape == "config4" else 300
+            res["cpu_1t"], c1 = _drive(drv, 1, comm.fn, comm.ptr, packed, 64, 1, inner_threads=1, max_calls=n1)
+            _drive(drv, 1, comm.fn, comm.ptr, packed, 64, 1, inner_threads=threads, max_calls=50)  # pool up
+            res[f"cpu_{threads}t"], c2 = _drive(drv, 1, comm.fn, comm.ptr, packed, 64, 1, inner_threads=threads,
+                                                max_calls=max(200, batches // 4))
+            ok &= c1 and c2
+            res["cpu_p50_over_gpu_p50"] = {k: round(res[k]["p50_us"] / res["gpu"]["p50_us"], 3)
+                                           for k in ("cpu_1t", f"cpu_{threads}t")}
+        # concurrent 1-block callers
+        conc = {"callers": callers, "seconds": conc_seconds}
+        q0 = eng.queue_stats()
+        conc["gpu"], g = _drive(drv, 0, mv_fn, eng.ctx, packed, 1, callers, seconds=conc_seconds)
+        q1 = eng.queue_stats()
+        conc["gpu"]["calls_per_device_pass"] = round((q1[0] - q0[0]) / max(1, q1[1] - q0[1]), 2)
+        ok &= g
+        if comm is not None:
+            conc["cpu_own_core"], c = _drive(drv, 1, comm.fn, comm.ptr, packed, 1, callers, inner_threads=1,
+                                             seconds=conc_seconds)
+            ok &= c
+            conc["gpu_over_cpu_blocks_per_s"] = round(conc["gpu"]["blocks_per_s"] / conc["cpu_own_core"]["blocks_per_s"],
+                                                      3)
+            comm.close()
         res["concurrent_1_block_callers"] = conc
         out["shapes"][shape] = res
-    out["correct"] = ok
-    out["note"] = ("GPU: host parse-free path (raw bincode H2D, device parse/hash/verify, verdicts D2H), "
-                   "64 blocks < MV_BATCH_MIN so signatures take the committee comb tables (comb.hip); "
-                   "CPU: oracle/block.c StatementBlock::verify on a persistent thread pool (oracle/pool.c)")
+    out["correct"] = bool(ok)
+    out["note"] = ("GPU: mv_verify_blocks on host buffers (raw bincode in, verdicts out; 64 blocks < MV_BATCH_MIN "
+                   "take the committee comb tables, comb.hip); CPU: oracle/block.c StatementBlock::verify with the "
+                   "committee keys decoded once (orc_committee), 64-block calls on 1 core and on the pooled CPU "
+                   "share, concurrent callers each on its own core; every caller is a pthread "
+                   "(bench_native/concurrent.c)")
+    return out
+
+
+def config5(args, eng, rank) -> int:
+    res = config5_measure(eng, batches=args.batches, conc_seconds=args.conc_seconds, cpu=args.cpu_sample > 0)
+    out = {"metric": "config5: 64-block batch verify latency, submit -> verdicts (mv_verify_blocks, host buffers)",
+           "higher_is_better": False, "n_gpus": 1, "data": "synthetic (blocks signed on the GPU)"}
+    out.update(res)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    return 0 if ok else 1
-
-
-def _concurrent(eng, lib, blocks, pks, stakes, callers: int, seconds: float):
-    """callers threads, each verifying one block per call for `seconds`: per-call latency
-    percentiles and the aggregate blocks/s, GPU (queue-merged) and CPU (own core each)."""
-    import threading
-
-    import mysticeti_amd.blocks as MB
-
-    singles = [MB.pack([b]) for b in blocks]
-    out, ok = {"callers": callers}, True
-
-    def drive(call):
-        lats = [[] for _ in range(callers)]
-        bad = []
-        stop = time.perf_counter() + seconds
-
-        def worker(t):
-            k = t
-            while time.perf_counter() < stop:
-                t0 = time.perf_counter()
-                st = call(singles[k % len(singles)])
-                lats[t].append(time.perf_counter() - t0)
-                if st[0] != 0:
-                    bad.append(k)
-                k += callers
-
-        th = [threading.Thread(target=worker, args=(t,)) for t in range(callers)]
-        t0 = time.perf_counter()
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        wall = time.perf_counter() - t0
-        flat = [x for l in lats for x in l]
-        r = _lat_summary(flat)
-        r["blocks_per_s"] = round(len(flat) / wall, 1)
-        return r, not bad
-
-    c0 = eng.queue_stats()
-    out["gpu"], g_ok = drive(lambda b: eng.verify_blocks_packed(*b)[0])
-    c1 = eng.queue_stats()
-    out["gpu"]["calls_per_device_pass"] = round((c1[0] - c0[0]) / max(1, c1[1] - c0[1]), 2)
-    ok &= g_ok
-    if lib is not None:
-        out["cpu_own_core"], c_ok = drive(lambda b: _cpu_blocks(lib, *b, pks, stakes, 1))
-        ok &= c_ok
-    out["ok"] = ok
-    return out
+    return 0 if res["correct"] else 1
 
 
 # ------------------------------------------------------------------ config 4 (throughput)
@@ -330,6 +353,7 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     cpu_res = None
     if cpu and int(os.environ.get("RANK", "0")) == 0:  # the CPU baseline: rank 0 at any N
         lib = _oracle_native()
+        comm = _Committee(lib, pks, stakes)
         threads, share_src = _cpu_threads()
         res = {}
         for t, seconds in ((1, 4.0), (threads, 8.0)):
@@ -337,16 +361,17 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
             sub = nb if t > 1 else 400
             o2, l2 = off[:sub].copy(), ln[:sub].copy()
             while time.perf_counter() - t0 < seconds:
-                st = _cpu_blocks(lib, buf, o2, l2, pks, stakes, t)
+                st = _cpu_blocks(comm, buf, o2, l2, t)
                 ok &= bool((st == 0).all())
                 done += sub
             res[t] = (done / (time.perf_counter() - t0), done)
+        comm.close()
         cpu_res = {"value": round(res[threads][0], 1), "unit": "blocks/s", "cores": threads, "kind": "port",
                    "sample": f"{res[threads][1]} config-4 blocks on {threads} threads (~8 s); single core: "
                              f"{res[1][1]} blocks (~4 s)", "single_core_value": round(res[1][0], 1),
                    "host_cpu": _host_cpu(), "nproc": os.cpu_count(), "cores_source": share_src,
-                   "impl": "oracle/block.c StatementBlock::verify (parse, 2 x BLAKE2b, ZIP-215 verify), gcc -O3 "
-                           "-march=native, persistent thread pool"}
+                   "impl": "oracle/block.c StatementBlock::verify (parse, 2 x BLAKE2b, ZIP-215 verify; committee keys "
+                           "decoded once), gcc -O3 -march=native, persistent thread pool"}
     roof = None
     from bench import pmc_traffic
 

@@ -211,8 +211,11 @@ long orc_block_preimage(const uint8_t* bincode, size_t len, uint8_t* out, size_t
   return (long)s.len;
 }
 
-int orc_block_verify(const uint8_t* bincode, size_t len, const uint8_t* committee_pks, const uint64_t* stakes,
-                     uint32_t n_auth, uint64_t epoch, uint8_t msg_digest[32], uint8_t block_digest[32]) {
+/* `vks` (may be NULL): the committee's keys decoded once (orc_committee); else each verify
+ * decodes its key from committee_pks */
+static int block_verify(const uint8_t* bincode, size_t len, const uint8_t* committee_pks, const uint8_t* vks,
+                        const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint8_t msg_digest[32],
+                        uint8_t block_digest[32]) {
   parsed_t b;
   int vr_bad = 0;
   long plen = orc_block_preimage(bincode, len, NULL, 0);
@@ -232,8 +235,10 @@ int orc_block_verify(const uint8_t* bincode, size_t len, const uint8_t* committe
   if (b.epoch != epoch) return ORC_BLOCK_EPOCH_MISMATCH;
   if (b.reference.authority >= n_auth) return ORC_BLOCK_UNKNOWN_AUTHOR;
   if (b.reference.round == 0) return ORC_BLOCK_GENESIS;
-  if (orc_ed25519_verify(committee_pks + 32 * b.reference.authority, b.signature, msg, 32) != ORC_SIG_OK)
-    return ORC_BLOCK_SIG_INVALID;
+  const int sig_st = vks ? orc_ed25519_verify_vk((const orc_vk*)(vks + orc_vk_size() * b.reference.authority),
+                                                 b.signature, msg, 32)
+                         : orc_ed25519_verify(committee_pks + 32 * b.reference.authority, b.signature, msg, 32);
+  if (sig_st != ORC_SIG_OK) return ORC_BLOCK_SIG_INVALID;
   /* includes (types.rs:349-362), checked in order */
   cur_t c = {bincode, len, b.includes_pos, 0};
   uint64_t total = 0;
@@ -266,6 +271,46 @@ int orc_block_verify(const uint8_t* bincode, size_t len, const uint8_t* committe
   return ORC_BLOCK_OK;
 }
 
+int orc_block_verify(const uint8_t* bincode, size_t len, const uint8_t* committee_pks, const uint64_t* stakes,
+                     uint32_t n_auth, uint64_t epoch, uint8_t msg_digest[32], uint8_t block_digest[32]) {
+  return block_verify(bincode, len, committee_pks, NULL, stakes, n_auth, epoch, msg_digest, block_digest);
+}
+
+/* The committee as a node holds it: keys decoded once (Committee::new, committee.rs:83-87) */
+struct orc_committee {
+  uint32_t n;
+  uint64_t epoch;
+  uint8_t* pks;
+  uint64_t* stakes;
+  uint8_t* vks; /* n x orc_vk_size() */
+};
+
+orc_committee* orc_committee_new(const uint8_t* pks, const uint64_t* stakes, uint32_t n, uint64_t epoch) {
+  orc_committee* c = (orc_committee*)calloc(1, sizeof *c);
+  c->n = n;
+  c->epoch = epoch;
+  c->pks = (uint8_t*)malloc(32 * (size_t)n + 1);
+  c->stakes = (uint64_t*)malloc(8 * (size_t)n + 8);
+  c->vks = (uint8_t*)malloc(orc_vk_size() * (size_t)n + 1);
+  memcpy(c->pks, pks, 32 * (size_t)n);
+  memcpy(c->stakes, stakes, 8 * (size_t)n);
+  for (uint32_t i = 0; i < n; i++) orc_vk_init((orc_vk*)(c->vks + orc_vk_size() * i), pks + 32 * (size_t)i);
+  return c;
+}
+
+void orc_committee_free(orc_committee* c) {
+  if (!c) return;
+  free(c->pks);
+  free(c->stakes);
+  free(c->vks);
+  free(c);
+}
+
+int orc_block_verify_c(const orc_committee* c, const uint8_t* bincode, size_t len, uint8_t msg_digest[32],
+                       uint8_t block_digest[32]) {
+  return block_verify(bincode, len, c->pks, c->vks, c->stakes, c->n, c->epoch, msg_digest, block_digest);
+}
+
 typedef struct {
   const uint8_t* buf;
   const uint64_t *off, *len;
@@ -274,18 +319,25 @@ typedef struct {
   uint32_t n_auth;
   uint64_t epoch;
   uint8_t *status, *msgd, *blkd;
+  const uint8_t* vks;
 } bjob_t;
 
 static void block_item(void* arg, size_t i) {
   bjob_t* j = (bjob_t*)arg;
-  j->status[i] = (uint8_t)orc_block_verify(j->buf + j->off[i], j->len[i], j->pks, j->stakes, j->n_auth, j->epoch,
-                                           j->msgd ? j->msgd + 32 * i : NULL, j->blkd ? j->blkd + 32 * i : NULL);
+  j->status[i] = (uint8_t)block_verify(j->buf + j->off[i], j->len[i], j->pks, j->vks, j->stakes, j->n_auth, j->epoch,
+                                       j->msgd ? j->msgd + 32 * i : NULL, j->blkd ? j->blkd + 32 * i : NULL);
 }
 
 /* persistent pool (pool.c), one block per item */
 void orc_block_verify_batch(const uint8_t* buf, const uint64_t* off, const uint64_t* len, size_t n,
                             const uint8_t* committee_pks, const uint64_t* stakes, uint32_t n_auth, uint64_t epoch,
                             uint8_t* status, uint8_t* msg_digests, uint8_t* block_digests, int threads) {
-  bjob_t j = {buf, off, len, committee_pks, stakes, n_auth, epoch, status, msg_digests, block_digests};
+  bjob_t j = {buf, off, len, committee_pks, stakes, n_auth, epoch, status, msg_digests, block_digests, NULL};
+  orc_parallel_for(n, threads, 1, block_item, &j);
+}
+
+void orc_block_verify_batch_c(const orc_committee* c, const uint8_t* buf, const uint64_t* off, const uint64_t* len,
+                              size_t n, uint8_t* status, uint8_t* msg_digests, uint8_t* block_digests, int threads) {
+  bjob_t j = {buf, off, len, c->pks, c->stakes, c->n, c->epoch, status, msg_digests, block_digests, c->vks};
   orc_parallel_for(n, threads, 1, block_item, &j);
 }

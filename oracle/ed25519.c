@@ -552,11 +552,30 @@ int orc_point_decodes(const uint8_t enc[32]) {
   return ext_decompress(&p, enc);
 }
 
-int orc_ed25519_verify(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t msg_len) {
+/* VerificationKey (ed25519-consensus 2.1.0): the key bytes and -A, decoded once at
+ * VerificationKey::try_from; the reference's committee keys are built that way once per
+ * authority (crypto.rs:25, committee.rs:83-87), so per-block verifies start from -A. */
+struct orc_vk {
+  uint8_t bytes[32];
+  int ok;
+  ge_ext minusA;
+};
+size_t orc_vk_size(void) { return sizeof(struct orc_vk); }
+int orc_vk_init(orc_vk* vk, const uint8_t pk[32]) {
   ensure_init();
-  ge_ext A, minusA, R, Rp, diff;
-  if (!ext_decompress(&A, pk)) return ORC_SIG_MALFORMED_KEY; /* VerificationKey::try_from */
-  ext_neg(&minusA, &A);
+  ge_ext A;
+  memcpy(vk->bytes, pk, 32);
+  vk->ok = ext_decompress(&A, pk);
+  if (vk->ok) ext_neg(&vk->minusA, &A);
+  return vk->ok;
+}
+
+int orc_ed25519_verify_vk(const orc_vk* vk, const uint8_t sig[64], const uint8_t* msg, size_t msg_len) {
+  ensure_init();
+  if (!vk->ok) return ORC_SIG_MALFORMED_KEY;
+  const uint8_t* pk = vk->bytes;
+  const ge_ext minusA = vk->minusA;
+  ge_ext R, Rp, diff;
   if (!sc_is_canonical(sig + 32)) return ORC_SIG_INVALID;
   if (!ext_decompress(&R, sig)) return ORC_SIG_INVALID;
   uint8_t h[64], k[32];
@@ -576,6 +595,12 @@ int orc_ed25519_verify(const uint8_t pk[32], const uint8_t sig[64], const uint8_
   ext_double(&diff, &diff);
   ext_double(&diff, &diff);
   return ext_is_identity(&diff) ? ORC_SIG_OK : ORC_SIG_INVALID;
+}
+
+int orc_ed25519_verify(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t msg_len) {
+  orc_vk vk;
+  if (!orc_vk_init(&vk, pk)) return ORC_SIG_MALFORMED_KEY; /* VerificationKey::try_from */
+  return orc_ed25519_verify_vk(&vk, sig, msg, msg_len);
 }
 
 static void clamp_secret(uint8_t a[32], const uint8_t h[32]) {

@@ -40,6 +40,11 @@ enum { ORC_SIG_OK = 0, ORC_SIG_INVALID = 1, ORC_SIG_MALFORMED_KEY = 2 };
 int orc_ed25519_verify(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t msg_len);
 void orc_ed25519_pubkey(const uint8_t seed[32], uint8_t pk[32]);
 void orc_ed25519_sign(const uint8_t seed[32], const uint8_t* msg, size_t msg_len, uint8_t sig[64]);
+/* A decoded verification key (bytes + -A), as ed25519_consensus::VerificationKey holds it. */
+typedef struct orc_vk orc_vk;
+size_t orc_vk_size(void);
+int orc_vk_init(orc_vk* vk, const uint8_t pk[32]); /* 1 if pk decodes */
+int orc_ed25519_verify_vk(const orc_vk* vk, const uint8_t sig[64], const uint8_t* msg, size_t msg_len);
 /* ZIP-215 decode of a point encoding; returns 1 if it decodes. */
 int orc_point_decodes(const uint8_t enc[32]);
 /* x mod l for a 64-byte little-endian integer (Scalar::from_bytes_wide). */
@@ -85,6 +90,15 @@ int orc_block_verify(const uint8_t* bincode, size_t len, const uint8_t* committe
 void orc_block_verify_batch(const uint8_t* buf, const uint64_t* off, const uint64_t* len, size_t n,
                             const uint8_t* committee_pks, const uint64_t* stakes, uint32_t n_auth, uint64_t epoch,
                             uint8_t* status, uint8_t* msg_digests, uint8_t* block_digests, int threads);
+/* A committee with its keys decoded once, as the reference's Committee holds them (the CPU
+ * baseline legs use it; orc_block_verify decodes the author's key on every call). */
+typedef struct orc_committee orc_committee;
+orc_committee* orc_committee_new(const uint8_t* pks, const uint64_t* stakes, uint32_t n, uint64_t epoch);
+void orc_committee_free(orc_committee* c);
+int orc_block_verify_c(const orc_committee* c, const uint8_t* bincode, size_t len, uint8_t msg_digest[32],
+                       uint8_t block_digest[32]);
+void orc_block_verify_batch_c(const orc_committee* c, const uint8_t* buf, const uint64_t* off, const uint64_t* len,
+                              size_t n, uint8_t* status, uint8_t* msg_digests, uint8_t* block_digests, int threads);
 
 /* ---- WAL replay check (wal.c) ---- */
 enum { ORC_WAL_OK = 0, ORC_WAL_CRC_MISMATCH = 1, ORC_WAL_NONZERO_CRC_LEN0 = 2, ORC_WAL_BAD_LENGTH = 3 };

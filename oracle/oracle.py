@@ -57,6 +57,10 @@ def lib():
         _lib.orc_block_verify.restype = ctypes.c_int
         _lib.orc_block_verify_batch.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_uint32,
                                                 ctypes.c_uint64, u8p, u8p, u8p, ctypes.c_int]
+        _lib.orc_committee_new.argtypes = [u8p, u8p, ctypes.c_uint32, ctypes.c_uint64]
+        _lib.orc_committee_new.restype = ctypes.c_void_p
+        _lib.orc_committee_free.argtypes = [u8p]
+        _lib.orc_block_verify_batch_c.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, u8p, ctypes.c_int]
         _lib.orc_crc32.argtypes = [u8p, ctypes.c_size_t]
         _lib.orc_crc32.restype = ctypes.c_uint32
         _lib.orc_crc32_table.argtypes = [u8p, ctypes.c_size_t]
@@ -152,7 +156,9 @@ def block_verify(bincode: bytes, pks: np.ndarray, stakes: np.ndarray, epoch: int
 
 
 def block_verify_batch(buf: np.ndarray, off: np.ndarray, lens: np.ndarray, pks: np.ndarray, stakes: np.ndarray,
-                       epoch: int, threads: int = 0):
+                       epoch: int, threads: int = 0, decoded_committee: bool = False):
+    """StatementBlock::verify of every block; decoded_committee: through orc_committee (keys
+    decoded once, as the reference's Committee holds them) instead of a decode per verify."""
     n = off.shape[0]
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     off = np.ascontiguousarray(off, dtype=np.uint64)
@@ -162,6 +168,14 @@ def block_verify_batch(buf: np.ndarray, off: np.ndarray, lens: np.ndarray, pks: 
     status = np.zeros(n, dtype=np.uint8)
     md = np.zeros((n, 32), dtype=np.uint8)
     bd = np.zeros((n, 32), dtype=np.uint8)
+    if decoded_committee:
+        c = lib().orc_committee_new(_ptr(pks), _ptr(stakes), pks.shape[0], epoch)
+        try:
+            lib().orc_block_verify_batch_c(c, _ptr(buf), _ptr(off), _ptr(lens), n, _ptr(status), _ptr(md), _ptr(bd),
+                                           threads)
+        finally:
+            lib().orc_committee_free(c)
+        return status, md, bd
     lib().orc_block_verify_batch(_ptr(buf), _ptr(off), _ptr(lens), n, _ptr(pks), _ptr(stakes), pks.shape[0], epoch,
                                  _ptr(status), _ptr(md), _ptr(bd), threads)
     return status, md, bd

@@ -86,12 +86,13 @@ void orc_parallel_for(size_t n, int threads, size_t grain, orc_item_fn fn, void*
   if (grain == 0) grain = 1;
   const size_t chunks = (n + grain - 1) / grain;
   if ((size_t)threads > chunks) threads = chunks ? (int)chunks : 1;
-  pthread_mutex_lock(&g_pool.submit_mu);
   if (threads == 1) {
+    /* inline on the caller's thread, without the pool: concurrent single-threaded callers
+     * (one per peer, the config-5 "own core" leg) must run side by side, not one at a time */
     for (size_t i = 0; i < n; i++) fn(ctx, i);
-    pthread_mutex_unlock(&g_pool.submit_mu);
     return;
   }
+  pthread_mutex_lock(&g_pool.submit_mu);
   while (g_pool.nworkers < threads - 1) {
     pthread_t t;
     pthread_attr_t a;

@@ -83,6 +83,25 @@ def test_block_edge_statuses(golden):
         assert st == c["status"], c["note"]
 
 
+def test_decoded_committee_path_matches(golden):
+    """orc_committee (keys decoded once, the CPU baseline's form) gives the per-verify-decode
+    path's statuses and digests on every edge case and on config-1 blocks, on 1 and 4 threads."""
+    e = golden("block_edge.json")
+    pks = np.frombuffer(b"".join(bytes.fromhex(x) for x in e["committee"]["pks"]), dtype=np.uint8).reshape(-1, 32)
+    stakes = np.array(e["committee"]["stakes"], dtype=np.uint64)
+    bins = [bytes.fromhex(c["bincode"]) for c in e["cases"]]
+    buf = np.frombuffer(b"".join(bins) + b"\0", dtype=np.uint8)
+    lens = np.array([len(x) for x in bins], dtype=np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    want = np.array([c["status"] for c in e["cases"]], dtype=np.uint8)
+    for threads in (1, 4):
+        a = O.block_verify_batch(buf, offs, lens, pks, stakes, e["committee"]["epoch"], threads)
+        b = O.block_verify_batch(buf, offs, lens, pks, stakes, e["committee"]["epoch"], threads,
+                                 decoded_committee=True)
+        assert (a[0] == want).all() and (b[0] == want).all()
+        assert (a[1] == b[1]).all() and (a[2] == b[2]).all()
+
+
 def test_config1_blocks_oracle(golden):
     g = golden("blocks_config1.json")
     blks = B.gen_config1(O.sign)
