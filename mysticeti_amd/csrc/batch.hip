@@ -167,11 +167,6 @@ struct CommitteeA {
   uint32_t aggregate;  // 1: A's term is summed per key (k_bv_keyacc / k_bv_keypts), no A points
 };
 
-// one decode at a time at 3 waves/SIMD beat two decodes in lock-step at 2 (seq3 vs
-// x2 A/B on MI355X: 241 vs 220 M verifies/s for the whole batch path)
-#ifndef MV_PREP_X2
-#define MV_PREP_SEQ
-#endif
 #ifndef MV_PREP_OCC
 #define MV_PREP_OCC 3
 #endif
@@ -272,7 +267,8 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
         if (live) pt_store(pts, (size_t)n + gid, pc);
       }
     } else {
-#ifdef MV_PREP_SEQ  // experiment: one decode at a time (fewer registers, more waves)
+    // one decode at a time at 3 waves/SIMD beat the two decodes in lock-step (decompress_x2)
+    // at 2 waves/SIMD: 241 vs 220 M verifies/s for the whole batch path
     p3 P;
     decompress1_lean(P, okR, rw);
     precomp_from_affine(pc, P);
@@ -283,14 +279,6 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     decompress1_lean(P, okA, aw);
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, (size_t)n + gid, pc);
-#else
-    p3 A, R;
-    decompress_x2(A, okA, aw, R, okR, rw);
-    precomp_from_affine(pc, R);
-    if (live) pt_store(pts, gid, pc);
-    precomp_from_affine(pc, A);
-    if (live) pt_store(pts, (size_t)n + gid, pc);
-#endif
     }
   }
   const bool ok = live && okA && okR && s_ok;

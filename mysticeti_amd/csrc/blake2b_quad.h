@@ -124,12 +124,7 @@ MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* con
     // keep each round's message reads in their round: hoisting all 48 ahead of the chain
     // (what the scheduler does unchecked) doubles the VGPRs and halves the waves per SIMD
     asm volatile("" ::: "memory");
-#ifdef MV_B2Q_NOHOIST
-    uint32_t qq = q;
-    asm volatile("" : "+v"(qq));  // offsets computed in their round, not hoisted (registers)
-#else
     const uint32_t qq = q;
-#endif
     const uint32_t i0 = sel_at<NS>(r, 0, qq), i1 = sel_at<NS>(r, 1, qq);
     const uint32_t i2 = sel_at<NS>(r, 2, qq), i3 = sel_at<NS>(r, 3, qq);
     uint64_t x0[NS], y0[NS], x1[NS], y1[NS];

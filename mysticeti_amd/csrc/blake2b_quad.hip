@@ -25,11 +25,7 @@
 namespace mv {
 namespace b2q {
 
-#ifdef MV_B2Q_NOHOIST
-#define MV_B2Q_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6)))
-#else
 #define MV_B2Q_BOUNDS __launch_bounds__(64, NS == 1 ? 4 : 3)
-#endif
 template <bool DUAL, int NS>
 __global__ void MV_B2Q_BOUNDS k_b2_quad(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                         const uint64_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ out0,

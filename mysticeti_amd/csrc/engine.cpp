@@ -119,6 +119,20 @@ struct Device {
   bool blk_used[kSlots] = {};
   int blk_next = 0;
   HostBuf h_in, h_out;
+  // mv_verify_blocks passes (the submission queue): two sets of pinned staging, device
+  // buffers and a stream each, so pass k + 1 is packed and enqueued while pass k runs
+  struct PassSet {
+    HostBuf h_in, h_out;
+    DevBuf bytes, out2;
+    hipStream_t stream = nullptr;  // set 0: `stream`, set 1: pstream[1] (distinct hardware queues)
+    hipEvent_t done = nullptr;
+    // the chunk in flight: items [lo, lo + m) of `it`, outputs in h_out when finished
+    const void* it = nullptr;
+    uint64_t lo = 0;
+    uint32_t m = 0;
+    bool inflight = false;
+  };
+  PassSet pset[2];
   bool committee_loaded = false;
   // WAL replay (wal.hip): crc tables, walk records, per-map counts / flags / offsets, entries,
   // the image and outputs of host-buffer calls
@@ -167,7 +181,8 @@ struct mv_ctx {
   std::mutex q_mu;
   std::condition_variable q_cv;
   std::deque<BlockReq*> q;
-  bool q_busy = false;
+  bool q_packing = false;                // a combining caller is packing / enqueueing a pass
+  bool q_set_busy[2] = {false, false};   // pass sets with a pass in flight
   std::atomic<uint64_t> q_calls{0}, q_passes{0};
 };
 
@@ -379,7 +394,15 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   const int slot = dev.blk_next;
   dev.blk_next = (slot + 1) % Device::kSlots;
   if (!dev.blk_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.blk_done[slot], hipEventDisableTiming));
-  if (dev.blk_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.blk_done[slot], 0));
+  if (dev.blk_used[slot]) {
+    // skip the cross-stream wait when the slot's previous pass has finished (the common case
+    // on the online path, where a wait costs a queue drain)
+    const hipError_t q = hipEventQuery(dev.blk_done[slot]);
+    if (q != hipSuccess) {
+      (void)hipGetLastError();  // hipErrorNotReady is not an error here
+      HIPCHK(ctx, hipStreamWaitEvent(s, dev.blk_done[slot], 0));
+    }
+  }
   // scratch: stage | pre_off | pre_len | sig | key_idx | facts | claimed | sig status | md | bd
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t nn = n;
@@ -581,127 +604,288 @@ std::vector<uint64_t> balanced_cuts(const uint64_t* w, uint64_t n, uint32_t part
   return cut;
 }
 
-// One device pass over a list of blocks gathered from several requests: raw bincode packed
-// (8-aligned, 16 zero bytes after the last block) with offset/length arrays into pinned
-// staging, one H2D; parse, hashes, signatures and checks on the GPU; one D2H of
-// [msg digests | block digests | statuses]; verdicts scattered back to each block's owner.
+// Device passes over lists of blocks gathered from one or several mv_verify_blocks requests.
+// A chunk of blocks is packed into a pass set's pinned staging (raw bincode 8-aligned, 16 zero
+// bytes after the last block, then the offset and length arrays), read by the GPU (one H2D,
+// or zero-copy for small chunks), parsed, hashed and verified there, and its outputs
+// [msg digests | block digests | statuses] come back to pinned memory; the verdicts are then
+// scattered to each block's owner.
 struct BlockItem {
   const uint8_t* p;
   uint64_t len;
   uint8_t *st, *md, *bd;
 };
 
-mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint64_t lo, uint64_t hi) {
+// packed bytes of one block (8-aligned)
+inline uint64_t packed_len(const BlockItem& b) { return (b.len + 7) & ~7ull; }
+
+// Chunk limits: <= max_batch blocks and <= MV_BLK_CHUNK_BYTES (default 256 MiB) of bincode.
+// A host-fed call larger than one chunk streams: chunk c + 1 is packed, copied and enqueued
+// on the other pass set while chunk c runs.
+uint64_t chunk_bytes_limit() {
+  static const uint64_t v = [] {
+    const char* e = getenv("MV_BLK_CHUNK_BYTES");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? (uint64_t)x : (uint64_t)(256ull << 20);
+  }();
+  return v;
+}
+uint64_t chunk_end(mv_ctx* ctx, const BlockItem* it, uint64_t lo, uint64_t hi) {
+  uint64_t j = lo, bytes = 0;
+  const uint64_t lim = chunk_bytes_limit();
+  while (j < hi && j - lo < ctx->max_batch && (bytes < lim || j == lo)) bytes += packed_len(it[j++]);
+  return j;
+}
+
+// Copies items [lo, hi) into h (their packed offsets in off[], lengths in len[]), on up to
+// `threads` threads for large chunks.
+void pack_items(uint8_t* h, uint64_t* off, uint64_t* len, const BlockItem* it, uint64_t lo, uint64_t hi,
+                size_t buf_bytes) {
+  const uint32_t m = (uint32_t)(hi - lo);
+  uint64_t pos = 0;
+  for (uint32_t k = 0; k < m; k++) {
+    off[k] = pos;
+    len[k] = it[lo + k].len;
+    pos += packed_len(it[lo + k]);
+  }
+  auto copy = [&](uint32_t a, uint32_t b) {
+    for (uint32_t k = a; k < b; k++) {
+      const uint64_t l = len[k], o = off[k];
+      memcpy(h + o, it[lo + k].p, l);
+      memset(h + o + l, 0, ((l + 7) & ~7ull) - l);
+    }
+  };
+  static const unsigned max_thr = [] {  // MV_PACK_THREADS: host threads packing a large chunk
+    const char* e = getenv("MV_PACK_THREADS");
+    const unsigned hw = std::thread::hardware_concurrency();
+    return e ? (unsigned)std::max(1, atoi(e)) : std::min(8u, hw ? hw : 4u);
+  }();
+  const unsigned threads = pos < (8u << 20) ? 1u : std::min<unsigned>(max_thr, m);
+  if (threads <= 1) {
+    copy(0, m);
+  } else {  // item ranges of about equal bytes
+    std::vector<std::thread> th;
+    uint32_t a = 0;
+    for (unsigned t = 1; t <= threads; t++) {
+      const uint64_t target = pos * t / threads;
+      uint32_t b = a;
+      while (b < m && off[b] < target) b++;
+      if (t == threads) b = m;
+      if (b > a) {
+        if (t == threads) copy(a, b);
+        else th.emplace_back(copy, a, b);
+      }
+      a = b;
+    }
+    for (auto& x : th) x.join();
+  }
+  memset(h + pos, 0, buf_bytes - pos);
+}
+
+mv_status ensure_pass_set(mv_ctx* ctx, Device& dev, int s) {
+  Device::PassSet& ps = dev.pset[s];
+  if (!ps.stream) {
+    if (s == 0) {
+      ps.stream = dev.stream;
+    } else {
+      if (!dev.pstream[1]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[1], hipStreamNonBlocking));
+      ps.stream = dev.pstream[1];
+    }
+  }
+  if (!ps.done) HIPCHK(ctx, hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
+  return MV_OK;
+}
+
+// Packs items [lo, hi) into pass set s of dev and enqueues the device pipeline on its stream
+// (no wait). The set must be idle.
+mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* it, uint64_t lo, uint64_t hi) {
   HIPCHK(ctx, hipSetDevice(dev.id));
+  mv_status rc = ensure_pass_set(ctx, dev, s);
+  if (rc != MV_OK) return rc;
+  Device::PassSet& ps = dev.pset[s];
   static const bool trace = getenv("MV_BLK_TRACE") != nullptr;  // diagnostics: host-side times
   auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  uint64_t i = lo;
-  while (i < hi) {
-    const double t0 = trace ? now() : 0;
-    uint64_t j = i, bytes = 0;
-    while (j < hi && j - i < ctx->max_batch && bytes < (1ull << 30)) bytes += (it[j++].len + 7) & ~7ull;
-    const uint32_t m = (uint32_t)(j - i);
-    const size_t buf_bytes = (bytes + 16 + 15) & ~(size_t)15;
-    const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
-    HIPCHK(ctx, dev.h_in.ensure(total));
-    uint8_t* h = dev.h_in.as<uint8_t>();
-    uint64_t* hoff = (uint64_t*)(h + o_off);
-    uint64_t* hlen = (uint64_t*)(h + o_len);
-    uint64_t pos = 0;
-    for (uint32_t k = 0; k < m; k++) {
-      const uint64_t l = it[i + k].len;
-      memcpy(h + pos, it[i + k].p, l);
-      hoff[k] = pos;
-      hlen[k] = l;
-      const uint64_t next = (pos + l + 7) & ~7ull;
-      memset(h + pos + l, 0, next - pos - l);
-      pos = next;
+  const double t0 = trace ? now() : 0;
+  const uint32_t m = (uint32_t)(hi - lo);
+  uint64_t bytes = 0;
+  for (uint64_t k = lo; k < hi; k++) bytes += packed_len(it[k]);
+  const size_t buf_bytes = (bytes + 16 + 15) & ~(size_t)15;
+  const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
+  HIPCHK(ctx, ps.h_in.ensure(total));
+  uint8_t* h = ps.h_in.as<uint8_t>();
+  pack_items(h, (uint64_t*)(h + o_off), (uint64_t*)(h + o_len), it, lo, hi, buf_bytes);
+  HIPCHK(ctx, ps.bytes.ensure(total));
+  HIPCHK(ctx, ps.out2.ensure(65 * (size_t)m + 256));
+  HIPCHK(ctx, ps.h_out.ensure(65 * (size_t)m));
+  const double t1 = trace ? now() : 0;
+  // small chunks (the online path): the ingest kernel reads the pinned staging over PCIe
+  // itself (zero-copy) instead of waiting for an H2D copy and the launch behind it
+  static const uint64_t zc_max = [] {  // MV_BLK_ZEROCOPY=<bytes> (experiments; 0 = always copy)
+    const char* e = getenv("MV_BLK_ZEROCOPY");
+    return e ? (uint64_t)atoll(e) : (uint64_t)(1u << 20);
+  }();
+  const uint8_t* dbuf = nullptr;
+  uint8_t* hout_dev = nullptr;  // zero-copy outputs too: the kernels write the pinned h_out
+  if (total <= zc_max) {
+    void* dp = nullptr;
+    void* dq = nullptr;
+    // outputs only under the comb path: the batch path re-reads the digests many times
+    const bool zc_out = m < MV_BATCH_MIN;
+    if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess && dp &&
+        (!zc_out || (hipHostGetDevicePointer(&dq, ps.h_out.p, 0) == hipSuccess && dq))) {
+      dbuf = static_cast<const uint8_t*>(dp);
+      hout_dev = static_cast<uint8_t*>(dq);
+    } else {
+      (void)hipGetLastError();
     }
-    memset(h + pos, 0, buf_bytes - pos);
-    HIPCHK(ctx, dev.bytes.ensure(total));
-    HIPCHK(ctx, dev.out2.ensure(65 * (size_t)m + 256));
-    HIPCHK(ctx, dev.h_out.ensure(65 * (size_t)m));
-    const double t1 = trace ? now() : 0;
-    // small passes (the online path): the ingest kernel reads the pinned staging over PCIe
-    // itself (zero-copy) instead of waiting for an H2D copy and the launch behind it
-    static const uint64_t zc_max = [] {  // MV_BLK_ZEROCOPY=<bytes> (experiments; 0 = always copy)
-      const char* e = getenv("MV_BLK_ZEROCOPY");
-      return e ? (uint64_t)atoll(e) : (uint64_t)(1u << 20);
-    }();
-    const uint8_t* dbuf = nullptr;
-    uint8_t* hout_dev = nullptr;  // zero-copy outputs too: the kernels write the pinned h_out
-    if (total <= zc_max) {
-      void* dp = nullptr;
-      void* dq = nullptr;
-      // outputs only under the comb path: the batch path re-reads the digests many times
-      const bool zc_out = m < MV_BATCH_MIN;
-      if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess && dp &&
-          (!zc_out || (hipHostGetDevicePointer(&dq, dev.h_out.p, 0) == hipSuccess && dq))) {
-        dbuf = static_cast<const uint8_t*>(dp);
-        hout_dev = static_cast<uint8_t*>(dq);
-      } else {
-        (void)hipGetLastError();
-      }
-    }
-    if (!dbuf) {
-      HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, h, total, hipMemcpyHostToDevice, dev.stream));
-      dbuf = dev.bytes.as<uint8_t>();
-    }
-    const double t2 = trace ? now() : 0;
-    uint8_t* dout = hout_dev ? hout_dev : dev.out2.as<uint8_t>();
-    mv_status st = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off),
-                                  (const uint64_t*)(dbuf + o_len), m, dout + 64 * (size_t)m, dout,
-                                  dout + 32 * (size_t)m, dev.stream);
-    if (st != MV_OK) return st;
-    const double t3 = trace ? now() : 0;
-    if (!hout_dev) HIPCHK(ctx, hipMemcpyAsync(dev.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
-    const double t4 = trace ? now() : 0;
-    HIPCHK(ctx, hipStreamSynchronize(dev.stream));
-    if (trace)
-      fprintf(stderr, "[blk] %u blocks: pack %.1f, h2d %.1f, kernels %.1f, d2h %.1f, wait %.1f us\n", m, t1 - t0,
-              t2 - t1, t3 - t2, t4 - t3, now() - t4);
-    poll_flags(ctx, dev);
-    const uint8_t* ho = dev.h_out.as<uint8_t>();
-    for (uint32_t k = 0; k < m; k++) {
-      const BlockItem& b = it[i + k];
-      *b.st = ho[64 * (size_t)m + k];
-      if (b.md) memcpy(b.md, ho + 32 * (size_t)k, 32);
-      if (b.bd) memcpy(b.bd, ho + 32 * ((size_t)m + k), 32);
-    }
-    i = j;
+  }
+  if (!dbuf) {
+    HIPCHK(ctx, hipMemcpyAsync(ps.bytes.p, h, total, hipMemcpyHostToDevice, ps.stream));
+    dbuf = ps.bytes.as<uint8_t>();
+  }
+  const double t2 = trace ? now() : 0;
+  uint8_t* dout = hout_dev ? hout_dev : ps.out2.as<uint8_t>();
+  rc = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off), (const uint64_t*)(dbuf + o_len), m,
+                      dout + 64 * (size_t)m, dout, dout + 32 * (size_t)m, ps.stream);
+  if (rc != MV_OK) {
+    (void)hipStreamSynchronize(ps.stream);  // what was queued reads the staging
+    return rc;
+  }
+  if (!hout_dev) HIPCHK(ctx, hipMemcpyAsync(ps.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, ps.stream));
+  HIPCHK(ctx, hipEventRecord(ps.done, ps.stream));
+  ps.it = it;
+  ps.lo = lo;
+  ps.m = m;
+  ps.inflight = true;
+  if (trace) fprintf(stderr, "[blk] set %d, %u blocks: pack %.1f, h2d %.1f, kernels %.1f us\n", s, m, t1 - t0, t2 - t1, now() - t2);
+  return MV_OK;
+}
+
+// Waits for pass set s's chunk and scatters its verdicts and digests to the blocks' owners.
+// Needs no context lock (the set is owned by the caller until it is marked idle).
+mv_status finish_block_chunk(mv_ctx* ctx, Device& dev, int s) {
+  Device::PassSet& ps = dev.pset[s];
+  if (!ps.inflight) return MV_OK;
+  ps.inflight = false;
+  HIPCHK(ctx, hipSetDevice(dev.id));
+  const hipError_t e = hipEventSynchronize(ps.done);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(ps.stream);
+    return set_err(ctx, MV_E_HIP, std::string("block pass: ") + hipGetErrorString(e));
+  }
+  const BlockItem* it = static_cast<const BlockItem*>(ps.it);
+  const uint32_t m = ps.m;
+  const uint8_t* ho = ps.h_out.as<uint8_t>();
+  for (uint32_t k = 0; k < m; k++) {
+    const BlockItem& b = it[ps.lo + k];
+    *b.st = ho[64 * (size_t)m + k];
+    if (b.md) memcpy(b.md, ho + 32 * (size_t)k, 32);
+    if (b.bd) memcpy(b.bd, ho + 32 * ((size_t)m + k), 32);
   }
   return MV_OK;
 }
 
-// The combining caller's pass over every request it took from the queue.
-void run_block_requests(mv_ctx* ctx, std::vector<mv_ctx::BlockReq*>& reqs) {
-  std::vector<BlockItem> items;
-  size_t total = 0;
-  for (auto* r : reqs) total += r->n;
-  items.reserve(total);
-  for (auto* r : reqs)
-    for (uint32_t k = 0; k < r->n; k++)
-      items.push_back(BlockItem{r->buf + r->off[k], r->len[k], r->status + k, r->md ? r->md + 32 * (size_t)k : nullptr,
-                                r->bd ? r->bd + 32 * (size_t)k : nullptr});
+// Items [lo, hi) on dev in chunks over both pass sets (chunk c + 1 packed and enqueued while
+// chunk c runs); returns when all are scattered. Caller holds ctx->mu and owns both sets.
+mv_status verify_block_items(mv_ctx* ctx, Device& dev, const BlockItem* it, uint64_t lo, uint64_t hi) {
+  mv_status rc = MV_OK;
+  int s = 0;
+  for (uint64_t i = lo; i < hi && rc == MV_OK; s ^= 1) {
+    rc = finish_block_chunk(ctx, dev, s);  // the set's chunk before last
+    if (rc != MV_OK) break;
+    const uint64_t j = chunk_end(ctx, it, i, hi);
+    rc = enqueue_block_chunk(ctx, dev, s, it, i, j);
+    i = j;
+  }
+  for (int k = 0; k < 2; k++) {
+    const mv_status r2 = finish_block_chunk(ctx, dev, k);
+    if (rc == MV_OK) rc = r2;
+  }
+  poll_flags(ctx, dev);
+  return rc;
+}
+
+bool committee_ready(mv_ctx* ctx) {
+  if (!ctx->has_committee) return false;
+  for (auto& dev : ctx->devs)
+    if (!dev.committee_loaded) return false;
+  return true;
+}
+
+// One pass of the submission queue over the requests the combining caller took. set >= 0:
+// the pass fits one chunk per device and runs on that pass set: it is packed and enqueued
+// under ctx->mu, `enqueued()` is called, and the caller waits for the device without the
+// lock (the next pass can be packed meanwhile). set < 0: a large pass that owns both sets
+// and streams its chunks (`enqueued()` at the end). Every request gets rc (and err).
+template <class Enqueued>
+void run_block_requests(mv_ctx* ctx, std::deque<mv_ctx::BlockReq*>& reqs, int set, Enqueued enqueued) {
+  bool signalled = false;
+  auto signal = [&] {
+    if (!signalled) {
+      signalled = true;
+      enqueued();
+    }
+  };
   std::string err;
-  mv_status rc;
-  {
+  mv_status rc = MV_OK;
+  std::vector<BlockItem> items;
+  std::vector<std::pair<size_t, std::pair<uint64_t, uint64_t>>> shards;  // device, [lo, hi)
+  try {
+    size_t total = 0;
+    for (auto* r : reqs) total += r->n;
+    items.reserve(total);
+    for (auto* r : reqs)
+      for (uint32_t k = 0; k < r->n; k++)
+        items.push_back(BlockItem{r->buf + r->off[k], r->len[k], r->status + k,
+                                  r->md ? r->md + 32 * (size_t)k : nullptr, r->bd ? r->bd + 32 * (size_t)k : nullptr});
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->q_passes++;
     t_err = &err;
     const size_t nd = ctx->devs.size();
+    std::vector<uint64_t> cut;
     if (nd == 1 || items.size() < 2 * nd) {
-      rc = verify_block_items(ctx, ctx->devs[0], items.data(), 0, items.size());
+      cut = {0, (uint64_t)items.size()};
     } else {
       std::vector<uint64_t> w(items.size());
       for (size_t k = 0; k < items.size(); k++) w[k] = items[k].len + 64;  // bytes, plus a per-block constant
-      rc = for_each_cut(ctx, balanced_cuts(w.data(), w.size(), (uint32_t)nd),
-                        [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
-                          return verify_block_items(ctx, dev, items.data(), lo, hi);
-                        });
+      cut = balanced_cuts(w.data(), w.size(), (uint32_t)nd);
+    }
+    // the committee is checked again under the lock: a failed mv_set_committee may have
+    // unpublished it after the request was queued
+    if (!committee_ready(ctx)) {
+      rc = set_err(ctx, MV_E_NO_COMMITTEE, "mv_set_committee first");
+    } else if (set >= 0) {
+      shards.reserve(cut.size());  // push_back below must not throw once a chunk is in flight
+      for (size_t d = 0; d + 1 < cut.size() && rc == MV_OK; d++) {
+        if (cut[d] == cut[d + 1]) continue;
+        rc = enqueue_block_chunk(ctx, ctx->devs[d], set, items.data(), cut[d], cut[d + 1]);
+        if (rc == MV_OK) shards.push_back({d, {cut[d], cut[d + 1]}});
+      }
+    } else if (cut.size() == 2) {
+      rc = verify_block_items(ctx, ctx->devs[0], items.data(), 0, items.size());
+    } else {
+      rc = for_each_cut(ctx, cut, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
+        return verify_block_items(ctx, dev, items.data(), lo, hi);
+      });
       if (rc != MV_OK) err = ctx->err;
     }
     t_err = nullptr;
+  } catch (...) {  // std::bad_alloc from the item list or the shard plan
+    t_err = nullptr;
+    rc = MV_E_ALLOC;
+    err = "mv_verify_blocks: host allocation failed";
+  }
+  signal();
+  // set >= 0: wait for this pass's chunks (outside the context lock) and scatter the verdicts
+  for (auto& sh : shards) {
+    t_err = &err;
+    const mv_status r2 = finish_block_chunk(ctx, ctx->devs[sh.first], set);
+    t_err = nullptr;
+    if (rc == MV_OK) rc = r2;
+  }
+  if (set >= 0 && !shards.empty()) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (auto& sh : shards) poll_flags(ctx, ctx->devs[sh.first]);
   }
   for (auto* r : reqs) {
     r->rc = rc;
@@ -1046,6 +1230,13 @@ void mv_destroy(mv_ctx* ctx) {
       if (ev) (void)hipEventDestroy(ev);
     dev.h_in.release();
     dev.h_out.release();
+    for (auto& ps : dev.pset) {
+      ps.h_in.release();
+      ps.h_out.release();
+      ps.bytes.release();
+      ps.out2.release();
+      if (ps.done) (void)hipEventDestroy(ps.done);
+    }
     if (dev.stream) (void)hipStreamDestroy(dev.stream);
   }
   delete ctx;
@@ -1232,26 +1423,47 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     std::lock_guard<std::mutex> lk(ctx->mu);
     return verify_blocks_host_parse(ctx, buf, off, len, n, status, msg_digest, block_digest);
   }
-  // Flat combining: the request joins the queue; a caller that finds no pass running takes
-  // every queued request (its own included) into one device pass, so n - 1 peer tasks each
-  // submitting a block or two (net_sync.rs:214-221, 314-386) share one GPU round trip.
+  // Flat combining, pipelined: the request joins the queue; a caller that finds no pass being
+  // packed and a free pass set takes every queued request (its own included) into one pass,
+  // packs and enqueues it, then lets the next caller pack the following pass into the other
+  // set while its own runs on the device. n - 1 peer tasks each submitting a block or two
+  // (net_sync.rs:214-221, 314-386) thus share GPU round trips, two passes in flight.
   mv_ctx::BlockReq req{buf, off, len, n, status, msg_digest, block_digest};
   ctx->q_calls++;
   std::unique_lock<std::mutex> ql(ctx->q_mu);
   ctx->q.push_back(&req);
   while (!req.done) {
-    if (ctx->q_busy) {
+    const int s = !ctx->q_set_busy[0] ? 0 : (!ctx->q_set_busy[1] ? 1 : -1);
+    if (ctx->q_packing || s < 0 || ctx->q.empty()) {
       ctx->q_cv.wait(ql);
       continue;
     }
-    ctx->q_busy = true;
-    std::vector<mv_ctx::BlockReq*> batch(ctx->q.begin(), ctx->q.end());
-    ctx->q.clear();
+    std::deque<mv_ctx::BlockReq*> batch;
+    batch.swap(ctx->q);  // no allocation
+    uint64_t blocks = 0, bytes = 0;
+    for (auto* r : batch) {
+      blocks += r->n;
+      for (uint32_t k = 0; k < r->n; k++) bytes += (r->len[k] + 7) & ~7ull;
+    }
+    // larger than one chunk per device: the pass streams its chunks over both sets
+    const uint64_t nd = ctx->devs.size();
+    const bool big = blocks > (uint64_t)ctx->max_batch * nd || bytes > chunk_bytes_limit() * nd;
+    ctx->q_packing = true;
+    if (big)
+      while (ctx->q_set_busy[0] || ctx->q_set_busy[1]) ctx->q_cv.wait(ql);
+    const int set = big ? -1 : s;
+    if (big) ctx->q_set_busy[0] = ctx->q_set_busy[1] = true;
+    else ctx->q_set_busy[s] = true;
     ql.unlock();
-    run_block_requests(ctx, batch);
+    run_block_requests(ctx, batch, set, [ctx] {
+      std::lock_guard<std::mutex> lk(ctx->q_mu);
+      ctx->q_packing = false;
+      ctx->q_cv.notify_all();
+    });
     ql.lock();
     for (auto* r : batch) r->done = true;
-    ctx->q_busy = false;
+    if (big) ctx->q_set_busy[0] = ctx->q_set_busy[1] = false;
+    else ctx->q_set_busy[s] = false;
     ctx->q_cv.notify_all();
   }
   ql.unlock();

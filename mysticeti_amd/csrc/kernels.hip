@@ -29,31 +29,11 @@
 
 namespace mv {
 
-// Phase clocks for tools/phase_clock.hip (compiled only there): lane 0 of every wave
-// records clock64() deltas at the verify kernel's phase boundaries.
-#ifdef MV_PHASE_CLOCKS
-__device__ unsigned long long* g_phase_buf;
-#define MV_PHASE(i)                                                                   \
-  do {                                                                                \
-    if ((threadIdx.x & 63) == 0 && g_phase_buf)                                       \
-      g_phase_buf[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (i)] = clock64(); \
-  } while (0)
-#else
-#define MV_PHASE(i) \
-  do {              \
-  } while (0)
-#endif
-
 // Per-wave variable-base table scratch. Lane-major: each lane owns 2 x 81 contiguous
 // uint4 ([table][entry][quad]), so one entry gather reads 144 contiguous bytes per lane
-// (2 cache lines) and the whole line is used; the wave-major alternative
-// ([table][entry][quad][lane], MV_TAB_WAVE_MAJOR) coalesces the build's stores but a
-// random-digit gather then touches ~5 partly used lines per 8 lanes per quad.
-#ifdef MV_TAB_WAVE_MAJOR
-constexpr int TAB_LANE_STRIDE = 1, TAB_QUAD_STRIDE = 64;
-#else
+// (2 cache lines) and the whole line is used (a wave-major layout coalesces the build's
+// stores, but a random-digit gather then touches ~5 partly used lines per 8 lanes per quad).
 constexpr int TAB_LANE_STRIDE = 2 * AT_TABLE, TAB_QUAD_STRIDE = 1;
-#endif
 constexpr int TAB_ENTRY_STRIDE = AT_QUADS * TAB_QUAD_STRIDE;
 constexpr int TAB_TABLE_STRIDE = AT_ENTRIES * TAB_ENTRY_STRIDE;  // A table -> R table
 MV_DEV void atab_put(uint4* tab, int e, const cached& c) {
@@ -179,15 +159,10 @@ __global__ void __launch_bounds__(256, MINW)
   if (skip && skip[skip_group ? blockIdx.x * blockDim.x / skip_group : 0]) return;
   __shared__ uint4 btab[2 * BT_TABLE];
   lds_btab_load(btab, btab_g, 2 * BT_TABLE);
-  MV_PHASE(0);
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t idx = gid < n ? gid : n - 1;
   const int lane = threadIdx.x & 63;
-#ifdef MV_EXP_SHARED_TAB  // timing experiment only (tools/phase_clock.hip): one table region for all waves
-  uint4* wave_tab = scratch + (size_t)((gid >> 6) & 7) * (WAVE_QUADS * 64);
-#else
   uint4* wave_tab = scratch + (size_t)(gid >> 6) * (WAVE_QUADS * 64);
-#endif
   uint4* wave_dig = wave_tab + SCR_DIG;
   uint4* tabA = wave_tab + lane * TAB_LANE_STRIDE;
   uint4* tabR = tabA + TAB_TABLE_STRIDE;
@@ -211,16 +186,9 @@ __global__ void __launch_bounds__(256, MINW)
     }
     sha512_short(h, kin, 96);
     sc_reduce512(k, h);
-    MV_PHASE(1);
     uint32_t c[4], d[8], e[8], zero[8];
     bool c_neg;
-#ifdef MV_EXP_NO_HALFSIZE  // timing experiment only: wrong (c, d), same instruction stream after
-    for (int i = 0; i < 4; i++) { c[i] = k[i] >> 2; d[i] = k[4 + i] >> 2; }
-    c_neg = k[0] & 1;
-#else
     sc_halfsize(c, c_neg, d, k);
-#endif
-    MV_PHASE(2);
 #pragma unroll
     for (int i = 0; i < 8; i++) zero[i] = 0;
 #pragma unroll
@@ -232,7 +200,6 @@ __global__ void __launch_bounds__(256, MINW)
     sc_recode256(ed, e);
 #pragma unroll
     for (int g = 0; g < 4; g++) wave_dig[g * 64 + lane] = make_uint4(cd[g], dd[g], ed[g], ed[4 + g]);
-    MV_PHASE(3);
 
     p3 A, R, nR;
     if (pv.pts) {  // decoded by k_bv_prep; lanes prep already rejected keep its verdict
@@ -257,14 +224,12 @@ __global__ void __launch_bounds__(256, MINW)
     } else {
       decompress_x2(A, okA, aw, R, okR, rw);
     }
-    MV_PHASE(4);
     // -[c]A = [|c|](-A) for c >= 0, [|c|]A for c < 0
     if (!c_neg) p3_neg(A, A);
     vtab_build(tabA, A);
     p3_neg(nR, R);
     vtab_build(tabR, nR);
   }
-  MV_PHASE(5);
 
   p2 P;
   p3 P3;
@@ -307,7 +272,6 @@ __global__ void __launch_bounds__(256, MINW)
       p1p1_to_p2(P, Q);
     }
   }
-  MV_PHASE(6);
   // cofactored check: [8]([e]B - [c]A - [d]R) == identity
 #pragma unroll 1
   for (int i = 0; i < 3; i++) {
@@ -319,7 +283,6 @@ __global__ void __launch_bounds__(256, MINW)
     uint8_t st = !okA ? 2 : ((s_ok && okR && ident) ? 0 : 1);
     status[gid] = st;
   }
-  MV_PHASE(7);
 }
 
 // RFC 8032: (pk, R || S) from (seed, 32-byte msg)
@@ -521,6 +484,17 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
     }
     case 9: {  // sha512 of 64 bytes
       sha512_short(y, x, 64);
+#pragma unroll
+      for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
+      return;
+    }
+    case 15: {  // sha512 of 96 bytes (the R || A || M challenge input): the 64 input bytes, then their first 32
+      uint32_t m96[24];
+#pragma unroll
+      for (int i = 0; i < 16; i++) m96[i] = x[i];
+#pragma unroll
+      for (int i = 0; i < 8; i++) m96[16 + i] = x[i];
+      sha512_short(y, m96, 96);
 #pragma unroll
       for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
       return;

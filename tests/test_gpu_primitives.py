@@ -109,6 +109,18 @@ def test_sha512_64(engine):
         assert o.astype("<u4").tobytes() == hashlib.sha512(m).digest()
 
 
+def test_sha512_96(engine):
+    """The 96-byte form the challenge k = SHA-512(R || A || M) uses (crypto.rs:188 via
+    ed25519-consensus): selftest op 15 hashes the 64 input bytes followed by their first 32."""
+    r = random.Random(7)
+    msgs = [bytes(r.randrange(256) for _ in range(64)) for _ in range(100)]
+    msgs += [bytes(64), bytes([0xff]) * 64]
+    w = np.array([list(np.frombuffer(m, dtype=np.uint32)) for m in msgs], dtype=np.uint32)
+    out = engine.selftest(15, w)
+    for m, o in zip(msgs, out):
+        assert o.astype("<u4").tobytes() == hashlib.sha512(m + m[:32]).digest()
+
+
 def test_basepoint_mul(engine):
     r = random.Random(8)
     ks = [0, 1, 2, 3, 127, 128, 129, 255, 256, Z.L - 1] + [r.randrange(Z.L) for _ in range(60)]
