@@ -28,10 +28,13 @@
 // field ops per signature against k_verify's ~2,335.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fe25519.h"
+#include "fe_q4.h"
 #include "ge25519.h"
 #include "hash_dev.h"
+#include "quad25519.h"
 #include "kernels.h"
 #include "scalar25519.h"
 #include "tables.h"
@@ -194,6 +197,180 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* msg, const u
     }
     const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
     if (gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
+  }
+}
+
+// ---------------------------------------------------------------- four lanes per signature
+// k_verify_comb4: the same predicate with every chain on FOUR lanes per signature, for the
+// online path (64-block calls), where k_verify_comb's latency is its longest single-lane chain:
+// the R decode (~265 field operations) and the 32 B-table additions each take ~80 us on one
+// lane. 512 threads per 32 signatures, four roles of 128 lanes (one quad per signature; two
+// waves per SIMD leave each 256 VGPRs):
+//   role 0  ZIP-215 decode of R with the (p-5)/8 power on fe_q4.h (each product split over
+//           the quad), then the combination below
+//   role 1  the 32 C_B entries of s's digits, point additions on quad25519.h's layout (lane c
+//           holds coordinate c; lane c loads only the entry coordinate its product needs)
+//   role 2  SHA-512 k; the C_A entries of k's digits 0..15
+//   role 3  SHA-512 k; the C_A entries of k's digits 16..31
+// Role 0 then adds the three partial sums (LDS), subtracts them from R, clears the cofactor
+// and tests for the identity. Same predicate, same status as k_verify_comb.
+MV_DEV void decompress1_q4(p3& A, bool& okA, const uint32_t ea[8]) {
+  fe d, one, ya, ua, va, t, v3a, ea7, pa, xa, n;
+  fe_const(d, K_D);
+  fe_set(one, 1);
+  fe_from_words(ya, ea);
+  fe_sq(t, ya);
+  fe_sub(ua, t, one);
+  fe_mul(va, t, d);
+  fe_add(va, va, one);
+  fe_sq(t, va); fe_mul(v3a, t, va);
+  fe_sq(t, v3a); fe_mul(ea7, t, va); fe_mul(ea7, ea7, ua);
+  {
+    feq x, r;
+    feq_from_fe(x, ea7);
+    feq_pow_p58(r, x);
+    fe_from_feq(pa, r);
+  }
+  fe_mul(pa, pa, v3a); fe_mul(pa, pa, ua);
+  okA = sqrt_ratio_finish(xa, ua, va, pa);
+  fe_neg(n, xa);
+  fe_cmov(xa, n, (ea[7] >> 31) != 0);
+  A.X = xa; A.Y = ya; fe_set(A.Z, 1); fe_mul(A.T, xa, ya);
+}
+
+// v = coordinate c of P (extended) -> coordinate c of P + e, e = a table entry (affine
+// precomp, p3_add_precomp's sequence): lane 0 multiplies Y + X by e's y + x, lane 1 Y - X by
+// y - x, lane 2 Z by 2, lane 3 T by 2dxy (`op` is the lane's operand, the entry's sign applied)
+MV_DEV void qp_madd(fe& v, const fe& op) {
+  const uint32_t c = qlane();
+  fe X1, Y1, ypx, ymx, o1, prod;
+  fe_qget<0>(X1, v);
+  fe_qget<1>(Y1, v);
+  fe_add(ypx, Y1, X1);
+  fe_sub(ymx, Y1, X1);
+  fe_qsel(o1, c, ypx, ymx, v, v);
+  fe_mul(prod, o1, op);
+  fe PP, MM, Z2, TT, rX, rY, rZ, rT, a1, a2;
+  fe_qget<0>(PP, prod);
+  fe_qget<1>(MM, prod);
+  fe_qget<2>(Z2, prod);
+  fe_qget<3>(TT, prod);
+  fe_sub(rX, PP, MM);   // N
+  fe_add(rY, PP, MM);   // A
+  fe_addn(rZ, Z2, TT);  // N
+  fe_sub(rT, Z2, TT);   // N
+  fe_qsel(a1, c, rX, rY, rZ, rX);
+  fe_qsel(a2, c, rT, rZ, rT, rY);
+  fe_mul(v, a1, a2);
+}
+// the operand lane c needs from entry |d| of a comb row (CT_QUADS uint4: y+x, y-x, 2dxy limbs)
+MV_DEV void q_entry(fe& op, const uint4* row, int digit) {
+  const uint32_t c = qlane();
+  const bool neg = digit < 0;
+  const int e = neg ? -digit : digit;
+  // lane 0 takes y+x (y-x when negated), lane 1 the other, lane 3 2dxy, lane 2 the constant 2
+  const uint32_t part = c == 0 ? (neg ? 1u : 0u) : (c == 1 ? (neg ? 0u : 1u) : 2u);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(row + e * CT_QUADS) + 9 * part;
+#pragma unroll
+  for (int i = 0; i < 9; i++) op.v[i] = w[i];
+}
+MV_DEV void q_entry_fix(fe& op, int digit) {
+  const uint32_t c = qlane();
+  if (c == 3 && digit < 0) fe_neg(op, op);  // -(2dxy)
+  if (c == 2) fe_set(op, 2);
+}
+// sum over rows [r0, r1) of the comb entries of the signed radix-256 digits sd, coordinate form
+MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int r1) {
+  qp_identity(v);
+  fe op;
+  int dg = digit256(sd, r0);
+  q_entry(op, tab + (size_t)r0 * CT_ROW, dg);
+#pragma unroll 1
+  for (int i = r0; i < r1; i++) {
+    fe cur = op;
+    const int dcur = dg;
+    if (i + 1 < r1) {  // the next entry in flight during this addition
+      dg = digit256(sd, i + 1);
+      q_entry(op, tab + (size_t)(i + 1) * CT_ROW, dg);
+    }
+    q_entry_fix(cur, dcur);
+    qp_madd(v, cur);
+  }
+}
+
+constexpr uint32_t C4_SIGS = 32;  // signatures per k_verify_comb4 workgroup
+__global__ void __launch_bounds__(512) k_verify_comb4(const uint8_t* msg, const uint8_t* __restrict__ sig,
+                                                       const uint8_t* __restrict__ pk,
+                                                       const uint32_t* __restrict__ key_idx, uint32_t n,
+                                                       const uint4* __restrict__ combB,
+                                                       const uint4* __restrict__ combA,
+                                                       const uint8_t* __restrict__ key_ok, uint8_t* __restrict__ status,
+                                                       const mvk::BlockVerdictOut bv) {
+  __shared__ uint32_t part[3][C4_SIGS][36];  // roles 1..3: partial sums, coordinate c at words 9c..
+  const uint32_t t = threadIdx.x, role = t >> 7, sq = (t >> 2) & (C4_SIGS - 1), c = t & 3u;
+  const uint32_t gid = blockIdx.x * C4_SIGS + sq;
+  const uint32_t idx = gid < n ? gid : n - 1;
+  const uint32_t key = key_idx[idx];
+  fe v;  // coordinate c of this role's point
+  bool okR = false, s_ok = false;
+  if (role == 0) {
+    uint32_t rw[8], sw[8];
+    load8(rw, sig + 64 * (size_t)idx);
+    load8(sw, sig + 64 * (size_t)idx + 32);
+    s_ok = sc_is_canonical(sw);
+    p3 R;
+    decompress1_q4(R, okR, rw);
+    fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
+  } else {
+    if (role == 1) {
+      uint32_t sw[8], sd[8];
+      load8(sw, sig + 64 * (size_t)idx + 32);
+      sc_recode256(sd, sw);
+      q_ct_sum(v, combB, sd, 0, CT_ROWS);
+    } else {
+      // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's bytes)
+      uint32_t kin[24], h[16], k[8], kd[8];
+      load8(kin, sig + 64 * (size_t)idx);
+      load8(kin + 8, pk + 32 * (size_t)key);
+      load8(kin + 16, msg + 32 * (size_t)idx);
+      sha512_short(h, kin, 96);
+      sc_reduce512(k, h);
+      sc_recode256(kd, k);
+      const int r0 = (role - 2) * (CT_ROWS / 2);
+      q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / 2);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
+  }
+  __syncthreads();
+  if (role == 0) {
+    fe w, S;
+#pragma unroll
+    for (int i = 0; i < 9; i++) S.v[i] = part[0][sq][9 * c + i];
+#pragma unroll
+    for (int i = 0; i < 9; i++) w.v[i] = part[1][sq][9 * c + i];
+    qp_add(S, w);
+#pragma unroll
+    for (int i = 0; i < 9; i++) w.v[i] = part[2][sq][9 * c + i];
+    qp_add(S, w);
+    // R' = S = [s]B - [k]A (the A tables hold -A); R - R': -S has X and T negated
+    fe nS;
+    fe_neg(nS, S);
+    fe_cmov(S, nS, c == 0 || c == 3);
+    qp_add(v, S);
+    qp_dbl(v);  // cofactor
+    qp_dbl(v);
+    qp_dbl(v);
+    // identity: X == 0 and Y == Z
+    fe Z;
+    fe_qget<2>(Z, v);
+    const bool zx = fe_is_zero(v);   // meaningful in lane 0
+    const bool eyz = fe_eq(v, Z);    // meaningful in lane 1
+    const uint32_t bits = (zx ? 1u : 0u) | (eyz ? 2u : 0u);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x00, 0xf, 0xf, false);  // lane 0's
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xf, 0xf, false);  // lane 1's
+    const bool ident = (b0 & 1u) && (b1 & 2u);
+    if (c == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
   }
 }
 
@@ -363,8 +540,18 @@ hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv) {
   if (n == 0) return hipSuccess;
   const BlockVerdictOut none{};
-  hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
-                     (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);
+  // four lanes per signature up to one workgroup's worth of calls per CU (the online path);
+  // MV_COMB_QUAD=0 / 1 forces the one-lane / four-lane kernel (A/B, tests)
+  const char* qe = getenv("MV_COMB_QUAD");  // read per call: the tests switch it in-process
+  const int quad_env = qe && *qe ? atoi(qe) : -1;
+  const bool quad = quad_env >= 0 ? quad_env != 0 : n <= 64u * 256u;
+  if (quad)
+    hipLaunchKernelGGL(mv::k_verify_comb4, dim3((n + mv::C4_SIGS - 1) / mv::C4_SIGS), dim3(512), 0, s, msg, sig, pk,
+                       key_idx, n,
+                       (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);
+  else
+    hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
+                       (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);
   return hipGetLastError();
 }
 

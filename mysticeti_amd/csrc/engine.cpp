@@ -383,9 +383,10 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
   return MV_OK;
 }
 
-// The device block pipeline on stream s (enqueue only): k_block_parse -> k_block_hash ->
-// signatures (batch path for >= MV_BATCH_MIN blocks, else committee verify) ->
-// k_block_verdict. d_md / d_bd may be null (scratch then).
+// The device block pipeline on stream s (enqueue only): k_block_ingest_hash (or, for small
+// batches of long blocks, k_block_ingest -> k_hash_comb_pre) -> signatures (batch path for
+// >= MV_BATCH_MIN blocks, else committee verify) -> k_block_verdict. d_md / d_bd may be null
+// (scratch then).
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
                          const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
                          hipStream_t s) {
@@ -403,12 +404,19 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
       HIPCHK(ctx, hipStreamWaitEvent(s, dev.blk_done[slot], 0));
     }
   }
+  // small batches of long blocks: the comb verify's signature-only half beside the hash
+  // bytes per block from which the split pays (MV_COMB_SPLIT_BYTES: tests and experiments; 0 = never)
+  const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
+  const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
+  const bool batch = !(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN;
+  const bool split = !batch && !(ctx->flags & MV_FLAG_NO_COMB) && split_bytes && buf_bytes >= split_bytes * (uint64_t)n;
   // scratch: stage | pre_off | pre_len | sig | key_idx | facts | claimed | sig status | md | bd
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t nn = n;
   size_t o = 0;
   const size_t o_stage = o;
-  o += al(buf_bytes + 256);
+  const bool need_stage = split || getenv("MV_BLK_FUSED") != nullptr;  // the two-kernel form stages P || sig
+  o += need_stage ? al(buf_bytes + 256) : al(256);
   const size_t o_poff = o;
   o += al(8 * nn);
   const size_t o_plen = o;
@@ -427,12 +435,6 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   o += al(32 * nn);
   const size_t o_bd = o;
   o += al(32 * nn);
-  // small batches of long blocks: the comb verify's signature-only half beside the hash
-  // bytes per block from which the split pays (MV_COMB_SPLIT_BYTES: tests and experiments; 0 = never)
-  const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
-  const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
-  const bool batch = !(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN;
-  const bool split = !batch && !(ctx->flags & MV_FLAG_NO_COMB) && split_bytes && buf_bytes >= split_bytes * nn;
   const size_t o_q = o;
   if (split) o += 2 * al(144 * nn) + al(nn);
   HIPCHK(ctx, dev.blk[slot].ensure(o));
@@ -452,16 +454,29 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   if (st != MV_OK) return st;
   auto mark = [&](int i) -> hipError_t { return evs.empty() ? hipSuccess : hipEventRecord(evs[i], s); };
   HIPCHK(ctx, mark(0));
-  HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
-                                      com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
-  HIPCHK(ctx, mark(1));
   uint8_t* rbuf = (uint8_t*)(b + o_q);
   uint8_t* sbuf = rbuf + al(144 * nn);
   uint8_t* qflags = sbuf + al(144 * nn);
-  if (split)  // the hash, and beside it on workgroups of their own the signature-only terms
-    HIPCHK(ctx, mvk::launch_hash_comb_pre(stage, poff, plen, n, md, bd, sig, dev.combB.p, rbuf, sbuf, qflags, s));
-  else
-    HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
+  // the parse and both digests in one kernel, the pre-image streamed through LDS
+  // (ingest_hash.hip); MV_BLK_FUSED=0: the two-kernel form (k_block_ingest staging the
+  // pre-image in HBM, then k_b2_quad), which the split comb path always uses
+  static const bool fused_ih = [] {
+    const char* e = getenv("MV_BLK_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  if (fused_ih && !split) {
+    HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
+                                              com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
+    HIPCHK(ctx, mark(1));
+  } else {
+    HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
+                                        com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
+    HIPCHK(ctx, mark(1));
+    if (split)  // the hash, and beside it on workgroups of their own the signature-only terms
+      HIPCHK(ctx, mvk::launch_hash_comb_pre(stage, poff, plen, n, md, bd, sig, dev.combB.p, rbuf, sbuf, qflags, s));
+    else
+      HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
+  }
   // a block whose digest does not match is rejected ahead of its signature (types.rs:327-332):
   // s >= l takes it out of the batch equation, so a tampered block never fails the batch (the
   // per-signature paths need no gate: the verdict puts the digest first)

@@ -97,6 +97,13 @@ hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uin
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s);
+// ingest_hash.hip: the block parse of launch_block_parse and both BLAKE2b digests in one
+// kernel, one quad per block, the pre-image streamed through LDS (never staged in HBM).
+// buf_bytes bounds the blocks' extent in buf (16 readable bytes past it).
+hipError_t launch_block_ingest_hash(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off, const uint64_t* len,
+                                    uint32_t n, const uint64_t* stakes, uint32_t n_auth, uint64_t epoch,
+                                    uint64_t quorum_thr, uint8_t* sig, uint32_t* key_idx, uint32_t* facts,
+                                    uint8_t* claimed, uint8_t* md, uint8_t* bd, hipStream_t s);
 // sig[i]'s s := 2^256 - 1 (outside the batch equation) for every parsed block whose computed
 // digest differs from its claimed one
 hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* digest, const uint32_t* facts, uint32_t n,

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include "fe25519.h"
+#include "fe_q4.h"
 #include "ge25519.h"
 #include "hash_dev.h"
 #include "kernels.h"
@@ -498,6 +499,32 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
 #pragma unroll
       for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
       return;
+    }
+    // four lanes per element (fe_q4.h): every lane of a quad must hold the same input
+    case 16: {
+      feq qa, qb, qr;
+      feq_from_fe(qa, a);
+      feq_from_fe(qb, b);
+      feq_mul(qr, qa, qb);
+      fe_from_feq(r, qr);
+      fe_canon(r, r);
+      break;
+    }
+    case 17: {
+      feq qa, qr;
+      feq_from_fe(qa, a);
+      feq_pow_p58(qr, qa);
+      fe_from_feq(r, qr);
+      fe_canon(r, r);
+      break;
+    }
+    case 18: {  // a^(2^50) by repeated squaring
+      feq qa, qr;
+      feq_from_fe(qa, a);
+      feq_sqn(qr, qa, 50);
+      fe_from_feq(r, qr);
+      fe_canon(r, r);
+      break;
     }
     case 10: fe_set(r, sc_is_canonical(x) ? 1 : 0); break;
     case 11: {  // [a]B encoding for a scalar a < 2^253

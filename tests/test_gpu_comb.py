@@ -91,3 +91,40 @@ def test_ragged_sizes(engine, n):
     sig[n - 1, 0] ^= 1
     st = engine.ed25519_verify(msg, sig, key_idx=ki)
     assert st[n - 1] == 1 and (st[: n - 1] == 0).all()
+
+
+def test_four_lane_and_one_lane_comb_kernels_agree(engine):
+    """k_verify_comb4 (four lanes per signature, the online path) and k_verify_comb (one lane)
+    give identical verdicts on a committee batch with corrupted signatures, undecodable R,
+    s >= l and an undecodable key, and both match the oracle."""
+    import os
+
+    rng = np.random.default_rng(47)
+    na, n = 20, 300
+    seeds = rng.integers(0, 256, size=(na, 32), dtype=np.uint8)
+    pks, _ = engine.ed25519_sign(seeds, np.zeros((na, 32), np.uint8))
+    pks = pks.copy()
+    y = 2
+    while O.point_decodes(y.to_bytes(32, "little")):
+        y += 1
+    pks[7] = np.frombuffer(y.to_bytes(32, "little"), np.uint8)  # does not decode: MalformedPublicKey
+    engine.set_committee(pks, np.ones(na, np.uint64))
+    ki = rng.integers(0, na, size=n).astype(np.uint32)
+    msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    _, sig = engine.ed25519_sign(seeds[ki], msg)
+    sig = sig.copy()
+    sig[1::7, 40] ^= 4                  # corrupted s
+    sig[2::11, 63] |= 0xF0              # s >= l
+    sig[3::13, :32] = 0xFF              # R with y >= p (decodes or not, as ZIP-215 says)
+    sig[5::17, 0] ^= 1                  # corrupted R
+    out = {}
+    try:
+        for mode in ("0", "1"):
+            os.environ["MV_COMB_QUAD"] = mode
+            out[mode] = engine.ed25519_verify(msg, sig, key_idx=ki)
+    finally:
+        os.environ.pop("MV_COMB_QUAD", None)
+    assert (out["0"] == out["1"]).all(), np.nonzero(out["0"] != out["1"])[0][:10]
+    ref = O.verify_batch(pks[ki], sig, msg)
+    assert (out["1"] == ref).all()
+    assert (out["1"] == 0).sum() > n // 2 and (out["1"] == 2).any() and (out["1"] == 1).any()

@@ -109,6 +109,28 @@ def test_sha512_64(engine):
         assert o.astype("<u4").tobytes() == hashlib.sha512(m).digest()
 
 
+def test_quad_lane_field_ops(engine):
+    """fe_q4.h (four lanes per element, the online path's R decode): products, the
+    (p-5)/8 power and 50 repeated squarings, against Python big integers, on edge values and
+    random ones. Every lane of a quad carries the same input."""
+    r = random.Random(8)
+    items = pairs(r, 200)
+    rep = [it for it in items for _ in range(4)]
+    out = run(engine, 16, rep)
+    for k, (a, b) in enumerate(items):
+        want = (a % 2**256) * (b % 2**256) % P
+        for j in range(4):
+            assert val(out[4 * k + j][:8]) == want, (a, b, j)
+    out = run(engine, 17, rep)
+    for k, (a, b) in enumerate(items):
+        want = pow(a % 2**256, (P - 5) // 8, P)
+        assert val(out[4 * k][:8]) == want, a
+        assert all(val(out[4 * k + j][:8]) == want for j in range(4))
+    out = run(engine, 18, rep)
+    for k, (a, b) in enumerate(items):
+        assert val(out[4 * k][:8]) == pow(a % 2**256, 2**50, P), a
+
+
 def test_sha512_96(engine):
     """The 96-byte form the challenge k = SHA-512(R || A || M) uses (crypto.rs:188 via
     ed25519-consensus): selftest op 15 hashes the 64 input bytes followed by their first 32."""
