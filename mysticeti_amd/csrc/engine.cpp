@@ -105,10 +105,14 @@ struct Device {
   hipEvent_t slot_done[kSlots] = {};
   bool slot_used[kSlots] = {};
   int next_slot = 0;
-  // the batch flags of each slot's last call, copied to pinned host words behind it; read
-  // (without blocking) once slot_done has completed: flag_groups[slot] groups pending
-  uint32_t* h_flags = nullptr;  // kSlots x kFlagWords, pinned
-  uint32_t flag_groups[kSlots] = {};
+  // the batch flags of each call, copied to pinned host words behind it, in a ring larger
+  // than the scratch ring: read (without blocking) once flag_ev has completed;
+  // flag_groups[e] groups pending. A call blocks the host only with kFlagRing calls in flight.
+  static constexpr int kFlagRing = 16;
+  uint32_t* h_flags = nullptr;  // kFlagRing x kFlagWords, pinned
+  uint32_t flag_groups[kFlagRing] = {};
+  hipEvent_t flag_ev[kFlagRing] = {};
+  int flag_next = 0;
   // single-verify scratch (k_verify's per-wave tables), same ring
   DevBuf sscr[kSlots];
   hipEvent_t sscr_done[kSlots] = {};
@@ -274,9 +278,13 @@ void keep_events(mv_ctx* ctx, int device, int first_stage, std::vector<hipEvent_
 // Accounts the batch flags of every slot whose last call has completed (non-blocking):
 // counters, and the adaptive group policy (a failed equation arms the guard).
 void poll_flags(mv_ctx* ctx, Device& dev) {
-  for (int k = 0; k < Device::kSlots; k++) {
+  for (int k = 0; k < Device::kFlagRing; k++) {
     const uint32_t ng = dev.flag_groups[k];
-    if (!ng || hipEventQuery(dev.slot_done[k]) != hipSuccess) continue;
+    if (!ng) continue;
+    if (hipEventQuery(dev.flag_ev[k]) != hipSuccess) {
+      (void)hipGetLastError();  // hipErrorNotReady: still running
+      continue;
+    }
     dev.flag_groups[k] = 0;
     const uint32_t* f = dev.h_flags + k * Device::kFlagWords;
     ctx->batches++;
@@ -308,17 +316,18 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   dev.next_slot = (slot + 1) % Device::kSlots;
   if (!dev.slot_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.slot_done[slot], hipEventDisableTiming));
   if (!dev.h_flags) {
-    HIPCHK(ctx, hipHostMalloc((void**)&dev.h_flags, sizeof(uint32_t) * Device::kSlots * Device::kFlagWords,
+    HIPCHK(ctx, hipHostMalloc((void**)&dev.h_flags, sizeof(uint32_t) * Device::kFlagRing * Device::kFlagWords,
                               hipHostMallocDefault));
-    memset(dev.h_flags, 0, sizeof(uint32_t) * Device::kSlots * Device::kFlagWords);
+    memset(dev.h_flags, 0, sizeof(uint32_t) * Device::kFlagRing * Device::kFlagWords);
   }
-  if (dev.slot_used[slot]) {
-    if (dev.flag_groups[slot]) {  // the slot's previous call must be accounted before its words are reused
-      HIPCHK(ctx, hipEventSynchronize(dev.slot_done[slot]));
-      poll_flags(ctx, dev);
-    }
-    HIPCHK(ctx, hipStreamWaitEvent(s, dev.slot_done[slot], 0));
+  const int fe = dev.flag_next;
+  dev.flag_next = (fe + 1) % Device::kFlagRing;
+  if (!dev.flag_ev[fe]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.flag_ev[fe], hipEventDisableTiming));
+  if (dev.flag_groups[fe]) {  // kFlagRing calls in flight: the oldest must be accounted before its words are reused
+    HIPCHK(ctx, hipEventSynchronize(dev.flag_ev[fe]));
+    poll_flags(ctx, dev);
   }
+  if (dev.slot_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.slot_done[slot], 0));  // device-side order only
   const uint32_t groups = pick_groups(ctx);
   // scratch for the largest group count, so the adaptive policy never reallocates
   HIPCHK(ctx, dev.bscr[slot].ensure(mvk::batch_scratch_bytes(n, mvk::BATCH_MAX_GROUPS)));
@@ -342,11 +351,12 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   keep_events(ctx, dev.id, 0, evs);
   if (flag_dst) HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, hipMemcpyDeviceToDevice, s));
   const uint32_t ng = (n + mvk::batch_group_size(n, groups) - 1) / mvk::batch_group_size(n, groups);
-  HIPCHK(ctx, hipMemcpyAsync(dev.h_flags + slot * Device::kFlagWords, flag, sizeof(uint32_t) * (1 + ng),
+  HIPCHK(ctx, hipMemcpyAsync(dev.h_flags + fe * Device::kFlagWords, flag, sizeof(uint32_t) * (1 + ng),
                              hipMemcpyDeviceToHost, s));
   HIPCHK(ctx, hipEventRecord(dev.slot_done[slot], s));
+  HIPCHK(ctx, hipEventRecord(dev.flag_ev[fe], s));
   dev.slot_used[slot] = true;
-  dev.flag_groups[slot] = ng;
+  dev.flag_groups[fe] = ng;
   return MV_OK;
 }
 
@@ -1230,6 +1240,8 @@ void mv_destroy(mv_ctx* ctx) {
       for (DevBuf* b : {&dev.bscr[k], &dev.vscr[k], &dev.blk[k], &dev.sscr[k]}) b->release();
     for (hipEvent_t ev : dev.slot_done)
       if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : dev.flag_ev)
+      if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.sscr_done)
       if (ev) (void)hipEventDestroy(ev);
     for (int k = 0; k < 2; k++) {
@@ -1664,30 +1676,25 @@ static mv_status wal_run(mv_ctx* ctx, Device& dev, const uint8_t* d_img, uint64_
   auto mark = [&](std::vector<hipEvent_t>& e, int i) -> hipError_t {
     return e.empty() ? hipSuccess : hipEventRecord(e[i], s);
   };
-  for (;;) {
-    HIPCHK(ctx, dev.wal_rec.ensure(8 * (size_t)nmaps * cap_pm));
-    HIPCHK(ctx, dev.wal_mcount.ensure(4 * (size_t)nmaps));
-    HIPCHK(ctx, dev.wal_mflag.ensure(nmaps));
-    HIPCHK(ctx, mark(ew, 0));
-    HIPCHK(ctx, mvk::launch_wal_walk(d_img, size, end_pos, map_bits, nmaps, cap_pm, dev.wal_rec.as<unsigned long long>(),
-                                     dev.wal_mcount.as<uint32_t>(), dev.wal_mflag.as<uint8_t>(), s));
-    HIPCHK(ctx, mark(ew, 1));
-    HIPCHK(ctx, hipMemcpyAsync(mcount.data(), dev.wal_mcount.p, 4 * (size_t)nmaps, hipMemcpyDeviceToHost, s));
-    HIPCHK(ctx, hipMemcpyAsync(mflag.data(), dev.wal_mflag.p, nmaps, hipMemcpyDeviceToHost, s));
-    HIPCHK(ctx, hipStreamSynchronize(s));
-    // WalIterator order: map after map while each one hands over to the next
-    nincl = 0;
-    total = 0;
-    uint32_t maxc = 0;
-    for (uint32_t m = 0; m < nmaps; m++) {
-      if (mflag[m] == mvk::WAL_MAP_EMPTY) break;
-      nincl = m + 1;
-      total += mcount[m];
-      maxc = std::max(maxc, mcount[m]);
-      if (mflag[m] != mvk::WAL_MAP_NEXT) break;
-    }
-    if (maxc <= cap_pm) break;
-    cap_pm = maxc;  // a map held more entries than the first guess: walk again with room for them
+  HIPCHK(ctx, dev.wal_rec.ensure(8 * (size_t)nmaps * cap_pm));
+  HIPCHK(ctx, dev.wal_mcount.ensure(4 * (size_t)nmaps));
+  HIPCHK(ctx, dev.wal_mflag.ensure(nmaps));
+  HIPCHK(ctx, mark(ew, 0));
+  HIPCHK(ctx, mvk::launch_wal_walk(d_img, size, end_pos, map_bits, nmaps, cap_pm, nullptr,
+                                   dev.wal_rec.as<unsigned long long>(), dev.wal_mcount.as<uint32_t>(),
+                                   dev.wal_mflag.as<uint8_t>(), s));
+  HIPCHK(ctx, mark(ew, 1));
+  HIPCHK(ctx, hipMemcpyAsync(mcount.data(), dev.wal_mcount.p, 4 * (size_t)nmaps, hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipMemcpyAsync(mflag.data(), dev.wal_mflag.p, nmaps, hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipStreamSynchronize(s));
+  // WalIterator order: map after map while each one hands over to the next
+  uint32_t maxc = 0;
+  for (uint32_t m = 0; m < nmaps; m++) {
+    if (mflag[m] == mvk::WAL_MAP_EMPTY) break;
+    nincl = m + 1;
+    total += mcount[m];
+    maxc = std::max(maxc, mcount[m]);
+    if (mflag[m] != mvk::WAL_MAP_NEXT) break;
   }
   keep_events(ctx, dev.id, kWalStage0, ew);
   if (total == 0) {
@@ -1703,8 +1710,14 @@ static mv_status wal_run(mv_ctx* ctx, Device& dev, const uint8_t* d_img, uint64_
   HIPCHK(ctx, dev.wal_ent.ensure(8 * total));
   HIPCHK(ctx, dev.wal_ff.ensure(8));
   HIPCHK(ctx, hipMemcpyAsync(dev.wal_moff.p, moff.data(), 8 * (size_t)nincl, hipMemcpyHostToDevice, s));
-  HIPCHK(ctx, mvk::launch_wal_compact(dev.wal_rec.as<unsigned long long>(), cap_pm, dev.wal_mcount.as<uint32_t>(),
-                                      dev.wal_moff.as<uint64_t>(), nincl, dev.wal_ent.as<unsigned long long>(), s));
+  if (maxc <= cap_pm) {  // every map's records fit the first walk: compact them
+    HIPCHK(ctx, mvk::launch_wal_compact(dev.wal_rec.as<unsigned long long>(), cap_pm, dev.wal_mcount.as<uint32_t>(),
+                                        dev.wal_moff.as<uint64_t>(), nincl, dev.wal_ent.as<unsigned long long>(), s));
+  } else {  // a map held more entries than the first guess: walk again straight into the entry list
+    HIPCHK(ctx, mvk::launch_wal_walk(d_img, size, end_pos, map_bits, nincl, 0, dev.wal_moff.as<uint64_t>(),
+                                     dev.wal_ent.as<unsigned long long>(), dev.wal_mcount.as<uint32_t>(),
+                                     dev.wal_mflag.as<uint8_t>(), s));
+  }
   HIPCHK(ctx, hipMemsetAsync(dev.wal_ff.p, 0xff, 8, s));
   HIPCHK(ctx, mark(ec, 0));
   HIPCHK(ctx, mvk::launch_wal_crc(d_img, size, dev.wal_ent.as<unsigned long long>(), total, dev.wal_tab.as<uint32_t>(),

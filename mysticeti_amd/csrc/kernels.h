@@ -119,10 +119,13 @@ void wal_build_tables(uint32_t* out);
 hipError_t launch_crc32(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                         const uint32_t* tables, uint32_t* out, int cus, hipStream_t s);
 // one lane per map: records (position | walk status << 60) of map m at rec[m * cap_pm ..], the
-// record count (may exceed cap_pm: nothing past it is stored) and how the iteration leaves the map
+// record count (may exceed cap_pm: nothing past it is stored) and how the iteration leaves the map.
+// moff (optional, a second walk): map m's records at rec[moff[m] ..], mcount[m] of them (the
+// first walk's counts, read by the kernel)
 constexpr uint8_t WAL_MAP_EMPTY = 0, WAL_MAP_NEXT = 1, WAL_MAP_END = 2, WAL_MAP_BAD = 3;
 hipError_t launch_wal_walk(const uint8_t* img, uint64_t size, uint64_t end_pos, uint32_t map_bits, uint32_t nmaps,
-                           uint32_t cap_pm, unsigned long long* rec, uint32_t* mcount, uint8_t* mflag, hipStream_t s);
+                           uint32_t cap_pm, const uint64_t* moff, unsigned long long* rec, uint32_t* mcount,
+                           uint8_t* mflag, hipStream_t s);
 hipError_t launch_wal_compact(const unsigned long long* rec, uint32_t cap_pm, const uint32_t* mcount,
                               const uint64_t* moff, uint32_t nmaps, unsigned long long* ent, hipStream_t s);
 // one wave per entry: header, payload crc, verdict (MV_WAL_*); *first_fail = min failing index

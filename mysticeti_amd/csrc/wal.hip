@@ -182,6 +182,7 @@ MV_DEV uint64_t le64_bounded(const uint8_t* img, uint64_t size, uint64_t p) {
 // record = position | status << 60 (status: MV_WAL_OK for an entry whose crc is still to check)
 __global__ void __launch_bounds__(64) k_wal_walk(const uint8_t* __restrict__ img, uint64_t size, uint64_t end_pos,
                                                  uint32_t map_bits, uint32_t nmaps, uint32_t cap_pm,
+                                                 const uint64_t* __restrict__ moff,
                                                  unsigned long long* __restrict__ rec, uint32_t* __restrict__ mcount,
                                                  uint8_t* __restrict__ mflag) {
   const uint32_t m = blockIdx.x * 64 + threadIdx.x;
@@ -190,7 +191,9 @@ __global__ void __launch_bounds__(64) k_wal_walk(const uint8_t* __restrict__ img
   uint64_t p = start;
   uint32_t count = 0;
   uint8_t flag;
-  unsigned long long* r = rec + (size_t)m * cap_pm;
+  // moff (the second walk): map m's records at rec + moff[m], as many as the first walk counted
+  unsigned long long* r = moff ? rec + moff[m] : rec + (size_t)m * cap_pm;
+  if (moff) cap_pm = mcount[m];
   for (;;) {
     if (p >= end_pos) {
       flag = p == start ? MAP_EMPTY : MAP_END;
@@ -331,10 +334,11 @@ hipError_t launch_crc32(const uint8_t* buf, const uint64_t* off, const uint64_t*
 }
 
 hipError_t launch_wal_walk(const uint8_t* img, uint64_t size, uint64_t end_pos, uint32_t map_bits, uint32_t nmaps,
-                           uint32_t cap_pm, unsigned long long* rec, uint32_t* mcount, uint8_t* mflag, hipStream_t s) {
+                           uint32_t cap_pm, const uint64_t* moff, unsigned long long* rec, uint32_t* mcount,
+                           uint8_t* mflag, hipStream_t s) {
   if (nmaps == 0) return hipSuccess;
   hipLaunchKernelGGL(mv::wal::k_wal_walk, dim3((nmaps + 63) / 64), dim3(64), 0, s, img, size, end_pos, map_bits, nmaps,
-                     cap_pm, rec, mcount, mflag);
+                     cap_pm, moff, rec, mcount, mflag);
   return hipGetLastError();
 }
 

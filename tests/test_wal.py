@@ -184,6 +184,25 @@ def test_gpu_wal_block_entries_production_maps(engine):
 
 
 @pytest.mark.gpu
+def test_gpu_wal_dense_maps_second_walk(engine):
+    """Maps holding more entries than the walk's first per-map guess (4,096): the second walk
+    writes each map's records at its own offset (no maps x max-count buffer), as the reference
+    iterates them (wal.rs:226-346)."""
+    rng = np.random.default_rng(12)
+    w = W.WalWriter(W.MAP_BITS_PRODUCTION)
+    for i in range(9000):  # ~60 B entries: two maps hold > 4,096 each
+        w.write(i % 5, rng.integers(0, 256, size=int(rng.integers(0, 64)), dtype=np.uint8).tobytes())
+    w.write(3, rng.integers(0, 256, size=(1 << 24) - 100, dtype=np.uint8).tobytes())  # forces a map change
+    for i in range(5000):
+        w.write(1, rng.integers(0, 256, size=40, dtype=np.uint8).tobytes())
+    img = w.image()
+    pos, tag, ln, st = engine.wal_verify(img, w.pos, W.MAP_BITS_PRODUCTION)
+    opos, otag, oln, ost = O.wal_iter(np.frombuffer(img, dtype=np.uint8), w.pos, W.MAP_BITS_PRODUCTION)
+    assert len(pos) == 14001 and (st == 0).all()
+    assert pos.tolist() == opos.tolist() and ln.tolist() == oln.tolist() and tag.tolist() == otag.tolist()
+
+
+@pytest.mark.gpu
 def test_gpu_dev_wal_and_crc(engine):
     import torch
 
