@@ -267,7 +267,50 @@ def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     return 0 if res["correct"] else 1
 
 
-def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstreams=2, cpu=True) -> dict:
+def config4_host_fed(eng, torch, dev, buf, off, ln, nb, span, n_host, calls=3) -> dict:
+    """Config 4 fed from host memory (PCIe-inclusive, BASELINE.md 3 row 4 "streamed in chunks"):
+    `n_host` config-4 blocks in one pageable host buffer through mv_verify_blocks, which packs
+    them into pinned staging in chunks and overlaps chunk c + 1's pack and H2D with chunk c's
+    device pipeline. Best of `calls` calls. Beside it the measured pinned H2D bandwidth and the
+    bound it sets: H2D GB/s / bincode bytes per block."""
+    reps = (n_host + nb - 1) // nb
+    base_bytes = int(off[-1] + ln[-1])
+    hbuf = np.zeros(reps * span + 64, dtype=np.uint8)
+    hbuf[: reps * span].reshape(reps, span)[:, :base_bytes] = buf[:base_bytes]
+    hoff = (np.arange(reps, dtype=np.uint64)[:, None] * np.uint64(span) + off.astype(np.uint64)[None, :]).reshape(-1)[:n_host]
+    hlen = np.tile(ln.astype(np.uint64), reps)[:n_host]
+    st = None
+    best = None
+    eng.verify_blocks_packed(hbuf, hoff[:nb].copy(), hlen[:nb].copy())  # warm the staging
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        st, _, _ = eng.verify_blocks_packed(hbuf, hoff, hlen)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    # pinned H2D bandwidth (1 GiB, torch's pinned allocator, the copy engine alone)
+    h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    d = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d = 3 * (1 << 30) / (time.perf_counter() - t0)
+    del h, d
+    L = float(np.mean(hlen))
+    rate = n_host / best
+    return {"value": round(rate, 1), "unit": "blocks/s", "blocks": n_host,
+            "bincode_GB": round(float(hlen.sum()) / 1e9, 3), "seconds": round(best, 4),
+            "h2d_GBps_pinned": round(h2d / 1e9, 1), "pcie_bound_blocks_per_s": round(h2d / L, 1),
+            "frac_of_pcie_bound": round(rate / (h2d / L), 4), "correct": bool((st == 0).all()),
+            "note": "mv_verify_blocks on one pageable host buffer (the engine packs into pinned staging in "
+                    "256-MiB chunks, chunk c+1 packed and copied while chunk c runs), best of "
+                    f"{calls} calls; the PCIe bound is the measured pinned H2D rate over {L:.0f} B per block"}
+
+
+def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstreams=2, cpu=True,
+                    host_blocks=1 << 18) -> dict:
     """Config 4 on this rank's GPU: `n` HBM-resident config-4 blocks per step through
     mv_dev_verify_blocks (device parse -> pre-image -> 2 x BLAKE2b -> batch ZIP-215 -> verdicts);
     value = blocks/s over all ranks (weak scaling). Used by `--workload config4` and by the
@@ -375,14 +418,21 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     roof = None
     from bench import pmc_traffic
 
-    traffic, traffic_src = pmc_traffic("k_b2_quad", "c4")
+    kname = "k_b2_quad"
+    if os.environ.get("MV_BLK_FUSED") == "1":  # the fused parse + hash kernel (the "parse" stage)
+        kname, hash_ms = "k_block_ingest_hash", stage_ms.get("parse")
+    traffic, traffic_src = pmc_traffic(kname, "c4")
     if hash_ms:
         ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
-        roof = {"bound": "valu", "kernel": "k_b2_quad", "kernel_ms": hash_ms,
+        roof = {"bound": "valu", "kernel": kname, "kernel_ms": hash_ms,
                 "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
                 "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
                                   f"algorithmic) x {W_BLAKE2B_OPS} ops"}
+    host_fed = None
+    if int(os.environ.get("RANK", "0")) == 0 and host_blocks > 0:
+        host_fed = config4_host_fed(eng, torch, dev, buf, off, ln, nb, span, host_blocks)
+        ok &= host_fed["correct"]
     ok = all_ranks_ok(ok, dist)
     out = {"value": round(value, 1), "unit": "blocks/s (= verified block signatures/s)",
            "ms_per_step": round(elapsed / steps * 1e3, 4),
@@ -398,7 +448,8 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
                         "note": "stage_ms: 3 post-run steps on one stream (roofline); "
                                 "stage_ms_as_run: HIP events with overlapping streams",
                         "hbm_bincode_GBps": round(n * L / (elapsed / steps) / 1e9, 1)},
-           "cpu_baseline": cpu_res, "correct": bool(ok), "sha256_msg_digests_first_corpus": msg_sha}
+           "cpu_baseline": cpu_res, "host_fed": host_fed, "correct": bool(ok),
+           "sha256_msg_digests_first_corpus": msg_sha}
     if cpu_res:
         out["speedup_vs_cpu"] = {"all_cores": round(value / world / cpu_res["value"], 1),
                                  "single_core": round(value / world / cpu_res["single_core_value"], 1)}

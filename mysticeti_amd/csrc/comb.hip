@@ -31,7 +31,7 @@
 #include <stdlib.h>
 
 #include "fe25519.h"
-#include "fe_q4.h"
+#include "fe_r16.h"
 #include "ge25519.h"
 #include "hash_dev.h"
 #include "quad25519.h"
@@ -200,21 +200,23 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* msg, const u
   }
 }
 
-// ---------------------------------------------------------------- four lanes per signature
-// k_verify_comb4: the same predicate with every chain on FOUR lanes per signature, for the
-// online path (64-block calls), where k_verify_comb's latency is its longest single-lane chain:
-// the R decode (~265 field operations) and the 32 B-table additions each take ~80 us on one
-// lane. 512 threads per 32 signatures, four roles of 128 lanes (one quad per signature; two
-// waves per SIMD leave each 256 VGPRs):
-//   role 0  ZIP-215 decode of R with the (p-5)/8 power on fe_q4.h (each product split over
-//           the quad), then the combination below
-//   role 1  the 32 C_B entries of s's digits, point additions on quad25519.h's layout (lane c
-//           holds coordinate c; lane c loads only the entry coordinate its product needs)
-//   role 2  SHA-512 k; the C_A entries of k's digits 0..15
-//   role 3  SHA-512 k; the C_A entries of k's digits 16..31
-// Role 0 then adds the three partial sums (LDS), subtracts them from R, clears the cofactor
-// and tests for the identity. Same predicate, same status as k_verify_comb.
-MV_DEV void decompress1_q4(p3& A, bool& okA, const uint32_t ea[8]) {
+// ---------------------------------------------------------------- online path: short chains
+// k_verify_comb16: the same predicate with every dependent chain cut short, for the online
+// path (64-block calls), where k_verify_comb's latency is its longest single-lane chain: the
+// R decode (~265 field operations) and the 32 B-table additions, ~80 us each on one lane.
+// 16 signatures per 512-thread workgroup:
+//   role 0 (waves 0..3, one 16-lane DPP row per signature): ZIP-215 decode of R, its (p-5)/8
+//           power on fe_r16.h (~2x shorter per product than one lane), then the combination
+//   role 1 (wave 4, one quad per signature): the C_B entries of s's digits 0..15, point
+//           additions on quad25519.h's layout (lane c holds coordinate c; it loads only the
+//           entry coordinate its product needs)
+//   role 2 (wave 5): the C_B entries of s's digits 16..31
+//   role 3 (wave 6): SHA-512 k; the C_A entries of k's digits 0..15
+//   role 4 (wave 7): SHA-512 k; the C_A entries of k's digits 16..31
+// Role 0's lanes 0..3 of each row then add the four partial sums (LDS) as a quad, subtract them
+// from R, clear the cofactor and test for the identity. Same predicate, same status as
+// k_verify_comb.
+MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8]) {
   fe d, one, ya, ua, va, t, v3a, ea7, pa, xa, n;
   fe_const(d, K_D);
   fe_set(one, 1);
@@ -226,10 +228,10 @@ MV_DEV void decompress1_q4(p3& A, bool& okA, const uint32_t ea[8]) {
   fe_sq(t, va); fe_mul(v3a, t, va);
   fe_sq(t, v3a); fe_mul(ea7, t, va); fe_mul(ea7, ea7, ua);
   {
-    feq x, r;
-    feq_from_fe(x, ea7);
-    feq_pow_p58(r, x);
-    fe_from_feq(pa, r);
+    fer x, r;
+    fer_from_fe(x, ea7);
+    fer_pow_p58(r, x);
+    fe_from_fer(pa, r);
   }
   fe_mul(pa, pa, v3a); fe_mul(pa, pa, ua);
   okA = sqrt_ratio_finish(xa, ua, va, pa);
@@ -279,54 +281,64 @@ MV_DEV void q_entry_fix(fe& op, int digit) {
   if (c == 3 && digit < 0) fe_neg(op, op);  // -(2dxy)
   if (c == 2) fe_set(op, 2);
 }
-// sum over rows [r0, r1) of the comb entries of the signed radix-256 digits sd, coordinate form
+// sum over rows [r0, r1) of the comb entries of the signed radix-256 digits sd, coordinate form;
+// the entries of the next two rows are in flight during an addition
 MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int r1) {
   qp_identity(v);
-  fe op;
-  int dg = digit256(sd, r0);
-  q_entry(op, tab + (size_t)r0 * CT_ROW, dg);
+  fe op0, op1;
+  int d0 = digit256(sd, r0), d1 = r0 + 1 < r1 ? digit256(sd, r0 + 1) : 0;
+  q_entry(op0, tab + (size_t)r0 * CT_ROW, d0);
+  if (r0 + 1 < r1) q_entry(op1, tab + (size_t)(r0 + 1) * CT_ROW, d1);
 #pragma unroll 1
   for (int i = r0; i < r1; i++) {
-    fe cur = op;
-    const int dcur = dg;
-    if (i + 1 < r1) {  // the next entry in flight during this addition
-      dg = digit256(sd, i + 1);
-      q_entry(op, tab + (size_t)(i + 1) * CT_ROW, dg);
+    fe cur = op0;
+    const int dcur = d0;
+    op0 = op1;
+    d0 = d1;
+    if (i + 2 < r1) {
+      d1 = digit256(sd, i + 2);
+      q_entry(op1, tab + (size_t)(i + 2) * CT_ROW, d1);
     }
     q_entry_fix(cur, dcur);
     qp_madd(v, cur);
   }
 }
 
-constexpr uint32_t C4_SIGS = 32;  // signatures per k_verify_comb4 workgroup
-__global__ void __launch_bounds__(512) k_verify_comb4(const uint8_t* msg, const uint8_t* __restrict__ sig,
-                                                       const uint8_t* __restrict__ pk,
-                                                       const uint32_t* __restrict__ key_idx, uint32_t n,
-                                                       const uint4* __restrict__ combB,
-                                                       const uint4* __restrict__ combA,
-                                                       const uint8_t* __restrict__ key_ok, uint8_t* __restrict__ status,
-                                                       const mvk::BlockVerdictOut bv) {
-  __shared__ uint32_t part[3][C4_SIGS][36];  // roles 1..3: partial sums, coordinate c at words 9c..
-  const uint32_t t = threadIdx.x, role = t >> 7, sq = (t >> 2) & (C4_SIGS - 1), c = t & 3u;
-  const uint32_t gid = blockIdx.x * C4_SIGS + sq;
+constexpr uint32_t C16_SIGS = 16;  // signatures per k_verify_comb16 workgroup
+constexpr uint32_t C16_THREADS = 16 * C16_SIGS + 4 * 4 * C16_SIGS;
+__global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* __restrict__ sig,
+                                                               const uint8_t* __restrict__ pk,
+                                                               const uint32_t* __restrict__ key_idx, uint32_t n,
+                                                               const uint4* __restrict__ combB,
+                                                               const uint4* __restrict__ combA,
+                                                               const uint8_t* __restrict__ key_ok,
+                                                               uint8_t* __restrict__ status,
+                                                               const mvk::BlockVerdictOut bv) {
+  __shared__ uint32_t part[4][C16_SIGS][36];  // roles 1..4: partial sums, coordinate c at words 9c..
+  const uint32_t t = threadIdx.x;
+  const bool row_role = t < 16 * C16_SIGS;
+  const uint32_t role = row_role ? 0u : 1u + ((t - 16 * C16_SIGS) >> 6);
+  const uint32_t sq = row_role ? t >> 4 : (t >> 2) & (C16_SIGS - 1), c = t & 3u;
+  const uint32_t gid = blockIdx.x * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
   fe v;  // coordinate c of this role's point
   bool okR = false, s_ok = false;
-  if (role == 0) {
+  if (role == 0) {  // every lane of the row holds the signature's R and s
     uint32_t rw[8], sw[8];
     load8(rw, sig + 64 * (size_t)idx);
     load8(sw, sig + 64 * (size_t)idx + 32);
     s_ok = sc_is_canonical(sw);
     p3 R;
-    decompress1_q4(R, okR, rw);
+    decompress1_r16(R, okR, rw);
     fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
   } else {
-    if (role == 1) {
+    if (role <= 2) {
       uint32_t sw[8], sd[8];
       load8(sw, sig + 64 * (size_t)idx + 32);
       sc_recode256(sd, sw);
-      q_ct_sum(v, combB, sd, 0, CT_ROWS);
+      const int r0 = (role - 1) * (CT_ROWS / 2);
+      q_ct_sum(v, combB, sd, r0, r0 + CT_ROWS / 2);
     } else {
       // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's bytes)
       uint32_t kin[24], h[16], k[8], kd[8];
@@ -336,23 +348,23 @@ __global__ void __launch_bounds__(512) k_verify_comb4(const uint8_t* msg, const 
       sha512_short(h, kin, 96);
       sc_reduce512(k, h);
       sc_recode256(kd, k);
-      const int r0 = (role - 2) * (CT_ROWS / 2);
+      const int r0 = (role - 3) * (CT_ROWS / 2);
       q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / 2);
     }
 #pragma unroll
     for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
   }
   __syncthreads();
-  if (role == 0) {
+  if (role == 0) {  // lanes 0..3 of each row form the quad (the other lanes repeat it)
     fe w, S;
 #pragma unroll
     for (int i = 0; i < 9; i++) S.v[i] = part[0][sq][9 * c + i];
 #pragma unroll
-    for (int i = 0; i < 9; i++) w.v[i] = part[1][sq][9 * c + i];
-    qp_add(S, w);
+    for (int j = 1; j < 4; j++) {
 #pragma unroll
-    for (int i = 0; i < 9; i++) w.v[i] = part[2][sq][9 * c + i];
-    qp_add(S, w);
+      for (int i = 0; i < 9; i++) w.v[i] = part[j][sq][9 * c + i];
+      qp_add(S, w);
+    }
     // R' = S = [s]B - [k]A (the A tables hold -A); R - R': -S has X and T negated
     fe nS;
     fe_neg(nS, S);
@@ -370,7 +382,7 @@ __global__ void __launch_bounds__(512) k_verify_comb4(const uint8_t* msg, const 
     const uint32_t b0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x00, 0xf, 0xf, false);  // lane 0's
     const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xf, 0xf, false);  // lane 1's
     const bool ident = (b0 & 1u) && (b1 & 2u);
-    if (c == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
+    if ((t & 15u) == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
   }
 }
 
@@ -540,15 +552,16 @@ hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv) {
   if (n == 0) return hipSuccess;
   const BlockVerdictOut none{};
-  // four lanes per signature up to one workgroup's worth of calls per CU (the online path);
-  // MV_COMB_QUAD=0 / 1 forces the one-lane / four-lane kernel (A/B, tests)
+  // short chains (k_verify_comb16: a row per R decode, quads for the table sums) up to 64
+  // workgroups of 256 signatures' worth (the online path); MV_COMB_QUAD=0 / 1 forces
+  // k_verify_comb / k_verify_comb16 (A/B, tests)
   const char* qe = getenv("MV_COMB_QUAD");  // read per call: the tests switch it in-process
   const int quad_env = qe && *qe ? atoi(qe) : -1;
   const bool quad = quad_env >= 0 ? quad_env != 0 : n <= 64u * 256u;
   if (quad)
-    hipLaunchKernelGGL(mv::k_verify_comb4, dim3((n + mv::C4_SIGS - 1) / mv::C4_SIGS), dim3(512), 0, s, msg, sig, pk,
-                       key_idx, n,
-                       (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);
+    hipLaunchKernelGGL(mv::k_verify_comb16, dim3((n + mv::C16_SIGS - 1) / mv::C16_SIGS), dim3(mv::C16_THREADS), 0, s,
+                       msg, sig, pk, key_idx, n, (const uint4*)combB, (const uint4*)combA, key_ok, status,
+                       bv ? *bv : none);
   else
     hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);

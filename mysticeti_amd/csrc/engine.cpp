@@ -118,17 +118,23 @@ struct Device {
   hipEvent_t sscr_done[kSlots] = {};
   bool sscr_used[kSlots] = {};
   int sscr_next = 0;
-  DevBuf blk[kSlots];
-  hipEvent_t blk_done[kSlots] = {};
-  bool blk_used[kSlots] = {};
+  // block-pipeline scratch: one slot per pass set, so passes on different streams never
+  // wait for each other's scratch
+  static constexpr int kBlkSlots = 4;
+  DevBuf blk[kBlkSlots];
+  hipEvent_t blk_done[kBlkSlots] = {};
+  bool blk_used[kBlkSlots] = {};
   int blk_next = 0;
   HostBuf h_in, h_out;
-  // mv_verify_blocks passes (the submission queue): two sets of pinned staging, device
-  // buffers and a stream each, so pass k + 1 is packed and enqueued while pass k runs
+  // mv_verify_blocks passes (the submission queue): kPassSets sets of pinned staging, device
+  // buffers and a stream each, so pass k + 1 is packed and enqueued while passes k, k - 1, ...
+  // run (an online pass is a few workgroups: passes on distinct hardware queues run side by side)
+  static constexpr int kPassSets = 4;
+  hipStream_t qstream[kPassSets] = {};  // sets 2 and up (0: `stream`, 1: pstream[1])
   struct PassSet {
     HostBuf h_in, h_out;
     DevBuf bytes, out2;
-    hipStream_t stream = nullptr;  // set 0: `stream`, set 1: pstream[1] (distinct hardware queues)
+    hipStream_t stream = nullptr;  // set 0: `stream`, set 1: pstream[1], set k >= 2: qstream[k]
     hipEvent_t done = nullptr;
     // the chunk in flight: items [lo, lo + m) of `it`, outputs in h_out when finished
     const void* it = nullptr;
@@ -136,7 +142,7 @@ struct Device {
     uint32_t m = 0;
     bool inflight = false;
   };
-  PassSet pset[2];
+  PassSet pset[kPassSets];
   bool committee_loaded = false;
   // WAL replay (wal.hip): crc tables, walk records, per-map counts / flags / offsets, entries,
   // the image and outputs of host-buffer calls
@@ -186,7 +192,8 @@ struct mv_ctx {
   std::condition_variable q_cv;
   std::deque<BlockReq*> q;
   bool q_packing = false;                // a combining caller is packing / enqueueing a pass
-  bool q_set_busy[2] = {false, false};   // pass sets with a pass in flight
+  bool q_set_busy[Device::kPassSets] = {};  // pass sets with a pass in flight
+  int q_sets = 0;                          // pass sets in use (MV_PASS_SETS, default kPassSets)
   std::atomic<uint64_t> q_calls{0}, q_passes{0};
 };
 
@@ -403,7 +410,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   if (n == 0) return MV_OK;
   const mvh::Committee& com = ctx->committee;
   const int slot = dev.blk_next;
-  dev.blk_next = (slot + 1) % Device::kSlots;
+  dev.blk_next = (slot + 1) % Device::kBlkSlots;
   if (!dev.blk_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.blk_done[slot], hipEventDisableTiming));
   if (dev.blk_used[slot]) {
     // skip the cross-stream wait when the slot's previous pass has finished (the common case
@@ -425,7 +432,13 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   const size_t nn = n;
   size_t o = 0;
   const size_t o_stage = o;
-  const bool need_stage = split || getenv("MV_BLK_FUSED") != nullptr;  // the two-kernel form stages P || sig
+  // k_block_ingest stages the pre-image in HBM, then k_b2_quad hashes it. MV_BLK_FUSED=1: the
+  // parse and both digests in one kernel with the pre-image streamed through LDS
+  // (ingest_hash.hip; 2 waves/SIMD: config 4 measured 81 M blocks/s against 101 M for the
+  // two-kernel form). The split comb path always uses the two-kernel form.
+  const char* fe = getenv("MV_BLK_FUSED");  // read per call: the tests switch it in-process
+  const bool fused_ih = fe && fe[0] == '1';
+  const bool need_stage = split || !fused_ih;  // the two-kernel form stages P || sig
   o += need_stage ? al(buf_bytes + 256) : al(256);
   const size_t o_poff = o;
   o += al(8 * nn);
@@ -467,13 +480,6 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   uint8_t* rbuf = (uint8_t*)(b + o_q);
   uint8_t* sbuf = rbuf + al(144 * nn);
   uint8_t* qflags = sbuf + al(144 * nn);
-  // the parse and both digests in one kernel, the pre-image streamed through LDS
-  // (ingest_hash.hip); MV_BLK_FUSED=0: the two-kernel form (k_block_ingest staging the
-  // pre-image in HBM, then k_b2_quad), which the split comb path always uses
-  static const bool fused_ih = [] {
-    const char* e = getenv("MV_BLK_FUSED");
-    return !(e && e[0] == '0');
-  }();
   if (fused_ih && !split) {
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
@@ -712,9 +718,12 @@ mv_status ensure_pass_set(mv_ctx* ctx, Device& dev, int s) {
   if (!ps.stream) {
     if (s == 0) {
       ps.stream = dev.stream;
-    } else {
+    } else if (s == 1) {
       if (!dev.pstream[1]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[1], hipStreamNonBlocking));
       ps.stream = dev.pstream[1];
+    } else {
+      if (!dev.qstream[s]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.qstream[s], hipStreamNonBlocking));
+      ps.stream = dev.qstream[s];
     }
   }
   if (!ps.done) HIPCHK(ctx, hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
@@ -1181,6 +1190,13 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
     const int g = atoi(e);
     if (g >= 1 && g <= mvk::BATCH_MAX_GROUPS) ctx->base_groups = (uint32_t)g;
   }
+  // two passes in flight: four measured worse on 16 concurrent 1-block callers (68.0 k vs
+  // 72.2 k blocks/s, p99 203 vs 146 us; profiles/r03/c5_pass_sets.txt)
+  ctx->q_sets = 2;
+  if (const char* e = getenv("MV_PASS_SETS")) {  // A/B: block passes in flight (2 .. kPassSets)
+    const int k = atoi(e);
+    if (k >= 2 && k <= Device::kPassSets) ctx->q_sets = k;
+  }
   {
     FILE* f = fopen("/dev/urandom", "rb");
     size_t got = f ? fread(ctx->secret, 1, sizeof(ctx->secret), f) : 0;
@@ -1237,7 +1253,8 @@ void mv_destroy(mv_ctx* ctx) {
                       &dev.wal_st})
       b->release();
     for (int k = 0; k < Device::kSlots; k++)
-      for (DevBuf* b : {&dev.bscr[k], &dev.vscr[k], &dev.blk[k], &dev.sscr[k]}) b->release();
+      for (DevBuf* b : {&dev.bscr[k], &dev.vscr[k], &dev.sscr[k]}) b->release();
+    for (DevBuf& b : dev.blk) b.release();
     for (hipEvent_t ev : dev.slot_done)
       if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.flag_ev)
@@ -1264,6 +1281,8 @@ void mv_destroy(mv_ctx* ctx) {
       ps.out2.release();
       if (ps.done) (void)hipEventDestroy(ps.done);
     }
+    for (hipStream_t st : dev.qstream)
+      if (st) (void)hipStreamDestroy(st);
     if (dev.stream) (void)hipStreamDestroy(dev.stream);
   }
   delete ctx;
@@ -1454,13 +1473,23 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
   // packed and a free pass set takes every queued request (its own included) into one pass,
   // packs and enqueues it, then lets the next caller pack the following pass into the other
   // set while its own runs on the device. n - 1 peer tasks each submitting a block or two
-  // (net_sync.rs:214-221, 314-386) thus share GPU round trips, two passes in flight.
+  // (net_sync.rs:214-221, 314-386) thus share GPU round trips, up to q_sets passes in flight.
   mv_ctx::BlockReq req{buf, off, len, n, status, msg_digest, block_digest};
   ctx->q_calls++;
   std::unique_lock<std::mutex> ql(ctx->q_mu);
   ctx->q.push_back(&req);
+  auto any_busy = [ctx] {
+    for (int k = 0; k < ctx->q_sets; k++)
+      if (ctx->q_set_busy[k]) return true;
+    return false;
+  };
+  auto mark_all = [ctx](bool v) {
+    for (int k = 0; k < ctx->q_sets; k++) ctx->q_set_busy[k] = v;
+  };
   while (!req.done) {
-    const int s = !ctx->q_set_busy[0] ? 0 : (!ctx->q_set_busy[1] ? 1 : -1);
+    int s = -1;
+    for (int k = 0; k < ctx->q_sets && s < 0; k++)
+      if (!ctx->q_set_busy[k]) s = k;
     if (ctx->q_packing || s < 0 || ctx->q.empty()) {
       ctx->q_cv.wait(ql);
       continue;
@@ -1477,9 +1506,9 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     const bool big = blocks > (uint64_t)ctx->max_batch * nd || bytes > chunk_bytes_limit() * nd;
     ctx->q_packing = true;
     if (big)
-      while (ctx->q_set_busy[0] || ctx->q_set_busy[1]) ctx->q_cv.wait(ql);
+      while (any_busy()) ctx->q_cv.wait(ql);
     const int set = big ? -1 : s;
-    if (big) ctx->q_set_busy[0] = ctx->q_set_busy[1] = true;
+    if (big) mark_all(true);
     else ctx->q_set_busy[s] = true;
     ql.unlock();
     run_block_requests(ctx, batch, set, [ctx] {
@@ -1489,7 +1518,7 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     });
     ql.lock();
     for (auto* r : batch) r->done = true;
-    if (big) ctx->q_set_busy[0] = ctx->q_set_busy[1] = false;
+    if (big) mark_all(false);
     else ctx->q_set_busy[s] = false;
     ctx->q_cv.notify_all();
   }

@@ -21,6 +21,7 @@
 
 #include "fe25519.h"
 #include "fe_q4.h"
+#include "fe_r16.h"
 #include "ge25519.h"
 #include "hash_dev.h"
 #include "kernels.h"
@@ -523,6 +524,32 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
       feq_from_fe(qa, a);
       feq_sqn(qr, qa, 50);
       fe_from_feq(r, qr);
+      fe_canon(r, r);
+      break;
+    }
+    // one DPP row per element (fe_r16.h): every lane of a 16-lane row must hold the same input
+    case 19: {
+      fer ra, rb, rr;
+      fer_from_fe(ra, a);
+      fer_from_fe(rb, b);
+      fer_mul(rr, ra, rb, r16::consts());
+      fe_from_fer(r, rr);
+      fe_canon(r, r);
+      break;
+    }
+    case 20: {
+      fer ra, rr;
+      fer_from_fe(ra, a);
+      fer_pow_p58(rr, ra);
+      fe_from_fer(r, rr);
+      fe_canon(r, r);
+      break;
+    }
+    case 21: {  // a^(2^50) by repeated squaring
+      fer ra, rr;
+      fer_from_fe(ra, a);
+      fer_sqn(rr, ra, 50, r16::consts());
+      fe_from_fer(r, rr);
       fe_canon(r, r);
       break;
     }

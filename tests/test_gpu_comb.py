@@ -93,8 +93,9 @@ def test_ragged_sizes(engine, n):
     assert st[n - 1] == 1 and (st[: n - 1] == 0).all()
 
 
-def test_four_lane_and_one_lane_comb_kernels_agree(engine):
-    """k_verify_comb4 (four lanes per signature, the online path) and k_verify_comb (one lane)
+def test_short_chain_and_one_lane_comb_kernels_agree(engine):
+    """k_verify_comb16 (the online path: R decoded on a 16-lane row, table sums on quads) and
+    k_verify_comb (one lane per signature)
     give identical verdicts on a committee batch with corrupted signatures, undecodable R,
     s >= l and an undecodable key, and both match the oracle."""
     import os

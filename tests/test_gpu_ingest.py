@@ -15,6 +15,14 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["two_kernel", "fused"], autouse=True)
+def ingest_form(request, monkeypatch):
+    """Every test runs on both device ingest forms: k_block_ingest + k_b2_quad (the default)
+    and the fused k_block_ingest_hash (ingest_hash.hip, MV_BLK_FUSED=1)."""
+    monkeypatch.setenv("MV_BLK_FUSED", "1" if request.param == "fused" else "0")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def host_engine():
     with M.Engine(devices=(0,), host_parse=True) as e:

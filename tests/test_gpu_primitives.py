@@ -131,6 +131,27 @@ def test_quad_lane_field_ops(engine):
         assert val(out[4 * k][:8]) == pow(a % 2**256, 2**50, P), a
 
 
+def test_row_lane_field_ops(engine):
+    """fe_r16.h (one 16-lane DPP row per element, the online path's R decode): products, the
+    (p-5)/8 power and 50 repeated squarings, against Python big integers, on edge values and
+    random ones. Every lane of a row carries the same input (whole rows: 16 copies)."""
+    r = random.Random(9)
+    items = pairs(r, 200)
+    rep = [it for it in items for _ in range(16)]
+    out = run(engine, 19, rep)
+    for k, (a, b) in enumerate(items):
+        want = (a % 2**256) * (b % 2**256) % P
+        for j in range(16):
+            assert val(out[16 * k + j][:8]) == want, (a, b, j)
+    out = run(engine, 20, rep)
+    for k, (a, b) in enumerate(items):
+        want = pow(a % 2**256, (P - 5) // 8, P)
+        assert all(val(out[16 * k + j][:8]) == want for j in range(16)), a
+    out = run(engine, 21, rep)
+    for k, (a, b) in enumerate(items):
+        assert val(out[16 * k][:8]) == pow(a % 2**256, 2**50, P), a
+
+
 def test_sha512_96(engine):
     """The 96-byte form the challenge k = SHA-512(R || A || M) uses (crypto.rs:188 via
     ed25519-consensus): selftest op 15 hashes the 64 input bytes followed by their first 32."""
