@@ -393,12 +393,10 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 //   k_hash_comb_pre  workgroups [0, nh): quad BLAKE2b of 16 blocks each (blake2b_quad.h);
 //                    [nh, nh + np): s < l and the ZIP-215 decode of R, 64 signatures each;
 //                    [nh + np, nh + 2 np): -[s]B on C_B, 64 signatures each
-//   k_comb_post (8 waves): k = SHA-512(R || A || M) mod l on wave 0 (alone on its SIMD; wave 7
-//                    meanwhile R - [s]B), digits through LDS; wave w: the A-table entries of
-//                    k's digits 4w .. 4w + 3 (4 additions);
-//                    a 3-level tree over the waves' sums; wave 0: R - [s]B - sum (the tables
-//                    hold -A), [8], identity test.
-// k_comb_post's latency is a SHA-512 and 4 + 5 additions instead of the R decode.
+//   k_comb_post      k = SHA-512(R || A || M) mod l, then the A-table entries of k's digits
+//                    on eight roles of quads, a tree over the roles, [8], identity test (below).
+// k_comb_post's latency is a SHA-512 and 4 + 5 two-product-deep additions instead of the R
+// decode.
 __global__ void __launch_bounds__(64) k_hash_comb_pre(const uint8_t* __restrict__ stage,
                                                       const uint64_t* __restrict__ poff,
                                                       const uint64_t* __restrict__ plen, uint8_t* __restrict__ md,
@@ -444,92 +442,105 @@ __global__ void __launch_bounds__(64) k_hash_comb_pre(const uint8_t* __restrict_
   }
 }
 
-constexpr int POST_WAVES = 8;
-__global__ void __launch_bounds__(64 * POST_WAVES) k_comb_post(const uint8_t* msg,  // not restrict: bv writes it
-                                                              const uint8_t* __restrict__ sig,
-                                                              const uint8_t* __restrict__ pk,
-                                                              const uint32_t* __restrict__ key_idx, uint32_t n,
-                                                              const uint4* __restrict__ combA,
-                                                              const uint8_t* __restrict__ key_ok,
-                                                              const uint4* __restrict__ rbuf,
-                                                              const uint4* __restrict__ sbuf,
-                                                              const uint8_t* __restrict__ qflags,
-                                                              uint8_t* __restrict__ status,
-                                                              const mvk::BlockVerdictOut bv) {
-  __shared__ uint4 part[POST_WAVES][9][64];  // per-wave partial sums, [quad][lane]
-  __shared__ uint32_t skd[8][64];            // k's signed radix-256 digits, [word][lane]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t gid = blockIdx.x * 64 + lane;
+// k_comb_post: 16 signatures per 512-thread workgroup, eight roles of one quad per signature
+// (quad25519.h's coordinate layout: every point operation is two products deep):
+//   phase 1  wave 0: k = SHA-512(R || A || M) mod l, one lane per signature, digits to LDS;
+//            role 7 meanwhile: R - [s]B from k_hash_comb_pre's two points
+//   phase 2  role w: the C_A entries of k's digits 4w .. 4w + 3 (four additions)
+//   phase 3  a 3-level tree over the roles' sums; role 0: R - [s]B - sum (the tables hold -A),
+//            [8], identity test
+constexpr uint32_t POST_SIGS = 16;
+constexpr int POST_ROLES = 8;
+__global__ void __launch_bounds__(4 * POST_SIGS * POST_ROLES) k_comb_post(const uint8_t* msg,  // not restrict: bv writes it
+                                                                         const uint8_t* __restrict__ sig,
+                                                                         const uint8_t* __restrict__ pk,
+                                                                         const uint32_t* __restrict__ key_idx, uint32_t n,
+                                                                         const uint4* __restrict__ combA,
+                                                                         const uint8_t* __restrict__ key_ok,
+                                                                         const uint4* __restrict__ rbuf,
+                                                                         const uint4* __restrict__ sbuf,
+                                                                         const uint8_t* __restrict__ qflags,
+                                                                         uint8_t* __restrict__ status,
+                                                                         const mvk::BlockVerdictOut bv) {
+  __shared__ uint32_t part[POST_ROLES][POST_SIGS][36];  // per-role sums, coordinate c at words 9c..
+  __shared__ uint32_t skd[8][POST_SIGS];                // k's signed radix-256 digits, [word][sig]
+  const uint32_t t = threadIdx.x, role = t / (4 * POST_SIGS), sq = (t >> 2) & (POST_SIGS - 1), c = t & 3u;
+  const uint32_t gid = blockIdx.x * POST_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
-  uint4 q[9];
-  p3 acc, X;
-  if (wave == 0) {  // k = SHA-512(R || A || M) mod l once, alone on its SIMD
+  if (t < POST_SIGS) {  // k once per signature (wave 0, lanes 0..15)
+    const uint32_t g2 = blockIdx.x * POST_SIGS + t, i2 = g2 < n ? g2 : n - 1;
     uint32_t kin[24], h[16], k[8], kd[8];
-    load8(kin, sig + 64 * (size_t)idx);
-    load8(kin + 8, pk + 32 * (size_t)key);
-    load8(kin + 16, msg + 32 * (size_t)idx);
+    load8(kin, sig + 64 * (size_t)i2);
+    load8(kin + 8, pk + 32 * (size_t)key_idx[i2]);
+    load8(kin + 16, msg + 32 * (size_t)i2);
     sha512_short(h, kin, 96);
     sc_reduce512(k, h);
     sc_recode256(kd, k);
 #pragma unroll
-    for (int i = 0; i < 8; i++) skd[i][lane] = kd[i];
-  } else if (wave == POST_WAVES - 1) {  // meanwhile R - [s]B (k_hash_comb_pre), into the spare slot 0
-    p3 R;
+    for (int i = 0; i < 8; i++) skd[i][t] = kd[i];
+  } else if (role == POST_ROLES - 1) {  // R - [s]B (k_hash_comb_pre's R and -[s]B), coordinate form
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(rbuf + (size_t)idx * 9) + 9 * c;
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sbuf + (size_t)idx * 9) + 9 * c;
+    fe v, w;
 #pragma unroll
-    for (int k = 0; k < 9; k++) q[k] = rbuf[(size_t)idx * 9 + k];
-    quads_to_p3(R, q);
+    for (int i = 0; i < 9; i++) {
+      v.v[i] = rw[i];
+      w.v[i] = sw[i];
+    }
+    qp_add(v, w);
 #pragma unroll
-    for (int k = 0; k < 9; k++) q[k] = sbuf[(size_t)idx * 9 + k];
-    quads_to_p3(X, q);
-    ct_acc(R, X);
-    p3_to_quads(q, R);
-#pragma unroll
-    for (int k = 0; k < 9; k++) part[0][k][lane] = q[k];
+    for (int i = 0; i < 9; i++) part[0][sq][9 * c + i] = v.v[i];  // role 0's slot is free until phase 3
   }
   __syncthreads();
+  fe v;
   {
     uint32_t kd[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) kd[i] = skd[i][lane];
-    const int r0 = wave * (CT_ROWS / POST_WAVES);
-    ct_sum(acc, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / POST_WAVES);  // -[k_w]A
+    for (int i = 0; i < 8; i++) kd[i] = skd[i][sq];
+    const int r0 = (int)role * (CT_ROWS / POST_ROLES);
+    q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / POST_ROLES);  // -[k_w]A
   }
-  // tree over the waves' partial sums: wave w < h adds wave w + h's
-  for (int h = POST_WAVES / 2; h >= 1; h >>= 1) {
-    if (wave >= h && wave < 2 * h) {
-      p3_to_quads(q, acc);
+  fe rs;  // R - [s]B, read by role 0 before its slot is overwritten
+  if (role == 0) {
 #pragma unroll
-      for (int k = 0; k < 9; k++) part[wave][k][lane] = q[k];
+    for (int i = 0; i < 9; i++) rs.v[i] = part[0][sq][9 * c + i];
+  }
+  __syncthreads();
+  // tree over the roles' sums: role w < h adds role w + h's
+  for (uint32_t h = POST_ROLES / 2; h >= 1; h >>= 1) {
+    if (role >= h && role < 2 * h) {
+#pragma unroll
+      for (int i = 0; i < 9; i++) part[role][sq][9 * c + i] = v.v[i];
     }
     __syncthreads();
-    if (wave < h) {
+    if (role < h) {
+      fe w;
 #pragma unroll
-      for (int k = 0; k < 9; k++) q[k] = part[wave + h][k][lane];
-      quads_to_p3(X, q);
-      ct_acc(acc, X);
+      for (int i = 0; i < 9; i++) w.v[i] = part[role + h][sq][9 * c + i];
+      qp_add(v, w);
     }
     __syncthreads();
   }
-  if (wave == 0) {
-    p3_neg(acc, acc);  // +[k]A
-#pragma unroll
-    for (int k = 0; k < 9; k++) q[k] = part[0][k][lane];
-    quads_to_p3(X, q);
-    ct_acc(acc, X);  // R - [s]B + [k]A = R - R'
-    p2 P;
-    p1p1 t;
-    P.X = acc.X;
-    P.Y = acc.Y;
-    P.Z = acc.Z;
-#pragma unroll 1
-    for (int d = 0; d < 3; d++) {  // cofactor
-      p2_dbl(t, P);
-      p1p1_to_p2(P, t);
-    }
-    const bool ident = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
+  if (role == 0) {
+    // v = -[k]A; R - [s]B + [k]A = R - R': negate v (X and T), add R - [s]B
+    fe nv;
+    fe_neg(nv, v);
+    fe_cmov(v, nv, c == 0 || c == 3);
+    qp_add(v, rs);
+    qp_dbl(v);  // cofactor
+    qp_dbl(v);
+    qp_dbl(v);
+    fe Z;
+    fe_qget<2>(Z, v);
+    const bool zx = fe_is_zero(v);  // meaningful in lane 0
+    const bool eyz = fe_eq(v, Z);   // meaningful in lane 1
+    const uint32_t bits = (zx ? 1u : 0u) | (eyz ? 2u : 0u);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x00, 0xf, 0xf, false);
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xf, 0xf, false);
+    const bool ident = (b0 & 1u) && (b1 & 2u);
     const uint8_t f = qflags[idx];
-    if (gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : (((f & 3) == 3 && ident) ? 0 : 1));
+    if (c == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : (((f & 3) == 3 && ident) ? 0 : 1));
   }
 }
 
@@ -584,7 +595,8 @@ hipError_t launch_comb_post(const uint8_t* msg, const uint8_t* sig, const uint8_
                             const BlockVerdictOut* bv) {
   if (n == 0) return hipSuccess;
   const BlockVerdictOut none{};
-  hipLaunchKernelGGL(mv::k_comb_post, dim3((n + 63) / 64), dim3(64 * mv::POST_WAVES), 0, s, msg, sig, pk, key_idx, n,
+  hipLaunchKernelGGL(mv::k_comb_post, dim3((n + mv::POST_SIGS - 1) / mv::POST_SIGS), dim3(4 * mv::POST_SIGS * mv::POST_ROLES),
+                     0, s, msg, sig, pk, key_idx, n,
                      (const uint4*)combA, key_ok, (const uint4*)rbuf, (const uint4*)sbuf, qflags, status, bv ? *bv : none);
   return hipGetLastError();
 }
