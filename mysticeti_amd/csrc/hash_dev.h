@@ -9,13 +9,33 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #ifndef MV_DEV
 #define MV_DEV __device__ __forceinline__
 #endif
 
 namespace mv {
 
-MV_DEV uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate right by a constant n (after inlining): two v_alignbit_b32, or a register swap
+MV_DEV uint64_t rotr64(uint64_t x, int n) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n == 32) return ((uint64_t)lo << 32) | hi;
+  if (n < 32)
+    return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+  return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, n - 32) << 32) | __builtin_amdgcn_alignbit(lo, hi, n - 32);
+}
+MV_DEV uint64_t shr64(uint64_t x, int n) {  // n < 32
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+}
+// 3-input logic per 32-bit half (v_bitop3_b32, gfx950): 0x96 = a ^ b ^ c, 0xE8 = majority
+template <int IMM>
+MV_DEV uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, IMM);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), IMM);
+  return ((uint64_t)hi << 32) | lo;
+}
 MV_DEV uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
 __constant__ const uint64_t SHA512_K[80] = {
@@ -42,29 +62,48 @@ MV_DEV void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
-// One compression; w[16] = the block as big-endian 64-bit words (clobbered).
-MV_DEV void sha512_compress(uint64_t st[8], uint64_t w[16]) {
-  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-  for (int r = 0; r < 80; r += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      if (r > 0) {
-        uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        w[j] += s0 + w[(j + 9) & 15] + s1;
-      }
-      uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-      uint64_t ch = (e & f) ^ (~e & g);
-      uint64_t t1 = h + S1 + ch + SHA512_K[r + j] + w[j];
-      uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-      uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
-      h = g; g = f; f = e; e = d + t1;
-      d = c; c = b; b = a; a = t1 + S0 + maj;
-    }
+// Round T of the compression, every index a constant: the a..h rotation is register renaming
+// (the slot of a round's new a is the old h's, of its new e the old d's), rotations are
+// v_alignbit_b32 pairs, the three-input XORs and the majority one v_bitop3_b32 per half, Ch a
+// v_bfi_b32 per half.
+template <int T>
+MV_DEV void sha512_round(uint64_t (&v)[8], uint64_t (&w)[16]) {
+  constexpr int j = T & 15, r = T & 7;
+  if constexpr (T >= 16) {
+    const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+    const uint64_t s0 = bitop3_64<0x96>(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+    const uint64_t s1 = bitop3_64<0x96>(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+    w[j] += s0 + w[(j + 9) & 15] + s1;
   }
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+  uint64_t& h = v[(15 - r) & 7];
+  uint64_t& d = v[(11 - r) & 7];
+  const uint64_t a = v[(8 - r) & 7], b = v[(9 - r) & 7], c = v[(10 - r) & 7];
+  const uint64_t e = v[(12 - r) & 7], f = v[(13 - r) & 7], g = v[(14 - r) & 7];
+  const uint64_t S1 = bitop3_64<0x96>(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+  const uint64_t ch = (e & f) | (~e & g);
+  const uint64_t t1 = h + S1 + ch + SHA512_K[T] + w[j];
+  const uint64_t S0 = bitop3_64<0x96>(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+  const uint64_t maj = bitop3_64<0xE8>(a, b, c);
+  d += t1;            // the next round's e
+  h = t1 + S0 + maj;  // the next round's a
+}
+template <int... T>
+MV_DEV void sha512_rounds(uint64_t (&v)[8], uint64_t (&w)[16], std::integer_sequence<int, T...>) {
+  (sha512_round<T>(v, w), ...);
+}
+
+// One compression; w[16] = the block as big-endian 64-bit words (clobbered). Straight-line
+// code: 80 rounds with constant indices (the looped form kept the state in a register array
+// indexed at run time and cost ~2.5x the instructions).
+MV_DEV void sha512_compress(uint64_t st[8], uint64_t w_in[16]) {
+  uint64_t v[8], w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = st[i];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = w_in[i];
+  sha512_rounds(v, w, std::make_integer_sequence<int, 80>{});
+#pragma unroll
+  for (int i = 0; i < 8; i++) st[i] += v[i];
 }
 
 // SHA-512 of up to 111 bytes given as little-endian 32-bit words (nbytes % 4 == 0);

@@ -9,6 +9,7 @@
 #include "fe25519.h"
 #include "fe_q4.h"
 #include "fe_r16.h"
+#include "hash_dev.h"
 
 using namespace mv;
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s\n", hipGetErrorString(e_)); return 1; } } while (0)
@@ -52,6 +53,18 @@ __global__ void __launch_bounds__(64) k_chain_r16(uint32_t* out, int iters) {
   out[threadIdx.x] = a.v;
 }
 
+// SHA-512 of 96 bytes (the challenge input), each input the previous digest's words
+__global__ void __launch_bounds__(64) k_chain_sha(uint32_t* out, int iters) {
+  uint32_t in[24], h[16];
+  for (int i = 0; i < 24; i++) in[i] = threadIdx.x * 7 + i;
+#pragma unroll 1
+  for (int it = 0; it < iters / 16; it++) {
+    sha512_short(h, in, 96);
+    for (int i = 0; i < 16; i++) in[i] = h[i];
+  }
+  out[threadIdx.x] = in[0] + in[5];
+}
+
 typedef void (*kfn)(uint32_t*, int);
 static int run(const char* name, kfn k, uint32_t* d) {
   hipEvent_t e0, e1;
@@ -79,7 +92,8 @@ int main() {
   uint32_t* d;
   CHECK(hipMalloc(&d, 64 * sizeof(uint32_t)));
   if (run("fe_sq (1 lane)", k_chain_sq, d) || run("fe_mul (1 lane)", k_chain_mul, d) ||
-      run("feq_sq (4 lanes)", k_chain_q4, d) || run("fer_sq (16-lane row)", k_chain_r16, d))
+      run("feq_sq (4 lanes)", k_chain_q4, d) || run("fer_sq (16-lane row)", k_chain_r16, d) ||
+      run("sha512_short 96 B (1 lane), per 16 ops = 1 hash", k_chain_sha, d))
     return 1;
   return 0;
 }
