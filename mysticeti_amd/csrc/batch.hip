@@ -530,9 +530,31 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* _
   const uint32_t g = (lin % span) / nsw, j = lin % nsw;
   const uint32_t sidx = (g * BV_NW + w) * nsw + j;  // segment index, row-major
   const uint32_t key0 = g * BV_NKG + w * BV_NB + j * seg;
-  p3 T, V;
+  // the running sum V waits in LDS ([word][thread]: conflict-free) while the bucket's points
+  // are added into T, so it holds no registers across the inner loop (no spill at 3 WG/CU)
+  __shared__ uint32_t sV[36][256];
+  const uint32_t tid = threadIdx.x;
+  auto v_load = [&](p3& V) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      V.X.v[i] = sV[i][tid];
+      V.Y.v[i] = sV[9 + i][tid];
+      V.Z.v[i] = sV[18 + i][tid];
+      V.T.v[i] = sV[27 + i][tid];
+    }
+  };
+  auto v_store = [&](const p3& V) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      sV[i][tid] = V.X.v[i];
+      sV[9 + i][tid] = V.Y.v[i];
+      sV[18 + i][tid] = V.Z.v[i];
+      sV[27 + i][tid] = V.T.v[i];
+    }
+  };
+  p3 T;
   p3_identity(T);
-  p3_identity(V);
+  if (seg > 1) v_store(T);  // V = identity
   const uint32_t e_lo = offs[key0];
   uint32_t e = offs[key0 + seg];
   uint4 q[7];
@@ -564,9 +586,18 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* _
       p1p1_to_p3(T, t);
     }
     b1 = b0;
-    if (seg > 1) p3_acc(V, T);
+    if (seg > 1) {
+      p3 V;
+      v_load(V);
+      p3_acc(V, T);
+      v_store(V);
+    }
   }
-  if (seg > 1) p3_store(segV, sidx, V);
+  if (seg > 1) {
+    p3 V;
+    v_load(V);
+    p3_store(segV, sidx, V);
+  }
   p3_store(segT, sidx, T);
 }
 

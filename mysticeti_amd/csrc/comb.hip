@@ -204,18 +204,16 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* msg, const u
 // k_verify_comb16: the same predicate with every dependent chain cut short, for the online
 // path (64-block calls), where k_verify_comb's latency is its longest single-lane chain: the
 // R decode (~265 field operations) and the 32 B-table additions, ~80 us each on one lane.
-// 16 signatures per 512-thread workgroup:
+// 16 signatures per 768-thread workgroup:
 //   role 0 (waves 0..3, one 16-lane DPP row per signature): ZIP-215 decode of R, its (p-5)/8
 //           power on fe_r16.h (~2x shorter per product than one lane), then the combination
-//   role 1 (wave 4, one quad per signature): the C_B entries of s's digits 0..15, point
-//           additions on quad25519.h's layout (lane c holds coordinate c; it loads only the
-//           entry coordinate its product needs)
-//   role 2 (wave 5): the C_B entries of s's digits 16..31
-//   role 3 (wave 6): SHA-512 k; the C_A entries of k's digits 0..15
-//   role 4 (wave 7): SHA-512 k; the C_A entries of k's digits 16..31
-// Role 0's lanes 0..3 of each row then add the four partial sums (LDS) as a quad, subtract them
-// from R, clear the cofactor and test for the identity. Same predicate, same status as
-// k_verify_comb.
+//   roles 1..4 (one wave each, one quad per signature): the C_B entries of s's digits in four
+//           blocks of 8 rows, point additions on quad25519.h's layout (lane c holds
+//           coordinate c; it loads only the entry coordinate its product needs)
+//   roles 5..8: SHA-512 k, then the C_A entries of k's digits in four blocks of 8 rows
+// A 3-level tree over the table roles' sums follows (LDS), then role 0's lanes 0..3 of each
+// row subtract the sum from R as a quad, clear the cofactor and test for the identity. Same
+// predicate, same status as k_verify_comb.
 MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8]) {
   fe d, one, ya, ua, va, t, v3a, ea7, pa, xa, n;
   fe_const(d, K_D);
@@ -304,8 +302,9 @@ MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int 
   }
 }
 
-constexpr uint32_t C16_SIGS = 16;  // signatures per k_verify_comb16 workgroup
-constexpr uint32_t C16_THREADS = 16 * C16_SIGS + 4 * 4 * C16_SIGS;
+constexpr uint32_t C16_SIGS = 16;   // signatures per k_verify_comb16 workgroup
+constexpr uint32_t C16_TROLES = 8;  // table-sum roles: four over the B rows, four over the A rows
+constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS;
 __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* __restrict__ sig,
                                                                const uint8_t* __restrict__ pk,
                                                                const uint32_t* __restrict__ key_idx, uint32_t n,
@@ -314,7 +313,8 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
                                                                const uint8_t* __restrict__ key_ok,
                                                                uint8_t* __restrict__ status,
                                                                const mvk::BlockVerdictOut bv) {
-  __shared__ uint32_t part[4][C16_SIGS][36];  // roles 1..4: partial sums, coordinate c at words 9c..
+  __shared__ uint32_t part[C16_TROLES][C16_SIGS][36];  // table roles' sums, coordinate c at words 9c..
+  constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);       // table rows per role
   const uint32_t t = threadIdx.x;
   const bool row_role = t < 16 * C16_SIGS;
   const uint32_t role = row_role ? 0u : 1u + ((t - 16 * C16_SIGS) >> 6);
@@ -333,12 +333,13 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
     decompress1_r16(R, okR, rw);
     fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
   } else {
-    if (role <= 2) {
+    const uint32_t tr = role - 1;  // 0 .. C16_TROLES / 2 - 1: B rows; then A rows
+    if (tr < C16_TROLES / 2) {
       uint32_t sw[8], sd[8];
       load8(sw, sig + 64 * (size_t)idx + 32);
       sc_recode256(sd, sw);
-      const int r0 = (role - 1) * (CT_ROWS / 2);
-      q_ct_sum(v, combB, sd, r0, r0 + CT_ROWS / 2);
+      const int r0 = (int)tr * ROWS;
+      q_ct_sum(v, combB, sd, r0, r0 + ROWS);
     } else {
       // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's bytes)
       uint32_t kin[24], h[16], k[8], kd[8];
@@ -348,23 +349,29 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
       sha512_short(h, kin, 96);
       sc_reduce512(k, h);
       sc_recode256(kd, k);
-      const int r0 = (role - 3) * (CT_ROWS / 2);
-      q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / 2);
+      const int r0 = (int)(tr - C16_TROLES / 2) * ROWS;
+      q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + ROWS);
     }
 #pragma unroll
-    for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
+    for (int i = 0; i < 9; i++) part[tr][sq][9 * c + i] = v.v[i];
   }
   __syncthreads();
+  // tree over the table roles' sums (role r < h adds role r + h's), then role 0
+  fe w;
+  for (uint32_t h = C16_TROLES / 2; h >= 1; h >>= 1) {
+    if (role >= 1 && role - 1 < h) {
+#pragma unroll
+      for (int i = 0; i < 9; i++) w.v[i] = part[role - 1 + h][sq][9 * c + i];
+      qp_add(v, w);
+#pragma unroll
+      for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
+    }
+    __syncthreads();
+  }
   if (role == 0) {  // lanes 0..3 of each row form the quad (the other lanes repeat it)
-    fe w, S;
+    fe S;
 #pragma unroll
     for (int i = 0; i < 9; i++) S.v[i] = part[0][sq][9 * c + i];
-#pragma unroll
-    for (int j = 1; j < 4; j++) {
-#pragma unroll
-      for (int i = 0; i < 9; i++) w.v[i] = part[j][sq][9 * c + i];
-      qp_add(S, w);
-    }
     // R' = S = [s]B - [k]A (the A tables hold -A); R - R': -S has X and T negated
     fe nS;
     fe_neg(nS, S);

@@ -1061,20 +1061,38 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   uint64_t bs64 = ((m + nb - 1) / nb + 1023) & ~1023ull;
   if (bs64 < MV_BATCH_MIN) bs64 = MV_BATCH_MIN;
   if (bs64 > ctx->max_batch) bs64 = ctx->max_batch;
-  const uint32_t bs = (uint32_t)bs64;
+  uint32_t bs = (uint32_t)bs64;
+  // the first batch's share (MV_STREAM_FIRST, A/B): a larger first batch shortens the last
+  // batch's sort, buckets and tail, which follow the last copy
+  static const double first_frac = [] {
+    const char* e = getenv("MV_STREAM_FIRST");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 && v < 1.0 ? v : 0.0;
+  }();
+  uint32_t b0 = bs;
+  if (first_frac > 0.0 && nb == 2) {
+    uint64_t f = ((uint64_t)(m * first_frac) + 1023) & ~1023ull;
+    if (f < MV_BATCH_MIN) f = MV_BATCH_MIN;
+    if (f > ctx->max_batch) f = ctx->max_batch;
+    if (f < m && m - f >= MV_BATCH_MIN && m - f <= ctx->max_batch) {
+      b0 = (uint32_t)f;
+      bs = (uint32_t)std::max<uint64_t>(m - f, 1);
+    }
+  }
+  const uint32_t cap = std::max(b0, bs);
   uint32_t chunk = 1u << chunk_log2;
-  while ((bs + chunk - 1) / chunk > (uint32_t)Device::kMaxChunks / 2) chunk <<= 1;
+  while ((cap + chunk - 1) / chunk > (uint32_t)Device::kMaxChunks / 2) chunk <<= 1;
   // chunk schedule: the first batch starts with small chunks (2^14, 2^15, ... signatures), so
   // the chip starts preparing after ~40 us of copying instead of a whole chunk's
   std::vector<uint32_t> sched[2];
   for (int b = 0; b < 2; b++) {
     uint32_t o = 0, c = b == 0 ? std::min<uint32_t>(chunk, 1u << 14) : chunk;
-    while (o < bs) {
+    while (o < cap) {
       sched[b].push_back(o);
       o += c;
       if (c < chunk) c *= 2;
     }
-    sched[b].push_back(bs);
+    sched[b].push_back(cap);
   }
   const size_t kb = pk ? 32 : 4;  // pk rows or committee key indices
   for (int b = 0; b < 2; b++) {
@@ -1082,10 +1100,10 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     if (!dev.pin_free[b]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[b], hipEventDisableTiming));
     for (int c = 0; c < Device::kMaxChunks; c++)
       if (!dev.chunk_ev[b][c]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.chunk_ev[b][c], hipEventDisableTiming));
-    HIPCHK(ctx, dev.pin_msg[b].ensure(32 * (size_t)bs));
-    HIPCHK(ctx, dev.pin_sig[b].ensure(64 * (size_t)bs));
-    HIPCHK(ctx, dev.pin_pk[b].ensure(kb * bs));
-    HIPCHK(ctx, dev.pin_st[b].ensure(bs));
+    HIPCHK(ctx, dev.pin_msg[b].ensure(32 * (size_t)cap));
+    HIPCHK(ctx, dev.pin_sig[b].ensure(64 * (size_t)cap));
+    HIPCHK(ctx, dev.pin_pk[b].ensure(kb * cap));
+    HIPCHK(ctx, dev.pin_st[b].ensure(cap));
   }
   HIPCHK(ctx, dev.h_out.ensure(m));
   uint8_t* hst = dev.h_out.as<uint8_t>();
@@ -1095,10 +1113,10 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   // queued behind another stream's kernels would serialise the pipeline)
   hipStream_t xs = dev.stream;
   uint64_t t = 0;
-  for (uint64_t i = lo; i < hi; i += bs, t++) {
+  for (uint64_t i = lo; i < hi; i += (t == 0 ? b0 : bs), t++) {
     const int b = (int)(t & 1);
     hipStream_t cs = dev.pstream[b];
-    const uint32_t k = (uint32_t)std::min<uint64_t>(bs, hi - i);
+    const uint32_t k = (uint32_t)std::min<uint64_t>(t == 0 ? b0 : bs, hi - i);
     // buffer b is free once batch t - 2 (or the previous call's last batch on it) is done
     HIPCHK(ctx, hipStreamWaitEvent(xs, dev.pin_free[b], 0));
     const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);

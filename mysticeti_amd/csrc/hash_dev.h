@@ -21,6 +21,10 @@ namespace mv {
 MV_DEV uint64_t rotr64(uint64_t x, int n) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   if (n == 32) return ((uint64_t)lo << 32) | hi;
+  if (n == 8 || n == 16 || n == 24) {  // byte rotations: v_perm_b32 (full rate; v_alignbit is half)
+    const uint32_t k = (uint32_t)n >> 3, sel = (k | (k + 1) << 8 | (k + 2) << 16 | (k + 3) << 24);
+    return ((uint64_t)__builtin_amdgcn_perm(lo, hi, sel) << 32) | __builtin_amdgcn_perm(hi, lo, sel);
+  }
   if (n < 32)
     return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
   return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, n - 32) << 32) | __builtin_amdgcn_alignbit(lo, hi, n - 32);

@@ -13,14 +13,16 @@
 namespace mv {
 MV_DEV uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
 
-// stamps: [role][0 start, 1 role work done, 2 after the barrier, 3 end] (lane 0 of each role, workgroup 0)
+// stamps: [role][0 start, 1 role work done, 2 after the first barrier, 3 end] (lane 0 of each
+// role, workgroup 0); table roles 5..8 also stamp the end of SHA-512 in slot 3
 __global__ void __launch_bounds__(C16_THREADS) k_comb16_phases(const uint8_t* msg, const uint8_t* __restrict__ sig,
                                                                const uint8_t* __restrict__ pk,
                                                                const uint32_t* __restrict__ key_idx, uint32_t n,
                                                                const uint4* __restrict__ combB,
                                                                const uint4* __restrict__ combA,
                                                                uint8_t* __restrict__ status, uint64_t* ts) {
-  __shared__ uint32_t part[4][C16_SIGS][36];
+  __shared__ uint32_t part[C16_TROLES][C16_SIGS][36];
+  constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);
   const uint64_t t0 = now();
   const uint32_t t = threadIdx.x;
   const bool row_role = t < 16 * C16_SIGS;
@@ -29,6 +31,7 @@ __global__ void __launch_bounds__(C16_THREADS) k_comb16_phases(const uint8_t* ms
   const uint32_t gid = blockIdx.x * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
+  const bool stamp = blockIdx.x == 0 && (t & 63) == 0;
   fe v;
   bool okR = false, s_ok = false;
   if (role == 0) {
@@ -40,12 +43,13 @@ __global__ void __launch_bounds__(C16_THREADS) k_comb16_phases(const uint8_t* ms
     decompress1_r16(R, okR, rw);
     fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
   } else {
-    if (role <= 2) {
+    const uint32_t tr = role - 1;
+    if (tr < C16_TROLES / 2) {
       uint32_t sw[8], sd[8];
       load8(sw, sig + 64 * (size_t)idx + 32);
       sc_recode256(sd, sw);
-      const int r0 = (role - 1) * (CT_ROWS / 2);
-      q_ct_sum(v, combB, sd, r0, r0 + CT_ROWS / 2);
+      const int r0 = (int)tr * ROWS;
+      q_ct_sum(v, combB, sd, r0, r0 + ROWS);
     } else {
       uint32_t kin[24], h[16], k[8], kd[8];
       load8(kin, sig + 64 * (size_t)idx);
@@ -54,26 +58,31 @@ __global__ void __launch_bounds__(C16_THREADS) k_comb16_phases(const uint8_t* ms
       sha512_short(h, kin, 96);
       sc_reduce512(k, h);
       sc_recode256(kd, k);
-      if (blockIdx.x == 0 && (t & 63) == 0) ts[role * 4 + 3] = now();  // role 3/4: after SHA (slot 3)
-      const int r0 = (role - 3) * (CT_ROWS / 2);
-      q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + CT_ROWS / 2);
+      if (stamp) ts[role * 4 + 3] = now();
+      const int r0 = (int)(tr - C16_TROLES / 2) * ROWS;
+      q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + ROWS);
     }
 #pragma unroll
-    for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
+    for (int i = 0; i < 9; i++) part[tr][sq][9 * c + i] = v.v[i];
   }
   const uint64_t t1 = now();
   __syncthreads();
   const uint64_t t2 = now();
+  fe w;
+  for (uint32_t h = C16_TROLES / 2; h >= 1; h >>= 1) {
+    if (role >= 1 && role - 1 < h) {
+#pragma unroll
+      for (int i = 0; i < 9; i++) w.v[i] = part[role - 1 + h][sq][9 * c + i];
+      qp_add(v, w);
+#pragma unroll
+      for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
+    }
+    __syncthreads();
+  }
   if (role == 0) {
-    fe w, S;
+    fe S;
 #pragma unroll
     for (int i = 0; i < 9; i++) S.v[i] = part[0][sq][9 * c + i];
-#pragma unroll
-    for (int j = 1; j < 4; j++) {
-#pragma unroll
-      for (int i = 0; i < 9; i++) w.v[i] = part[j][sq][9 * c + i];
-      qp_add(S, w);
-    }
     fe nS;
     fe_neg(nS, S);
     fe_cmov(S, nS, c == 0 || c == 3);
@@ -89,11 +98,11 @@ __global__ void __launch_bounds__(C16_THREADS) k_comb16_phases(const uint8_t* ms
     if ((t & 15u) == 0 && gid < n) status[gid] = (uint8_t)(bits + (s_ok ? 4 : 0) + (okR ? 8 : 0));
   }
   const uint64_t t3 = now();
-  if (blockIdx.x == 0 && (t & 63) == 0) {
+  if (stamp) {
     ts[role * 4 + 0] = t0;
     ts[role * 4 + 1] = t1;
     ts[role * 4 + 2] = t2;
-    if (role == 0 || role <= 2) ts[role * 4 + 3] = t3;
+    if (role <= C16_TROLES / 2) ts[role * 4 + 3] = t3;
   }
 }
 }  // namespace mv
@@ -118,7 +127,7 @@ int main() {
   CHECK(hipMalloc(&d_ok, nkeys));
   CHECK(hipMalloc(&d_st, n));
   CHECK(hipMalloc(&d_kidx, 4 * n));
-  CHECK(hipMalloc(&d_ts, 8 * 5 * 4));
+  CHECK(hipMalloc(&d_ts, 8 * 9 * 4));
   CHECK(hipMalloc(&d_B, mvk::comb_table_bytes(1)));
   CHECK(hipMalloc(&d_A, mvk::comb_table_bytes(nkeys)));
   CHECK(hipMemcpy(d_enc, enc.data(), enc.size(), hipMemcpyHostToDevice));
@@ -128,20 +137,21 @@ int main() {
   CHECK(mvk::launch_comb_init(nullptr, 1, 0, d_B, nullptr, 0));
   CHECK(mvk::launch_comb_init(d_enc, nkeys, 1, d_A, d_ok, 0));
   CHECK(hipDeviceSynchronize());
-  std::vector<std::vector<double>> ph(5 * 4);
+  std::vector<std::vector<double>> ph(9 * 4);
   for (int rep = 0; rep < 30; rep++) {
-    CHECK(hipMemset(d_ts, 0, 8 * 20));
+    CHECK(hipMemset(d_ts, 0, 8 * 36));
     hipLaunchKernelGGL(mv::k_comb16_phases, dim3(n / mv::C16_SIGS), dim3(mv::C16_THREADS), 0, 0, d_msg, d_sig, d_enc,
                        d_kidx, n, (const uint4*)d_B, (const uint4*)d_A, d_st, d_ts);
     CHECK(hipDeviceSynchronize());
-    uint64_t ts[20];
+    uint64_t ts[36];
     CHECK(hipMemcpy(ts, d_ts, sizeof(ts), hipMemcpyDeviceToHost));
     uint64_t base = ts[0];
-    for (int r = 0; r < 5; r++) base = std::min(base, ts[4 * r]);
-    for (int i = 0; i < 20; i++) ph[i].push_back(ts[i] ? (ts[i] - base) / 100.0 : -1.0);  // 100 MHz -> us
+    for (int r = 0; r < 9; r++) base = std::min(base, ts[4 * r]);
+    for (int i = 0; i < 36; i++) ph[i].push_back(ts[i] ? (ts[i] - base) / 100.0 : -1.0);  // 100 MHz -> us
   }
-  const char* names[5] = {"R decode (rows)", "B rows 0-15", "B rows 16-31", "SHA + A rows 0-15", "SHA + A rows 16-31"};
-  for (int r = 0; r < 5; r++) {
+  const char* names[9] = {"R decode (rows)", "B rows 0-7", "B rows 8-15", "B rows 16-23", "B rows 24-31",
+                          "SHA + A rows 0-7", "SHA + A rows 8-15", "SHA + A rows 16-23", "SHA + A rows 24-31"};
+  for (int r = 0; r < 9; r++) {
     double m[4];
     for (int k = 0; k < 4; k++) {
       auto v = ph[4 * r + k];
