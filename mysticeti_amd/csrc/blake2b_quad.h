@@ -113,7 +113,9 @@ MV_DEV uint64_t qrot(uint64_t x) {
 // dependency and DPP-hazard gaps, and the message-word addresses are computed once for
 // both. (h0, h1) = (h[q], h[4 + q]); (iv0, iv1) = (IV[q], IV[4 + q]); t = byte counter
 // (< 2^64), fin = final block.
-template <int NS, bool LIN = false>
+// HOIST (the latency path: one wave per SIMD): no per-round barrier, so the scheduler issues
+// the message reads ahead of the G chains and the LDS latency leaves the critical path
+template <int NS, bool LIN = false, bool HOIST = false>
 MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* const (&m)[NS], uint32_t q,
                      uint64_t iv0, uint64_t iv1, const uint64_t (&t)[NS], const bool (&fin)[NS]) {
   uint64_t va[NS], vb[NS], vc[NS], vd[NS];
@@ -129,7 +131,7 @@ MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* con
   for (int r = 0; r < 12; r++) {
     // keep each round's message reads in their round: hoisting all 48 ahead of the chain
     // (what the scheduler does unchecked) doubles the VGPRs and halves the waves per SIMD
-    asm volatile("" ::: "memory");
+    if (!HOIST) asm volatile("" ::: "memory");
     const uint32_t qq = q;
     const uint32_t i0 = sel_at<NS, LIN>(r, 0, qq), i1 = sel_at<NS, LIN>(r, 1, qq);
     const uint32_t i2 = sel_at<NS, LIN>(r, 2, qq), i3 = sel_at<NS, LIN>(r, 3, qq);
@@ -244,7 +246,7 @@ MV_DEV void load_quarter(uint64_t w[4], const uint8_t* p, uint64_t b, uint64_t l
 
 // 16 * NS strings per 64-lane workgroup: quad qd takes strings 16 k + qd, k < NS. DUAL:
 // out0 = B2(P) (msg), out1 = B2(P || sig) (digest); otherwise out0 = B2(string).
-template <bool DUAL, int NS>
+template <bool DUAL, int NS, bool HOIST = false>
 MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                       const uint64_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ out0,
                       uint8_t* __restrict__ out1) {
@@ -318,7 +320,7 @@ MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint6
       t[k] = 128ull * (s + 1);
       fin[k] = false;
     }
-    compress<NS>(h0, h1, mrow, q, iv0, iv1, t, fin);
+    compress<NS, false, HOIST>(h0, h1, mrow, q, iv0, iv1, t, fin);
 #pragma unroll
     for (int k = 0; k < NS; k++)
 #pragma unroll
@@ -339,7 +341,7 @@ MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint6
       s0[k] = h0[k];
       s1[k] = h1[k];
     }
-    compress<NS>(h0, h1, mrow, q, iv0, iv1, t, fin);
+    compress<NS, false, HOIST>(h0, h1, mrow, q, iv0, iv1, t, fin);
 #pragma unroll
     for (int k = 0; k < NS; k++) {
       if (DUAL && mfin[k] && s < pl[k].nsteps) reinterpret_cast<uint64_t*>(out0 + 32 * (size_t)idx[k])[q] = h0[k];

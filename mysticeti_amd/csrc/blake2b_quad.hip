@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "../../include/mysti_verify.h"
 #include "blake2b_quad.h"
 #include "kernels.h"
 
@@ -31,6 +32,13 @@ __global__ void MV_B2Q_BOUNDS k_b2_quad(const uint8_t* __restrict__ buf, const u
                                         const uint64_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ out0,
                                         uint8_t* __restrict__ out1) {
   quad_hash<DUAL, NS>(blockIdx.x, buf, off, len, n, out0, out1);
+}
+// the online path's form (a few waves on an idle chip): message reads hoisted out of their
+// rounds, so the LDS latency leaves the compression chain (more VGPRs, fewer waves: fine here)
+__global__ void __launch_bounds__(64) k_b2_quad_lat(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                                                    const uint64_t* __restrict__ len, uint32_t n,
+                                                    uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
+  quad_hash<true, 1, true>(blockIdx.x, buf, off, len, n, out0, out1);
 }
 
 
@@ -65,7 +73,9 @@ hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const ui
 hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                                   uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (b2q_ns(n) == 2)
+  if (n < MV_BATCH_MIN)  // the online path (comb verify): latency form
+    hipLaunchKernelGGL(mv::b2q::k_b2_quad_lat, dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, msg_out, dig_out);
+  else if (b2q_ns(n) == 2)
     hipLaunchKernelGGL((mv::b2q::k_b2_quad<true, 2>), dim3((n + 31) / 32), dim3(64), 0, s, buf, off, len, n, msg_out,
                        dig_out);
   else

@@ -204,17 +204,19 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* msg, const u
 // k_verify_comb16: the same predicate with every dependent chain cut short, for the online
 // path (64-block calls), where k_verify_comb's latency is its longest single-lane chain: the
 // R decode (~265 field operations) and the 32 B-table additions, ~80 us each on one lane.
-// 16 signatures per 768-thread workgroup:
-//   role 0 (waves 0..3, one 16-lane DPP row per signature): ZIP-215 decode of R, its (p-5)/8
+// C16_SIGS signatures per workgroup:
+//   role 0 (one 16-lane DPP row per signature): ZIP-215 decode of R, its (p-5)/8
 //           power on fe_r16.h (~2x shorter per product than one lane), then the combination
-//   roles 1..4 (one wave each, one quad per signature): the C_B entries of s's digits in four
+//   roles 1..4 (one quad per signature each): the C_B entries of s's digits in four
 //           blocks of 8 rows, point additions on quad25519.h's layout (lane c holds
 //           coordinate c; it loads only the entry coordinate its product needs)
 //   roles 5..8: SHA-512 k, then the C_A entries of k's digits in four blocks of 8 rows
-// A 3-level tree over the table roles' sums follows (LDS), then role 0's lanes 0..3 of each
-// row subtract the sum from R as a quad, clear the cofactor and test for the identity. Same
-// predicate, same status as k_verify_comb.
-MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8]) {
+// The table roles' sums are reduced (LDS, then lane shuffles) while role 0 finishes its decode
+// (a barrier inside the power chain), then role 0's lanes 0..3 of each row subtract the sum
+// from R as a quad, clear the cofactor and test for the identity. Same predicate, same status
+// as k_verify_comb.
+template <class Mid = NoMid>
+MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8], Mid mid = Mid()) {
   fe d, one, ya, ua, va, t, v3a, ea7, pa, xa, n;
   fe_const(d, K_D);
   fe_set(one, 1);
@@ -228,7 +230,7 @@ MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8]) {
   {
     fer x, r;
     fer_from_fe(x, ea7);
-    fer_pow_p58(r, x);
+    fer_pow_p58(r, x, mid);
     fe_from_fer(pa, r);
   }
   fe_mul(pa, pa, v3a); fe_mul(pa, pa, ua);
@@ -302,7 +304,10 @@ MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int 
   }
 }
 
-constexpr uint32_t C16_SIGS = 16;   // signatures per k_verify_comb16 workgroup
+// 4 signatures per workgroup: one wave decodes (4 rows), one wave holds the four B roles and
+// one the four A roles (16 lanes each), so every wave has a SIMD of its own; with 16
+// signatures per workgroup (12 waves, 3 per SIMD) SHA-512 k took 27 us instead of ~10
+constexpr uint32_t C16_SIGS = 4;    // signatures per k_verify_comb16 workgroup
 constexpr uint32_t C16_TROLES = 8;  // table-sum roles: four over the B rows, four over the A rows
 constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS;
 __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* __restrict__ sig,
@@ -317,24 +322,31 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
   constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);       // table rows per role
   const uint32_t t = threadIdx.x;
   const bool row_role = t < 16 * C16_SIGS;
-  const uint32_t role = row_role ? 0u : 1u + ((t - 16 * C16_SIGS) >> 6);
+  const uint32_t role = row_role ? 0u : 1u + (t - 16 * C16_SIGS) / (4 * C16_SIGS);
   const uint32_t sq = row_role ? t >> 4 : (t >> 2) & (C16_SIGS - 1), c = t & 3u;
   const uint32_t gid = blockIdx.x * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
   fe v;  // coordinate c of this role's point
   bool okR = false, s_ok = false;
-  if (role == 0) {  // every lane of the row holds the signature's R and s
+  // Barrier 1 (inside role 0's decode, after 208 of its 263 products): every table role has
+  // written its sum. The B wave then folds in the A wave's sums and reduces its four roles by
+  // lane shuffles while role 0 finishes the decode. Barrier 2: the total is in LDS.
+  // the branches around the barriers are wave-uniform (readfirstlane: scalar branches), so
+  // every wave meets exactly two barriers
+  static_assert(4 * C16_SIGS * (C16_TROLES / 2) == 64, "the B roles fill one wave, the A roles another");
+  if (__builtin_amdgcn_readfirstlane(role) == 0) {  // every lane of the row holds the signature's R and s
     uint32_t rw[8], sw[8];
     load8(rw, sig + 64 * (size_t)idx);
     load8(sw, sig + 64 * (size_t)idx + 32);
     s_ok = sc_is_canonical(sw);
     p3 R;
-    decompress1_r16(R, okR, rw);
+    decompress1_r16(R, okR, rw, [] { __syncthreads(); });  // barrier 1
     fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
   } else {
     const uint32_t tr = role - 1;  // 0 .. C16_TROLES / 2 - 1: B rows; then A rows
-    if (tr < C16_TROLES / 2) {
+    const bool b_wave = __builtin_amdgcn_readfirstlane(tr) < C16_TROLES / 2;
+    if (b_wave) {
       uint32_t sw[8], sd[8];
       load8(sw, sig + 64 * (size_t)idx + 32);
       sc_recode256(sd, sw);
@@ -354,20 +366,24 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
     }
 #pragma unroll
     for (int i = 0; i < 9; i++) part[tr][sq][9 * c + i] = v.v[i];
-  }
-  __syncthreads();
-  // tree over the table roles' sums (role r < h adds role r + h's), then role 0
-  fe w;
-  for (uint32_t h = C16_TROLES / 2; h >= 1; h >>= 1) {
-    if (role >= 1 && role - 1 < h) {
+    __syncthreads();  // barrier 1
+    if (b_wave) {  // the B wave: + the A role of the same rank, then the lane tree
+      fe w;
 #pragma unroll
-      for (int i = 0; i < 9; i++) w.v[i] = part[role - 1 + h][sq][9 * c + i];
+      for (int i = 0; i < 9; i++) w.v[i] = part[tr + C16_TROLES / 2][sq][9 * c + i];
       qp_add(v, w);
+      for (uint32_t h = C16_TROLES / 4; h >= 1; h >>= 1) {  // role tr + h is 4 C16_SIGS h lanes up
 #pragma unroll
-      for (int i = 0; i < 9; i++) part[role - 1][sq][9 * c + i] = v.v[i];
+        for (int i = 0; i < 9; i++) w.v[i] = (uint32_t)__shfl_down((int)v.v[i], 4 * C16_SIGS * h, 64);
+        if (tr < h) qp_add(v, w);
+      }
+      if (tr == 0) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) part[0][sq][9 * c + i] = v.v[i];
+      }
     }
-    __syncthreads();
   }
+  __syncthreads();  // barrier 2
   if (role == 0) {  // lanes 0..3 of each row form the quad (the other lanes repeat it)
     fe S;
 #pragma unroll
@@ -413,7 +429,7 @@ __global__ void __launch_bounds__(64) k_hash_comb_pre(const uint8_t* __restrict_
                                                       uint4* __restrict__ sbuf, uint8_t* __restrict__ qflags) {
   const uint32_t blk = blockIdx.x;
   if (blk < nh) {
-    b2q::quad_hash<true, 1>(blk, stage, poff, plen, n, md, bd);
+    b2q::quad_hash<true, 1, true>(blk, stage, poff, plen, n, md, bd);  // latency form: reads hoisted
     return;
   }
   const bool role_r = blk < nh + np;
@@ -449,14 +465,14 @@ __global__ void __launch_bounds__(64) k_hash_comb_pre(const uint8_t* __restrict_
   }
 }
 
-// k_comb_post: 16 signatures per 512-thread workgroup, eight roles of one quad per signature
+// k_comb_post: POST_SIGS signatures per workgroup, eight roles of one quad per signature
 // (quad25519.h's coordinate layout: every point operation is two products deep):
 //   phase 1  wave 0: k = SHA-512(R || A || M) mod l, one lane per signature, digits to LDS;
 //            role 7 meanwhile: R - [s]B from k_hash_comb_pre's two points
 //   phase 2  role w: the C_A entries of k's digits 4w .. 4w + 3 (four additions)
 //   phase 3  a 3-level tree over the roles' sums; role 0: R - [s]B - sum (the tables hold -A),
 //            [8], identity test
-constexpr uint32_t POST_SIGS = 16;
+constexpr uint32_t POST_SIGS = 4;  // two waves per workgroup: each on a SIMD of its own
 constexpr int POST_ROLES = 8;
 __global__ void __launch_bounds__(4 * POST_SIGS * POST_ROLES) k_comb_post(const uint8_t* msg,  // not restrict: bv writes it
                                                                          const uint8_t* __restrict__ sig,
@@ -475,7 +491,7 @@ __global__ void __launch_bounds__(4 * POST_SIGS * POST_ROLES) k_comb_post(const 
   const uint32_t gid = blockIdx.x * POST_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
-  if (t < POST_SIGS) {  // k once per signature (wave 0, lanes 0..15)
+  if (t < POST_SIGS) {  // k once per signature (wave 0, lanes 0 .. POST_SIGS - 1)
     const uint32_t g2 = blockIdx.x * POST_SIGS + t, i2 = g2 < n ? g2 : n - 1;
     uint32_t kin[24], h[16], k[8], kd[8];
     load8(kin, sig + 64 * (size_t)i2);

@@ -139,8 +139,14 @@ MV_DEV void fe_from_fer(fe& r, const fer& x) {
   r.v[8] = bcast<8>(x.v);
 }
 
-// x^((p-5)/8) on one row: fe_pow22501's addition chain (fe_q4.h's feq_pow_p58)
-MV_DEV void fer_pow_p58(fer& r, const fer& x) {
+// x^((p-5)/8) on one row: fe_pow22501's addition chain (fe_q4.h's feq_pow_p58). mid() runs
+// after x^(2^200 - 1) is formed (208 of 263 products): a caller's workgroup barrier there
+// lets other waves sync while the chain's last 55 products are still to come
+struct NoMid {
+  MV_DEV void operator()() const {}
+};
+template <class Mid = NoMid>
+MV_DEV void fer_pow_p58(fer& r, const fer& x, Mid mid = Mid()) {
   const r16::Consts K = r16::consts();
   fer t0, t1, t2, t3, t5, t7, t13, t15, a;
   fer_sq(t0, x, K);          // 2
@@ -161,6 +167,7 @@ MV_DEV void fer_pow_p58(fer& r, const fer& x) {
   fer_mul(t15, a, t13, K);   // 2^100-1
   fer_sqn(a, t15, 100, K);
   fer_mul(a, a, t15, K);     // 2^200-1
+  mid();
   fer_sqn(a, a, 50, K);
   fer_mul(a, a, t13, K);     // 2^250-1
   fer_sqn(a, a, 2, K);
