@@ -802,7 +802,17 @@ mv_status finish_block_chunk(mv_ctx* ctx, Device& dev, int s) {
   if (!ps.inflight) return MV_OK;
   ps.inflight = false;
   HIPCHK(ctx, hipSetDevice(dev.id));
-  const hipError_t e = hipEventSynchronize(ps.done);
+  // MV_PASS_SPIN=1 (A/B): the pass owner polls its event instead of blocking in the runtime
+  static const bool spin = [] {
+    const char* e = getenv("MV_PASS_SPIN");
+    return e && e[0] == '1';
+  }();
+  hipError_t e;
+  if (spin) {
+    while ((e = hipEventQuery(ps.done)) == hipErrorNotReady) std::this_thread::yield();
+  } else {
+    e = hipEventSynchronize(ps.done);
+  }
   if (e != hipSuccess) {
     (void)hipStreamSynchronize(ps.stream);
     return set_err(ctx, MV_E_HIP, std::string("block pass: ") + hipGetErrorString(e));
