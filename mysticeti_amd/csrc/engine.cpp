@@ -133,7 +133,7 @@ struct Device {
   hipStream_t qstream[kPassSets] = {};  // sets 2 and up (0: `stream`, 1: pstream[1])
   struct PassSet {
     HostBuf h_in, h_out;
-    DevBuf bytes, out2;
+    DevBuf bytes, out2, scr;  // scr: the block pipeline's scratch for this set's passes
     hipStream_t stream = nullptr;  // set 0: `stream`, set 1: pstream[1], set k >= 2: qstream[k]
     hipEvent_t done = nullptr;
     // the chunk in flight: items [lo, lo + m) of `it`, outputs in h_out when finished
@@ -404,23 +404,29 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
 // batches of long blocks, k_block_ingest -> k_hash_comb_pre) -> signatures (batch path for
 // >= MV_BATCH_MIN blocks, else committee verify) -> k_block_verdict. d_md / d_bd may be null
 // (scratch then).
+// own: scratch owned by the caller (a submission-queue pass set, whose reuse is ordered by its
+// own completion event): no ring slot, no slot events (two runtime calls less per pass).
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
                          const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
-                         hipStream_t s) {
+                         hipStream_t s, DevBuf* own = nullptr) {
   if (n == 0) return MV_OK;
   const mvh::Committee& com = ctx->committee;
-  const int slot = dev.blk_next;
-  dev.blk_next = (slot + 1) % Device::kBlkSlots;
-  if (!dev.blk_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.blk_done[slot], hipEventDisableTiming));
-  if (dev.blk_used[slot]) {
-    // skip the cross-stream wait when the slot's previous pass has finished (the common case
-    // on the online path, where a wait costs a queue drain)
-    const hipError_t q = hipEventQuery(dev.blk_done[slot]);
-    if (q != hipSuccess) {
-      (void)hipGetLastError();  // hipErrorNotReady is not an error here
-      HIPCHK(ctx, hipStreamWaitEvent(s, dev.blk_done[slot], 0));
+  int slot = -1;
+  if (!own) {
+    slot = dev.blk_next;
+    dev.blk_next = (slot + 1) % Device::kBlkSlots;
+    if (!dev.blk_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.blk_done[slot], hipEventDisableTiming));
+    if (dev.blk_used[slot]) {
+      // skip the cross-stream wait when the slot's previous pass has finished (the common case
+      // on the online path, where a wait costs a queue drain)
+      const hipError_t q = hipEventQuery(dev.blk_done[slot]);
+      if (q != hipSuccess) {
+        (void)hipGetLastError();  // hipErrorNotReady is not an error here
+        HIPCHK(ctx, hipStreamWaitEvent(s, dev.blk_done[slot], 0));
+      }
     }
   }
+  DevBuf& scr = own ? *own : dev.blk[slot];
   // small batches of long blocks: the comb verify's signature-only half beside the hash
   // bytes per block from which the split pays (MV_COMB_SPLIT_BYTES: tests and experiments; 0 = never)
   const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
@@ -460,8 +466,8 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   o += al(32 * nn);
   const size_t o_q = o;
   if (split) o += 2 * al(144 * nn) + al(nn);
-  HIPCHK(ctx, dev.blk[slot].ensure(o));
-  char* b = dev.blk[slot].as<char>();
+  HIPCHK(ctx, scr.ensure(o));
+  char* b = scr.as<char>();
   uint8_t* stage = (uint8_t*)(b + o_stage);
   uint64_t* poff = (uint64_t*)(b + o_poff);
   uint64_t* plen = (uint64_t*)(b + o_plen);
@@ -519,8 +525,10 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   if (!fused) HIPCHK(ctx, mvk::launch_block_verdict(facts, claimed, md, bd, sst, n, d_status, s));
   HIPCHK(ctx, mark(4));
   keep_events(ctx, dev.id, kBlockStage0, evs);
-  HIPCHK(ctx, hipEventRecord(dev.blk_done[slot], s));
-  dev.blk_used[slot] = true;
+  if (!own) {
+    HIPCHK(ctx, hipEventRecord(dev.blk_done[slot], s));
+    dev.blk_used[slot] = true;
+  }
   return MV_OK;
 }
 
@@ -780,7 +788,7 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   const double t2 = trace ? now() : 0;
   uint8_t* dout = hout_dev ? hout_dev : ps.out2.as<uint8_t>();
   rc = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off), (const uint64_t*)(dbuf + o_len), m,
-                      dout + 64 * (size_t)m, dout, dout + 32 * (size_t)m, ps.stream);
+                      dout + 64 * (size_t)m, dout, dout + 32 * (size_t)m, ps.stream, &ps.scr);
   if (rc != MV_OK) {
     (void)hipStreamSynchronize(ps.stream);  // what was queued reads the staging
     return rc;
@@ -1307,6 +1315,7 @@ void mv_destroy(mv_ctx* ctx) {
       ps.h_out.release();
       ps.bytes.release();
       ps.out2.release();
+      ps.scr.release();
       if (ps.done) (void)hipEventDestroy(ps.done);
     }
     for (hipStream_t st : dev.qstream)
