@@ -246,16 +246,29 @@ MV_DEV void load_quarter(uint64_t w[4], const uint8_t* p, uint64_t b, uint64_t l
 
 // 16 * NS strings per 64-lane workgroup: quad qd takes strings 16 k + qd, k < NS. DUAL:
 // out0 = B2(P) (msg), out1 = B2(P || sig) (digest); otherwise out0 = B2(string).
-template <bool DUAL, int NS, bool HOIST = false>
-MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
-                      const uint64_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ out0,
-                      uint8_t* __restrict__ out1) {
+// WAVE: one wave of a larger workgroup runs this alone (k_verify_comb16's online hash): its
+// steps are ordered by wave-scope fences instead of workgroup barriers. Strings
+// [first, first + count) of the n, count <= 16 NS (quad qd takes string first + 16 k + qd).
+template <bool WAVE>
+MV_DEV void qh_sync() {
+  if (WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+template <bool DUAL, int NS, bool HOIST = false, bool WAVE = false>
+MV_DEV void quad_hash_range(uint32_t first, uint32_t count, const uint8_t* __restrict__ buf,
+                            const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint32_t n,
+                            uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
   // [buffer][word rank][string][word class] (WG/WH above)
   __shared__ uint64_t mbuf[2][4][16 * NS][4];
+  const uint32_t lane = threadIdx.x & 63u, q = lane & 3, qd = lane >> 2;
   uint32_t wo[4];  // offsets of this lane's quarter (words 4q .. 4q+3) from the string's base
 #pragma unroll
-  for (int j = 0; j < 4; j++) wo[j] = (uint32_t)WH[4 * (threadIdx.x & 3) + j] * 64u * NS + WG[4 * (threadIdx.x & 3) + j];
-  const uint32_t lane = threadIdx.x, q = lane & 3, qd = lane >> 2;
+  for (int j = 0; j < 4; j++) wo[j] = (uint32_t)WH[4 * q + j] * 64u * NS + WG[4 * q + j];
   uint32_t idx[NS];
   bool live[NS];
   const uint8_t* p[NS];
@@ -263,8 +276,8 @@ MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint6
   uint32_t nsteps_max = 0, nfull_min = 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < NS; k++) {
-    idx[k] = blk * 16 * NS + 16 * k + qd;
-    live[k] = idx[k] < n;
+    idx[k] = first + 16 * k + qd;
+    live[k] = 16 * k + qd < count && idx[k] < n;
     p[k] = buf + (live[k] ? off[idx[k]] : 0);
     pl[k].init(live[k] ? len[idx[k]] : 0, live[k]);
     nsteps_max = max(nsteps_max, pl[k].nsteps);
@@ -303,7 +316,7 @@ MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint6
     for (int j = 0; j < 4; j++) (&mbuf[0][0][16 * k + qd][0])[wo[j]] = w[k][j];
   }
   for (uint32_t s = 0; s < nfull; s++) {
-    __syncthreads();
+    qh_sync<WAVE>();
 #pragma unroll
     for (int k = 0; k < NS; k++) {
       if (s + 1 < nfull) {  // the next whole block, in flight during this compression
@@ -327,7 +340,7 @@ MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint6
       for (int j = 0; j < 4; j++) (&mbuf[(s + 1) & 1][0][16 * k + qd][0])[wo[j]] = w[k][j];
   }
   for (uint32_t s = nfull; s < nmax; s++) {
-    __syncthreads();
+    qh_sync<WAVE>();
     bool mfin[NS];
     uint64_t s0[NS], s1[NS];
 #pragma unroll
@@ -356,6 +369,13 @@ MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint6
 #pragma unroll
   for (int k = 0; k < NS; k++)
     if (live[k]) reinterpret_cast<uint64_t*>((DUAL ? out1 : out0) + 32 * (size_t)idx[k])[q] = h0[k];
+}
+// 16 NS strings per 64-lane workgroup (block blk)
+template <bool DUAL, int NS, bool HOIST = false>
+MV_DEV void quad_hash(uint32_t blk, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                      const uint64_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ out0,
+                      uint8_t* __restrict__ out1) {
+  quad_hash_range<DUAL, NS, HOIST, false>(blk * 16 * NS, 16 * NS, buf, off, len, n, out0, out1);
 }
 
 

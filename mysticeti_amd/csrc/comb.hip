@@ -317,7 +317,8 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
                                                                const uint4* __restrict__ combA,
                                                                const uint8_t* __restrict__ key_ok,
                                                                uint8_t* __restrict__ status,
-                                                               const mvk::BlockVerdictOut bv) {
+                                                               const mvk::BlockVerdictOut bv,
+                                                               const mvk::BlockHashIn hin) {
   __shared__ uint32_t part[C16_TROLES][C16_SIGS][36];  // table roles' sums, coordinate c at words 9c..
   constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);       // table rows per role
   const uint32_t t = threadIdx.x;
@@ -353,6 +354,13 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
       const int r0 = (int)tr * ROWS;
       q_ct_sum(v, combB, sd, r0, r0 + ROWS);
     } else {
+      if (hin.stage) {
+        // the block path's two digests of this workgroup's blocks first (one quad per block,
+        // quads 0 .. C16_SIGS - 1 of the A wave): M = msg digest feeds the challenge below
+        b2q::quad_hash_range<true, 1, true, true>(blockIdx.x * C16_SIGS, C16_SIGS, hin.stage, hin.pre_off,
+                                                   hin.pre_len, n, hin.msg_digest, hin.digest);
+        __threadfence();  // the digests are read back below (other lanes) and by role 0's verdict
+      }
       // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's bytes)
       uint32_t kin[24], h[16], k[8], kd[8];
       load8(kin, sig + 64 * (size_t)idx);
@@ -581,21 +589,26 @@ hipError_t launch_comb_init(const uint8_t* enc, uint32_t nb, int negate, void* t
   return hipGetLastError();
 }
 
+bool comb_short_chain(uint32_t n) {
+  const char* qe = getenv("MV_COMB_QUAD");  // read per call: the tests switch it in-process
+  const int quad_env = qe && *qe ? atoi(qe) : -1;
+  return quad_env >= 0 ? quad_env != 0 : n <= 64u * 256u;
+}
+
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
-                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv) {
+                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv, const BlockHashIn* hin) {
+  if (hin && !comb_short_chain(n)) return hipErrorInvalidValue;  // the caller hashes first
   if (n == 0) return hipSuccess;
   const BlockVerdictOut none{};
   // short chains (k_verify_comb16: a row per R decode, quads for the table sums) up to 64
   // workgroups of 256 signatures' worth (the online path); MV_COMB_QUAD=0 / 1 forces
   // k_verify_comb / k_verify_comb16 (A/B, tests)
-  const char* qe = getenv("MV_COMB_QUAD");  // read per call: the tests switch it in-process
-  const int quad_env = qe && *qe ? atoi(qe) : -1;
-  const bool quad = quad_env >= 0 ? quad_env != 0 : n <= 64u * 256u;
-  if (quad)
+  const BlockHashIn nohash{};
+  if (comb_short_chain(n))
     hipLaunchKernelGGL(mv::k_verify_comb16, dim3((n + mv::C16_SIGS - 1) / mv::C16_SIGS), dim3(mv::C16_THREADS), 0, s,
                        msg, sig, pk, key_idx, n, (const uint4*)combB, (const uint4*)combA, key_ok, status,
-                       bv ? *bv : none);
+                       bv ? *bv : none, hin ? *hin : nohash);
   else
     hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);

@@ -390,10 +390,10 @@ mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const u
 // bv: the block verdict fused into the comb kernel (the block path); null otherwise.
 mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig,
                                    const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s,
-                                   const mvk::BlockVerdictOut* bv = nullptr) {
+                                   const mvk::BlockVerdictOut* bv = nullptr, const mvk::BlockHashIn* hin = nullptr) {
   if (!(ctx->flags & MV_FLAG_NO_COMB)) {
     HIPCHK(ctx, mvk::launch_verify_comb(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
-                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv));
+                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv, hin));
   } else {
     return enqueue_verify(ctx, dev, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, d_status, s);
   }
@@ -486,6 +486,12 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   uint8_t* rbuf = (uint8_t*)(b + o_q);
   uint8_t* sbuf = rbuf + al(144 * nn);
   uint8_t* qflags = sbuf + al(144 * nn);
+  // short blocks on the online path: the digests are computed inside the committee verify
+  // (k_verify_comb16's A wave hashes its blocks before the challenge), one launch less
+  const char* hce = getenv("MV_HASH_IN_COMB");  // A/B: 0 = a separate hash launch
+  const bool hash_in_comb = !fused_ih && !split && !batch && !(ctx->flags & MV_FLAG_NO_COMB) &&
+                            mvk::comb_short_chain(n) && !(hce && hce[0] == '0');
+  const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
   if (fused_ih && !split) {
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
@@ -496,7 +502,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, mark(1));
     if (split)  // the hash, and beside it on workgroups of their own the signature-only terms
       HIPCHK(ctx, mvk::launch_hash_comb_pre(stage, poff, plen, n, md, bd, sig, dev.combB.p, rbuf, sbuf, qflags, s));
-    else
+    else if (!hash_in_comb)
       HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
   }
   // a block whose digest does not match is rejected ahead of its signature (types.rs:327-332):
@@ -518,7 +524,8 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, mvk::launch_comb_post(md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, dev.combA.p,
                                       dev.keyok.as<uint8_t>(), rbuf, sbuf, qflags, sst, s, fused ? &bv : nullptr));
   } else {
-    st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s, fused ? &bv : nullptr);
+    st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s, fused ? &bv : nullptr,
+                                  hash_in_comb ? &hin : nullptr);
   }
   if (st != MV_OK) return st;
   HIPCHK(ctx, mark(3));

@@ -78,9 +78,21 @@ struct BlockVerdictOut {
   uint8_t* digest;
   uint8_t* status;
 };
+// the block hash folded into the online committee verify (k_verify_comb16): the staged
+// pre-images P || sig in, both digests out (msg_digest is then the kernel's msg input)
+struct BlockHashIn {
+  const uint8_t* stage;
+  const uint64_t* pre_off;
+  const uint64_t* pre_len;
+  uint8_t* msg_digest;
+  uint8_t* digest;
+};
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
-                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr);
+                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr,
+                              const BlockHashIn* hin = nullptr);
+// whether launch_verify_comb takes the short-chain kernel (the one that can fold the hash in)
+bool comb_short_chain(uint32_t n);
 // the comb verify split in two, for small batches of long blocks: k_hash_comb_pre is
 // launch_block_hash plus, on workgroups of their own, the signature-only terms (R decoded ->
 // rbuf, -[s]B -> sbuf, 144 B per signature each, flags: bit 0 s < l, bit 1 R decodes);
