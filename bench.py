@@ -165,6 +165,8 @@ def main():
                     help="skip the config-4 (100-validator blocks) rate in the default line")
     ap.add_argument("--config4-batch", type=int, default=1 << 21,
                     help="config-4 blocks per GPU per step (2^21: BASELINE config 4's 16M blocks over 8 GPUs)")
+    ap.add_argument("--host-fed-blocks", type=int, default=1 << 18,
+                    help="config 4's PCIe-inclusive leg: blocks fed from host memory (0 disables)")
     ap.add_argument("--no-config5", dest="config5", action="store_false",
                     help="skip the config-5 (online latency) key of the default line")
     ap.add_argument("--config5-batches", type=int, default=2000,
@@ -422,7 +424,7 @@ def main():
         cfg4 = bench_blocks.config4_measure(eng, torch, local_rank, world, dist, n=args.config4_batch,
                                             steps=max(3, min(args.steps, 100)), warmup=max(1, min(args.warmup, 3)),
                                             nstreams=nstreams,
-                                            cpu=args.cpu_sample > 0)
+                                            cpu=args.cpu_sample > 0, host_blocks=args.host_fed_blocks)
         ok = ok and cfg4["correct"]
 
     # f4: the WAL replay check over an HBM-resident WAL of config-4 blocks (bench_wal.wal_measure)

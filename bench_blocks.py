@@ -256,7 +256,7 @@ def config5(args, eng, rank) -> int:
 # ------------------------------------------------------------------ config 4 (throughput)
 def config4(args, eng, torch, local_rank, rank, world, dist) -> int:
     res = config4_measure(eng, torch, local_rank, world, dist, n=args.batch, steps=args.steps, warmup=args.warmup,
-                          nstreams=max(1, args.streams), cpu=args.cpu_sample > 0)
+                          nstreams=max(1, args.streams), cpu=args.cpu_sample > 0, host_blocks=args.host_fed_blocks)
     if rank == 0:
         out = {"metric": METRIC}
         out.update(res)
@@ -279,14 +279,24 @@ def config4_host_fed(eng, torch, dev, buf, off, ln, nb, span, n_host, calls=3) -
     hbuf[: reps * span].reshape(reps, span)[:, :base_bytes] = buf[:base_bytes]
     hoff = (np.arange(reps, dtype=np.uint64)[:, None] * np.uint64(span) + off.astype(np.uint64)[None, :]).reshape(-1)[:n_host]
     hlen = np.tile(ln.astype(np.uint64), reps)[:n_host]
-    st = None
-    best = None
-    eng.verify_blocks_packed(hbuf, hoff[:nb].copy(), hlen[:nb].copy())  # warm the staging
-    for _ in range(calls):
-        t0 = time.perf_counter()
-        st, _, _ = eng.verify_blocks_packed(hbuf, hoff, hlen)
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
+
+    def best_of(b):
+        eng.verify_blocks_packed(b, hoff[:nb].copy(), hlen[:nb].copy())  # warm the staging
+        st_, best_ = None, None
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            st_, _, _ = eng.verify_blocks_packed(b, hoff, hlen)
+            dt = time.perf_counter() - t0
+            best_ = dt if best_ is None else min(best_, dt)
+        return best_, st_
+
+    # page-locked caller memory (mv_host_alloc): the engine DMAs the bytes in place
+    pbuf = eng.host_empty(hbuf.shape)
+    pbuf[:] = hbuf
+    best, st = best_of(pbuf)
+    eng.host_free(pbuf)
+    del pbuf
+    best_page, st_page = best_of(hbuf)
     # pinned H2D bandwidth (1 GiB, torch's pinned allocator, the copy engine alone)
     h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
     d = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
@@ -303,10 +313,14 @@ def config4_host_fed(eng, torch, dev, buf, off, ln, nb, span, n_host, calls=3) -
     return {"value": round(rate, 1), "unit": "blocks/s", "blocks": n_host,
             "bincode_GB": round(float(hlen.sum()) / 1e9, 3), "seconds": round(best, 4),
             "h2d_GBps_pinned": round(h2d / 1e9, 1), "pcie_bound_blocks_per_s": round(h2d / L, 1),
-            "frac_of_pcie_bound": round(rate / (h2d / L), 4), "correct": bool((st == 0).all()),
-            "note": "mv_verify_blocks on one pageable host buffer (the engine packs into pinned staging in "
-                    "256-MiB chunks, chunk c+1 packed and copied while chunk c runs), best of "
-                    f"{calls} calls; the PCIe bound is the measured pinned H2D rate over {L:.0f} B per block"}
+            "frac_of_pcie_bound": round(rate / (h2d / L), 4),
+            "pageable": round(n_host / best_page, 1),
+            "correct": bool((st == 0).all()) and bool((st_page == 0).all()),
+            "note": "mv_verify_blocks over one host buffer of packed blocks, best of "
+                    f"{calls} calls; value: the buffer in page-locked memory (mv_host_alloc), which the engine "
+                    "DMAs in place in 256-MiB chunks (chunk c+1 copied while chunk c runs); pageable: a plain "
+                    "numpy buffer, which the engine first packs into its pinned staging with 8 threads; the "
+                    f"PCIe bound is the measured pinned H2D rate over {L:.0f} B per block"}
 
 
 def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstreams=2, cpu=True,

@@ -171,6 +171,12 @@ class Engine:
         raw = (ctypes.c_uint8 * max(nbytes, 1)).from_address(ptr.value)
         return np.frombuffer(raw, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
 
+    def host_free(self, arr: np.ndarray):
+        """Releases an array from host_empty (it must not be used afterwards)."""
+        ptr = getattr(self, "_pinned", {}).pop(arr.__array_interface__["data"][0], None)
+        if ptr is not None:
+            self.lib.mv_host_free(self.ctx, ptr)
+
     def __del__(self):
         try:
             self.close()

@@ -745,8 +745,13 @@ mv_status ensure_pass_set(mv_ctx* ctx, Device& dev, int s) {
   return MV_OK;
 }
 
+bool host_pinned(const void* p);
+
 // Packs items [lo, hi) into pass set s of dev and enqueues the device pipeline on its stream
-// (no wait). The set must be idle.
+// (no wait). The set must be idle. A large chunk whose blocks already lie in page-locked
+// caller memory (mv_host_alloc), in order with small gaps, skips the host pack: the DMA engine
+// reads the caller's bytes in place (only the offset / length arrays are staged), so the
+// host's memory bandwidth is not spent on a second copy.
 mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* it, uint64_t lo, uint64_t hi) {
   HIPCHK(ctx, hipSetDevice(dev.id));
   mv_status rc = ensure_pass_set(ctx, dev, s);
@@ -758,24 +763,50 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   const uint32_t m = (uint32_t)(hi - lo);
   uint64_t bytes = 0;
   for (uint64_t k = lo; k < hi; k++) bytes += packed_len(it[k]);
-  const size_t buf_bytes = (bytes + 16 + 15) & ~(size_t)15;
-  const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
-  HIPCHK(ctx, ps.h_in.ensure(total));
-  uint8_t* h = ps.h_in.as<uint8_t>();
-  pack_items(h, (uint64_t*)(h + o_off), (uint64_t*)(h + o_len), it, lo, hi, buf_bytes);
-  HIPCHK(ctx, ps.bytes.ensure(total));
-  HIPCHK(ctx, ps.out2.ensure(65 * (size_t)m + 256));
-  HIPCHK(ctx, ps.h_out.ensure(65 * (size_t)m));
-  const double t1 = trace ? now() : 0;
   // small chunks (the online path): the ingest kernel reads the pinned staging over PCIe
   // itself (zero-copy) instead of waiting for an H2D copy and the launch behind it
   static const uint64_t zc_max = [] {  // MV_BLK_ZEROCOPY=<bytes> (experiments; 0 = always copy)
     const char* e = getenv("MV_BLK_ZEROCOPY");
     return e ? (uint64_t)atoll(e) : (uint64_t)(1u << 20);
   }();
+  // in-place DMA of pinned caller bytes (see above)
+  const uint8_t* base = it[lo].p;
+  uint64_t span = 0;
+  bool direct = bytes > zc_max && host_pinned(base);
+  for (uint64_t k = lo; k < hi && direct; k++) {
+    if (it[k].p < base || (uint64_t)(it[k].p - base) < span) direct = false;  // in order, no overlap
+    span = (uint64_t)(it[k].p - base) + it[k].len;
+  }
+  // any alignment (the ingest kernels read from the aligned word at or below a block's start);
+  // gaps between blocks are copied too, so they must stay small
+  direct = direct && span && span <= 2 * bytes + 4096 && host_pinned(base + span - 1);
+  const size_t buf_bytes = direct ? (span + 16 + 15) & ~(size_t)15 : (bytes + 16 + 15) & ~(size_t)15;
+  const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
+  HIPCHK(ctx, ps.h_in.ensure(direct ? 16 * (size_t)m : total));
+  uint8_t* h = ps.h_in.as<uint8_t>();
+  if (direct) {
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(h);
+    uint64_t* hlen = hoff + m;
+    for (uint32_t k = 0; k < m; k++) {
+      hoff[k] = (uint64_t)(it[lo + k].p - base);
+      hlen[k] = it[lo + k].len;
+    }
+  } else {
+    pack_items(h, (uint64_t*)(h + o_off), (uint64_t*)(h + o_len), it, lo, hi, buf_bytes);
+  }
+  HIPCHK(ctx, ps.bytes.ensure(total));
+  HIPCHK(ctx, ps.out2.ensure(65 * (size_t)m + 256));
+  HIPCHK(ctx, ps.h_out.ensure(65 * (size_t)m));
+  const double t1 = trace ? now() : 0;
   const uint8_t* dbuf = nullptr;
   uint8_t* hout_dev = nullptr;  // zero-copy outputs too: the kernels write the pinned h_out
-  if (total <= zc_max) {
+  if (direct) {
+    uint8_t* d = ps.bytes.as<uint8_t>();
+    HIPCHK(ctx, hipMemcpyAsync(d, base, span, hipMemcpyHostToDevice, ps.stream));
+    HIPCHK(ctx, hipMemsetAsync(d + span, 0, buf_bytes - span, ps.stream));  // the 16 readable bytes past the end
+    HIPCHK(ctx, hipMemcpyAsync(d + o_off, h, 16 * (size_t)m, hipMemcpyHostToDevice, ps.stream));
+    dbuf = d;
+  } else if (total <= zc_max) {
     void* dp = nullptr;
     void* dq = nullptr;
     // outputs only under the comb path: the batch path re-reads the digests many times
@@ -806,7 +837,9 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   ps.lo = lo;
   ps.m = m;
   ps.inflight = true;
-  if (trace) fprintf(stderr, "[blk] set %d, %u blocks: pack %.1f, h2d %.1f, kernels %.1f us\n", s, m, t1 - t0, t2 - t1, now() - t2);
+  if (trace)
+    fprintf(stderr, "[blk] set %d, %u blocks%s: pack %.1f, h2d %.1f, kernels %.1f us\n", s, m, direct ? " (in place)" : "",
+            t1 - t0, t2 - t1, now() - t2);
   return MV_OK;
 }
 
