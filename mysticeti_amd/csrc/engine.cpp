@@ -227,6 +227,16 @@ void record_err(mv_ctx* ctx, const std::string& msg) {
     }                                                                                              \
   } while (0)
 
+// HIPCHK for functions that carry the status in `rc` (the first error is kept, no early return)
+#define HIPCHK_RC(ctx, rc, expr)                                                  \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess && (rc) == MV_OK) {                                      \
+      record_err((ctx), std::string(#expr) + ": " + hipGetErrorString(e_));       \
+      (rc) = MV_E_HIP;                                                            \
+    }                                                                             \
+  } while (0)
+
 mv_status set_err(mv_ctx* ctx, mv_status code, const std::string& msg) {
   record_err(ctx, msg);
   return code;
@@ -1095,6 +1105,64 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
   return MV_OK;
 }
 
+// mv_ed25519_verify's batch path over [lo, hi) of pinned caller arrays, zero-copy: k_bv_prep
+// reads msg / sig / pk straight from the page-locked host memory over PCIe (each input byte
+// once, the reads spread over the kernel by its waves) and the other kernels work on device
+// scratch, so there is no copy phase and no chunk gating; two batches on two compute streams
+// (batch 2's prep runs beside batch 1's sort, buckets and tail). false: the caller's pointers
+// have no device mapping (the caller falls back to verify_host_streamed).
+bool verify_host_zerocopy(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
+                          const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status, mv_status& rc) {
+  auto dptr = [](const void* h) -> const uint8_t* {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(h), 0) != hipSuccess || !d) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return static_cast<const uint8_t*>(d);
+  };
+  const uint8_t* dm = dptr(msg + 32 * lo);
+  const uint8_t* ds = dptr(sig + 64 * lo);
+  const uint8_t* dk = pk ? dptr(pk + 32 * lo) : dptr(key_idx + lo);
+  if (!dm || !ds || !dk) return false;
+  rc = MV_OK;
+  const uint64_t m = hi - lo;
+  static const double first_frac = [] {  // the first batch's share (MV_ZC_FIRST, A/B)
+    const char* e = getenv("MV_ZC_FIRST");
+    const double v = e ? atof(e) : 0.5;
+    return v > 0.0 && v < 1.0 ? v : 0.5;
+  }();
+  uint64_t b0 = m <= MV_BATCH_MIN * 2 ? m : (((uint64_t)(m * first_frac) + 1023) & ~1023ull);
+  if (b0 > ctx->max_batch) b0 = ctx->max_batch;
+  if (m - b0 > ctx->max_batch) b0 = m - ctx->max_batch;  // two batches at most per max_batch pair
+  for (int b = 0; b < 2; b++) {
+    if (!dev.pstream[b]) HIPCHK_RC(ctx, rc, hipStreamCreateWithFlags(&dev.pstream[b], hipStreamNonBlocking));
+    HIPCHK_RC(ctx, rc, dev.pin_st[b].ensure(std::max<uint64_t>(b0, m - b0) + 256));
+  }
+  HIPCHK_RC(ctx, rc, dev.h_out.ensure(m));
+  uint8_t* hst = dev.h_out.as<uint8_t>();
+  uint64_t i = 0;
+  for (int t = 0; i < m && rc == MV_OK; t++) {
+    const uint64_t k = t == 0 ? b0 : std::min<uint64_t>(m - i, ctx->max_batch);
+    hipStream_t cs = dev.pstream[t & 1];
+    if (t >= 2) HIPCHK_RC(ctx, rc, hipStreamSynchronize(cs));  // pin_st[t & 1] reuse (more than two batches)
+    rc = enqueue_batch(ctx, dev, dm + 32 * i, ds + 64 * i, pk ? dk + 32 * i : dev.committee_pk.as<uint8_t>(),
+                       pk ? nullptr : reinterpret_cast<const uint32_t*>(dk) + i, (uint32_t)k,
+                       dev.pin_st[t & 1].as<uint8_t>(), cs, nullptr);
+    if (rc == MV_OK)
+      HIPCHK_RC(ctx, rc, hipMemcpyAsync(hst + i, dev.pin_st[t & 1].p, k, hipMemcpyDeviceToHost, cs));
+    i += k;
+  }
+  // drain what was queued (it reads the caller's memory) before returning, error or not
+  const hipError_t e0 = hipStreamSynchronize(dev.pstream[0]), e1 = hipStreamSynchronize(dev.pstream[1]);
+  if (rc == MV_OK && (e0 != hipSuccess || e1 != hipSuccess))
+    rc = set_err(ctx, MV_E_HIP, std::string("zero-copy verify: ") + hipGetErrorString(e0 != hipSuccess ? e0 : e1));
+  if (rc != MV_OK) return true;
+  poll_flags(ctx, dev);
+  memcpy(status + lo, hst, m);
+  return true;
+}
+
 // mv_ed25519_verify's batch path over [lo, hi) of pinned caller arrays, in a few large
 // batches (two by default) on two compute streams. The DMA engines copy a batch's inputs
 // chunk by chunk on a copy stream, and k_bv_prep of chunk c starts as soon as chunk c has
@@ -1122,9 +1190,9 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   uint32_t bs = (uint32_t)bs64;
   // the first batch's share (MV_STREAM_FIRST, A/B): a larger first batch shortens the last
   // batch's sort, buckets and tail, which follow the last copy
-  static const double first_frac = [] {
+  static const double first_frac = [] {  // default 0.7: 199.5 vs 191.6 M/s at 0.5 (same box)
     const char* e = getenv("MV_STREAM_FIRST");
-    const double v = e ? atof(e) : 0.0;
+    const double v = e ? atof(e) : 0.7;
     return v > 0.0 && v < 1.0 ? v : 0.0;
   }();
   uint32_t b0 = bs;
@@ -1470,7 +1538,15 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
     // Pinned inputs (mv_host_alloc) stream: chunked DMA copies gate k_bv_prep chunk by chunk.
     static const int pipeline = getenv("MV_PIPELINE") ? atoi(getenv("MV_PIPELINE")) : 0;
     if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN) {
-      if (pinned) return verify_host_streamed(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
+      if (pinned) {
+        // MV_SIG_ZEROCOPY=1: k_bv_prep reads the pinned arrays over PCIe (no copy phase); measured
+        // slower than the chunked copies (175-185 vs 191-195 M/s, profiles/r03/e2e_zerocopy_ab.txt)
+        const char* zce = getenv("MV_SIG_ZEROCOPY");
+        const bool zc = zce && zce[0] == '1';
+        mv_status zrc = MV_OK;
+        if (zc && verify_host_zerocopy(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, zrc)) return zrc;
+        return verify_host_streamed(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
+      }
       if (pipeline) return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, pipeline == 2);
     }
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {
