@@ -41,6 +41,7 @@
 #include "comb.h"
 #include "blake2b_quad.h"
 #include "block_verdict.h"
+#include "ingest_dev.h"
 
 namespace mv {
 
@@ -309,19 +310,37 @@ MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int 
 // signatures per workgroup (12 waves, 3 per SIMD) SHA-512 k took 27 us instead of ~10
 constexpr uint32_t C16_SIGS = 4;    // signatures per k_verify_comb16 workgroup
 constexpr uint32_t C16_TROLES = 8;  // table-sum roles: four over the B rows, four over the A rows
-constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS;
-__global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* __restrict__ sig,
+// + one spare wave, which only ingests (with the other three) when the kernel parses its blocks
+constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS + 64;
+__global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* sig,  // not restrict: the ingest phase writes it
                                                                const uint8_t* __restrict__ pk,
-                                                               const uint32_t* __restrict__ key_idx, uint32_t n,
+                                                               const uint32_t* key_idx,  // likewise
+                                                               uint32_t n,
                                                                const uint4* __restrict__ combB,
                                                                const uint4* __restrict__ combA,
                                                                const uint8_t* __restrict__ key_ok,
                                                                uint8_t* __restrict__ status,
                                                                const mvk::BlockVerdictOut bv,
-                                                               const mvk::BlockHashIn hin) {
+                                                               const mvk::BlockHashIn hin,
+                                                               const mvk::BlockIngestIn ing) {
   __shared__ uint32_t part[C16_TROLES][C16_SIGS][36];  // table roles' sums, coordinate c at words 9c..
   constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);       // table rows per role
   const uint32_t t = threadIdx.x;
+  static_assert(C16_THREADS == 4 * 64 && C16_SIGS == 4, "one ingest wave per block of the workgroup");
+  if (ing.buf) {  // barrier 0: wave w parses block 4 b + w (ingest_dev.h) before anything reads it
+    __shared__ IngestLds igl[C16_SIGS];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), bi = blockIdx.x * C16_SIGS + w;
+    const CommitteeView cv{ing.stakes, ing.n_auth, ing.epoch, ing.quorum_thr};
+    const IngestOut io{ing.stage, ing.pre_off, ing.pre_len, ing.sig, ing.key_idx, ing.facts, ing.claimed};
+    if (bi < n) ingest_block<true>(bi, ing.buf, ing.off, ing.len, cv, io, igl[w]);
+    __threadfence();  // its outputs are read by the other waves after the barrier
+  }
+  __syncthreads();  // barrier 0
+  if (__builtin_amdgcn_readfirstlane(t) >= C16_THREADS - 64) {  // the spare wave: barriers 1 and 2
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
   const bool row_role = t < 16 * C16_SIGS;
   const uint32_t role = row_role ? 0u : 1u + (t - 16 * C16_SIGS) / (4 * C16_SIGS);
   const uint32_t sq = row_role ? t >> 4 : (t >> 2) & (C16_SIGS - 1), c = t & 3u;
@@ -597,18 +616,20 @@ bool comb_short_chain(uint32_t n) {
 
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
-                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv, const BlockHashIn* hin) {
-  if (hin && !comb_short_chain(n)) return hipErrorInvalidValue;  // the caller hashes first
+                              uint8_t* status, hipStream_t s, const BlockVerdictOut* bv, const BlockHashIn* hin,
+                              const BlockIngestIn* ing) {
+  if ((hin || ing) && !comb_short_chain(n)) return hipErrorInvalidValue;  // the caller parses / hashes first
   if (n == 0) return hipSuccess;
   const BlockVerdictOut none{};
   // short chains (k_verify_comb16: a row per R decode, quads for the table sums) up to 64
   // workgroups of 256 signatures' worth (the online path); MV_COMB_QUAD=0 / 1 forces
   // k_verify_comb / k_verify_comb16 (A/B, tests)
   const BlockHashIn nohash{};
+  const BlockIngestIn noingest{};
   if (comb_short_chain(n))
     hipLaunchKernelGGL(mv::k_verify_comb16, dim3((n + mv::C16_SIGS - 1) / mv::C16_SIGS), dim3(mv::C16_THREADS), 0, s,
                        msg, sig, pk, key_idx, n, (const uint4*)combB, (const uint4*)combA, key_ok, status,
-                       bv ? *bv : none, hin ? *hin : nohash);
+                       bv ? *bv : none, hin ? *hin : nohash, ing ? *ing : noingest);
   else
     hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);

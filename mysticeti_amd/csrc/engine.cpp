@@ -400,10 +400,11 @@ mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const u
 // bv: the block verdict fused into the comb kernel (the block path); null otherwise.
 mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig,
                                    const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s,
-                                   const mvk::BlockVerdictOut* bv = nullptr, const mvk::BlockHashIn* hin = nullptr) {
+                                   const mvk::BlockVerdictOut* bv = nullptr, const mvk::BlockHashIn* hin = nullptr,
+                                   const mvk::BlockIngestIn* ing = nullptr) {
   if (!(ctx->flags & MV_FLAG_NO_COMB)) {
     HIPCHK(ctx, mvk::launch_verify_comb(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
-                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv, hin));
+                                        dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv, hin, ing));
   } else {
     return enqueue_verify(ctx, dev, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, d_status, s);
   }
@@ -502,7 +503,15 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   const bool hash_in_comb = !fused_ih && !split && !batch && !(ctx->flags & MV_FLAG_NO_COMB) &&
                             mvk::comb_short_chain(n) && !(hce && hce[0] == '0');
   const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
-  if (fused_ih && !split) {
+  // ... and the parse too: k_verify_comb16 ingests its own blocks (one wave per block), so an
+  // online pass is one kernel launch (MV_INGEST_IN_COMB=0: a separate k_block_ingest, A/B)
+  const char* ice = getenv("MV_INGEST_IN_COMB");
+  const bool ingest_in_comb = hash_in_comb && !(ice && ice[0] == '0');
+  const mvk::BlockIngestIn ing{d_buf, d_off, d_len, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
+                               com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed};
+  if (ingest_in_comb) {
+    HIPCHK(ctx, mark(1));
+  } else if (fused_ih && !split) {
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
     HIPCHK(ctx, mark(1));
@@ -535,7 +544,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
                                       dev.keyok.as<uint8_t>(), rbuf, sbuf, qflags, sst, s, fused ? &bv : nullptr));
   } else {
     st = enqueue_committee_verify(ctx, dev, md, sig, kidx, n, sst, s, fused ? &bv : nullptr,
-                                  hash_in_comb ? &hin : nullptr);
+                                  hash_in_comb ? &hin : nullptr, ingest_in_comb ? &ing : nullptr);
   }
   if (st != MV_OK) return st;
   HIPCHK(ctx, mark(3));

@@ -87,10 +87,27 @@ struct BlockHashIn {
   uint8_t* msg_digest;
   uint8_t* digest;
 };
+// the block ingest folded into the online committee verify too (k_verify_comb16 parses its own
+// blocks first, one wave per block): bincode in, everything launch_block_parse writes out
+struct BlockIngestIn {
+  const uint8_t* buf;
+  const uint64_t* off;
+  const uint64_t* len;
+  const uint64_t* stakes;
+  uint32_t n_auth;
+  uint64_t epoch, quorum_thr;
+  uint8_t* stage;
+  uint64_t* pre_off;
+  uint64_t* pre_len;
+  uint8_t* sig;
+  uint32_t* key_idx;
+  uint32_t* facts;
+  uint8_t* claimed;
+};
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr,
-                              const BlockHashIn* hin = nullptr);
+                              const BlockHashIn* hin = nullptr, const BlockIngestIn* ing = nullptr);
 // whether launch_verify_comb takes the short-chain kernel (the one that can fold the hash in)
 bool comb_short_chain(uint32_t n);
 // the comb verify split in two, for small batches of long blocks: k_hash_comb_pre is

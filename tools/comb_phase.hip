@@ -26,12 +26,12 @@ __global__ void __launch_bounds__(C16_THREADS) k_comb16_phases(const uint8_t* ms
   const uint64_t t0 = now();
   const uint32_t t = threadIdx.x;
   const bool row_role = t < 16 * C16_SIGS;
-  const uint32_t role = row_role ? 0u : 1u + ((t - 16 * C16_SIGS) >> 6);
+  const uint32_t role = row_role ? 0u : 1u + (t - 16 * C16_SIGS) / (4 * C16_SIGS);
   const uint32_t sq = row_role ? t >> 4 : (t >> 2) & (C16_SIGS - 1), c = t & 3u;
   const uint32_t gid = blockIdx.x * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
-  const bool stamp = blockIdx.x == 0 && (t & 63) == 0;
+  const bool stamp = blockIdx.x == 0 && (row_role ? t == 0 : (t - 16 * C16_SIGS) % (4 * C16_SIGS) == 0);
   fe v;
   bool okR = false, s_ok = false;
   if (role == 0) {
