@@ -194,6 +194,11 @@ struct mv_ctx {
   bool q_packing = false;                // a combining caller is packing / enqueueing a pass
   bool q_set_busy[Device::kPassSets] = {};  // pass sets with a pass in flight
   int q_sets = 0;                          // pass sets in use (MV_PASS_SETS, default kPassSets)
+  // linger (MV_Q_LINGER_US): a combining caller that finds fewer requests queued than the last
+  // finished pass carried waits briefly for the rest of that pass's callers to come back
+  std::condition_variable q_linger_cv;
+  bool q_lingering = false;
+  size_t q_last_calls = 0;
   std::atomic<uint64_t> q_calls{0}, q_passes{0};
 };
 
@@ -204,7 +209,8 @@ struct mv_ctx::BlockReq {
   uint8_t *status, *md, *bd;
   mv_status rc = MV_OK;
   std::string err;
-  bool done = false;
+  bool taken = false;             // in a pass (q_mu)
+  std::atomic<bool> done{false};  // verdicts delivered (set under q_mu, may be polled without it)
 };
 
 namespace {
@@ -1638,8 +1644,20 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
   // (net_sync.rs:214-221, 314-386) thus share GPU round trips, up to q_sets passes in flight.
   mv_ctx::BlockReq req{buf, off, len, n, status, msg_digest, block_digest};
   ctx->q_calls++;
+  static const int linger_us = [] {
+    const char* e = getenv("MV_Q_LINGER_US");  // default 50 (tools/gpu_r03w.sh, gpu_r03x.sh A/B)
+    return e ? atoi(e) : 50;
+  }();
+  // MV_Q_SPIN_US: a caller whose request is in another caller's pass polls for its verdicts
+  // that long before sleeping on the queue's condition variable (no wake-up convoy on q_mu)
+  static const int spin_us = [] {
+    const char* e = getenv("MV_Q_SPIN_US");
+    return e ? atoi(e) : 0;
+  }();
+  bool lingered = false, spun = false;
   std::unique_lock<std::mutex> ql(ctx->q_mu);
   ctx->q.push_back(&req);
+  if (ctx->q_lingering) ctx->q_linger_cv.notify_one();
   auto any_busy = [ctx] {
     for (int k = 0; k < ctx->q_sets; k++)
       if (ctx->q_set_busy[k]) return true;
@@ -1652,12 +1670,35 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     int s = -1;
     for (int k = 0; k < ctx->q_sets && s < 0; k++)
       if (!ctx->q_set_busy[k]) s = k;
-    if (ctx->q_packing || s < 0 || ctx->q.empty()) {
+    if (req.taken && spin_us > 0 && !spun) {
+      spun = true;
+      ql.unlock();
+      const auto dl = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+      while (!req.done.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < dl)
+        std::this_thread::yield();
+      ql.lock();
+      continue;
+    }
+    if (ctx->q_packing || ctx->q_lingering || s < 0 || ctx->q.empty()) {
       ctx->q_cv.wait(ql);
+      continue;
+    }
+    // Callers released together by a pass come back within microseconds of each other; the
+    // first one back waits (bounded) for the others instead of starting a pass of one, so the
+    // passes stay as large as the callers' groups (a lone caller's last pass carried 1: no wait)
+    if (linger_us > 0 && !lingered && ctx->q.size() < ctx->q_last_calls) {
+      lingered = true;
+      ctx->q_lingering = true;
+      const auto dl = std::chrono::steady_clock::now() + std::chrono::microseconds(linger_us);
+      while (ctx->q.size() < ctx->q_last_calls && ctx->q_linger_cv.wait_until(ql, dl) != std::cv_status::timeout) {
+      }
+      ctx->q_lingering = false;
+      ctx->q_cv.notify_all();
       continue;
     }
     std::deque<mv_ctx::BlockReq*> batch;
     batch.swap(ctx->q);  // no allocation
+    for (auto* r : batch) r->taken = true;
     uint64_t blocks = 0, bytes = 0;
     for (auto* r : batch) {
       blocks += r->n;
@@ -1679,6 +1720,7 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
       ctx->q_cv.notify_all();
     });
     ql.lock();
+    ctx->q_last_calls = batch.size();
     for (auto* r : batch) r->done = true;
     if (big) mark_all(false);
     else ctx->q_set_busy[s] = false;
