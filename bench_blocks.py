@@ -432,7 +432,8 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     roof = None
     from bench import pmc_traffic
 
-    kname = "k_b2_quad"
+    # the batch-size hash kernel (blake2b_lane.hip; MV_B2_LANE=0: the quad kernel)
+    kname = "k_b2_quad" if os.environ.get("MV_B2_LANE") == "0" else "k_b2_lane"
     if os.environ.get("MV_BLK_FUSED") == "1":  # the fused parse + hash kernel (the "parse" stage)
         kname, hash_ms = "k_block_ingest_hash", stage_ms.get("parse")
     traffic, traffic_src = pmc_traffic(kname, "c4")

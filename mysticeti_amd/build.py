@@ -20,7 +20,7 @@ LIB = os.path.join(HERE, "libmysti_verify.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
-SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "wal.hip", "engine.cpp",
+SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "wal.hip", "engine.cpp",
            "block_codec.cpp"]
 HEADERS = ["asm_ops.h", "fe25519.h", "ge25519.h", "hash_dev.h", "scalar25519.h", "kernels.h", "block_codec.h", "tables.h", "carry32.h", "comb.h", "quad25519.h", "fe_q4.h", "fe_r16.h", "blake2b_quad.h", "block_verdict.h", "ingest_dev.h"]
 

@@ -70,11 +70,9 @@ constexpr uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6e
                             0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                             0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 
-MV_DEV uint64_t add64(uint64_t a, uint64_t b) {
-  uint64_t r;
-  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+// a plain 64-bit add: the compiler selects v_lshl_add_u64 itself and, unlike for an inline-asm
+// one, knows its hazards (no s_nop after every add)
+MV_DEV uint64_t add64(uint64_t a, uint64_t b) { return a + b; }
 MV_DEV uint64_t pack(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 MV_DEV uint64_t ror32(uint64_t x) { return (x >> 32) | (x << 32); }
 MV_DEV uint64_t ror24(uint64_t x) {

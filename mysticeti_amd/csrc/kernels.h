@@ -22,11 +22,16 @@ hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_
                           hipStream_t s);
 hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                              uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
-// blake2b_quad.hip: the same two hashes with four lanes per string (the product kernels;
-// launch_blake2b / launch_block_hash route to them unless MV_HASH_LANE=1)
+// blake2b_quad.hip: the same two hashes with four lanes per string (launch_blake2b /
+// launch_block_hash route to them; at batch size they route on to blake2b_lane.hip)
 hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                                hipStream_t s);
 hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                                  uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
+// blake2b_lane.hip: one lane per string (batch-size calls; the quad launchers route to it)
+hipError_t launch_blake2b_lane(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+                               hipStream_t s);
+hipError_t launch_block_hash_lane(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                                   uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
 hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s);
 // batch.hip: random-linear-combination batch verify with exact on-device fallback.

@@ -6,10 +6,8 @@
 //                    VerificationKey::verify, called at mysticeti-core/src/crypto.rs:188),
 //                    on half-size scalars (scalar25519.h sc_halfsize)
 //   k_sign           RFC 8032 signing, one per lane (crypto.rs:199-223, corpus generation)
-//   k_blake2b        Blake2b-256 of staged byte strings (crypto.rs:34 BlockHasher)
-//   k_block_hash     signed message Blake2b(P) and block digest Blake2b(P || sig) of
-//                    staged pre-images, sharing the common compressions
-//                    (crypto.rs:38-61 and crypto.rs:174-187)
+//   (BLAKE2b: blake2b_quad.hip for small calls, blake2b_lane.hip at batch size; the
+//   launch_blake2b / launch_block_hash entry points below route between them)
 //   k_selftest       field / scalar primitives for the parity tests
 //
 // The verify kernel is INT32-VALU bound: HBM traffic is 128 B of
@@ -343,106 +341,6 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
-// Load message words [b*16, b*16+16) of a byte string at 8-aligned `p`, zeroing bytes >= lim.
-MV_DEV void b2_load_block(uint64_t m[16], const uint8_t* p, uint64_t blk, uint64_t lim) {
-  const uint64_t* q = reinterpret_cast<const uint64_t*>(p) + blk * 16;
-  const uint64_t base = blk * 128;
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    uint64_t pos = base + 8 * j;
-    uint64_t v = 0;
-    if (pos < lim) {
-      v = q[j];
-      uint64_t rem = lim - pos;
-      if (rem < 8) v &= (1ULL << (8 * rem)) - 1;
-    }
-    m[j] = v;
-  }
-}
-MV_DEV void b2_store256(uint8_t* out, const uint64_t h[8]) {
-  uint32_t w[8];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    w[2 * i] = (uint32_t)h[i];
-    w[2 * i + 1] = (uint32_t)(h[i] >> 32);
-  }
-  store8(out, w);
-}
-
-// Blake2b-256 of n staged strings (each 8-aligned, readable up to round-up(len, 8)).
-__global__ void __launch_bounds__(256) k_blake2b(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
-                                                 const uint64_t* __restrict__ len, uint32_t n,
-                                                 uint8_t* __restrict__ out) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= n) return;
-  const uint8_t* p = buf + off[gid];
-  const uint64_t L = len[gid];
-  uint64_t h[8], m[16];
-  b2_init256(h);
-  const uint64_t nb = L == 0 ? 1 : (L + 127) / 128;
-  for (uint64_t b = 0; b + 1 < nb; b++) {
-    b2_load_block(m, p, b, L);
-    b2_compress(h, m, 128 * (b + 1), false);
-  }
-  b2_load_block(m, p, nb - 1, L);
-  b2_compress(h, m, L, true);
-  b2_store256(out + 32 * (size_t)gid, h);
-}
-
-// Staged P || sig (8-aligned, len[i] = |P|): msg = B2(P), digest = B2(P || sig).
-// The compressions common to both hashes are done once. All compressions go through ONE
-// b2_compress call site (a step loop that picks the block, the length limit, the counter
-// and the final flag), so the unrolled compression (~20 KB of code) is instantiated once:
-// with a call site per phase the kernel overflowed the instruction cache. The next step's
-// message block is loaded during the current compression.
-__global__ void __launch_bounds__(256) k_block_hash(const uint8_t* __restrict__ buf,
-                                                    const uint64_t* __restrict__ off,
-                                                    const uint64_t* __restrict__ len, uint32_t n,
-                                                    uint8_t* __restrict__ msg_out, uint8_t* __restrict__ dig_out) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= n) return;
-  const uint8_t* p = buf + off[gid];
-  const uint64_t L = len[gid], LD = L + 64;
-  const uint64_t common = L == 0 ? 0 : (L - 1) / 128;  // non-final in both hashes
-  const uint64_t last = (LD - 1) / 128;                 // final block of B2(P || sig)
-  // steps: [0, common) shared; common: final of B2(P); common+1 ..: rest of B2(P || sig)
-  const uint64_t nsteps = last + 2;
-  auto blk = [&](uint64_t s, uint64_t& lim) -> uint64_t {
-    if (s == common) {
-      lim = L;
-      return common;
-    }
-    lim = LD;
-    return s < common ? s : s - 1;
-  };
-  uint64_t h[8], hs[8], m[16], mn[16];
-  b2_init256(h);
-  uint64_t lim;
-  b2_load_block(m, p, blk(0, lim), lim);
-  for (uint64_t s = 0; s < nsteps; s++) {
-    uint64_t lim_n;
-    const uint64_t bn = blk(s + 1 < nsteps ? s + 1 : s, lim_n);
-    b2_load_block(mn, p, bn, lim_n);
-    const bool msg_final = s == common;
-    const uint64_t b = s < common ? s : (msg_final ? common : s - 1);
-    const bool fin = msg_final || b == last;
-    const uint64_t t = msg_final ? L : (b == last ? LD : 128 * (b + 1));
-    if (msg_final) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) hs[i] = h[i];
-    }
-    b2_compress(h, m, t, fin);
-    if (msg_final) {
-      b2_store256(msg_out + 32 * (size_t)gid, h);
-#pragma unroll
-      for (int i = 0; i < 8; i++) h[i] = hs[i];
-    }
-#pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = mn[j];
-  }
-  b2_store256(dig_out + 32 * (size_t)gid, h);
-}
-
 // Field / scalar primitives on 16-word lane inputs (parity tests).
 __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restrict__ in, uint32_t n,
                                                  const uint4* __restrict__ btab_g, uint32_t* __restrict__ out) {
@@ -657,27 +555,15 @@ hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, cons
   hipLaunchKernelGGL(mv::k_sign, dim3((n + 255) / 256), dim3(256), 0, s, seed, msg, n, (const uint4*)btab, pk, sig);
   return hipGetLastError();
 }
-// A/B switch: MV_HASH_LANE=1 runs the lane-per-string hash kernels instead of blake2b_quad.hip
-static bool hash_lane_kernels() {
-  static const bool v = [] {
-    const char* e = getenv("MV_HASH_LANE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
+// BLAKE2b launchers: four lanes per string on small calls (blake2b_quad.hip), one lane per
+// string at batch size (blake2b_lane.hip)
 hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                           hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  if (!hash_lane_kernels()) return launch_blake2b_quad(buf, off, len, n, out, s);
-  hipLaunchKernelGGL(mv::k_blake2b, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, out);
-  return hipGetLastError();
+  return launch_blake2b_quad(buf, off, len, n, out, s);
 }
 hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                              uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  if (!hash_lane_kernels()) return launch_block_hash_quad(buf, off, len, n, msg_out, dig_out, s);
-  hipLaunchKernelGGL(mv::k_block_hash, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, msg_out, dig_out);
-  return hipGetLastError();
+  return launch_block_hash_quad(buf, off, len, n, msg_out, dig_out, s);
 }
 hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -240,3 +240,17 @@ def test_blake2b_ragged_lengths(engine):
     out = engine.blake2b256(items)
     for it, o in zip(items, out):
         assert bytes(o) == hashlib.blake2b(it, digest_size=32).digest(), len(it)
+
+
+def test_blake2b_ragged_lengths_batch_size(engine):
+    """A batch-size call (>= MV_BATCH_MIN strings: the lane-per-string kernel, blake2b_lane.hip)
+    with ragged lengths, empty and block-boundary strings among them (checked with hashlib)."""
+    import hashlib
+
+    rng = np.random.default_rng(11)
+    lens = [0, 1, 127, 128, 129, 255, 256, 257, 8060, 8124] + [int(x) for x in rng.integers(0, 3000, size=4200)]
+    rng.shuffle(lens)
+    items = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    out = engine.blake2b256(items)
+    for it, o in zip(items, out):
+        assert bytes(o) == hashlib.blake2b(it, digest_size=32).digest(), len(it)

@@ -35,7 +35,7 @@ cp -r "$OUT/trace_c4" "$OUT/c4/trace1"
 for k in k_bv_prep k_bv_bucket k_fine_sort k_part_scatter k_bv_final k_bv_reduce; do
   python tools/pmc_summary.py "$OUT/c2" $k --json "$OUT/pmc_c2_$k.json" > "$OUT/pmc_c2_$k.txt" || true
 done
-for k in k_b2_quad k_block_ingest k_bv_prep k_bv_bucket; do
+for k in k_b2_lane k_block_ingest k_bv_prep k_bv_bucket; do
   python tools/pmc_summary.py "$OUT/c4" $k --json "$OUT/pmc_c4_$k.json" > "$OUT/pmc_c4_$k.txt" || true
 done
 echo profile done
