@@ -125,6 +125,9 @@ struct Device {
   hipEvent_t blk_done[kBlkSlots] = {};
   bool blk_used[kBlkSlots] = {};
   int blk_next = 0;
+  // batch-size block calls: the second half's parse on another stream beside the first half's
+  // hash (enqueue_blocks); the two events order it after the first parse and before the hash
+  hipEvent_t pipe_ev[2] = {};
   HostBuf h_in, h_out;
   // mv_verify_blocks passes (the submission queue): kPassSets sets of pinned staging, device
   // buffers and a stream each, so pass k + 1 is packed and enqueued while passes k, k - 1, ...
@@ -423,6 +426,14 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
 // (scratch then).
 // own: scratch owned by the caller (a submission-queue pass set, whose reuse is ordered by its
 // own completion event): no ring slot, no slot events (two runtime calls less per pass).
+static bool blk_pipe() {  // MV_BLK_PIPE=0 (A/B): batch-size block calls on one stream
+  static const bool v = [] {
+    const char* e = getenv("MV_BLK_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
                          const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
                          hipStream_t s, DevBuf* own = nullptr) {
@@ -521,6 +532,31 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
     HIPCHK(ctx, mark(1));
+  } else if (batch && !split && !ctx->stage_timing && n >= 2 * MV_BATCH_MIN && blk_pipe()) {
+    // Batch-size calls, two halves: the HBM-bound parse of the second half runs on another
+    // stream beside the VALU-bound hash of the first (the two streams of a caller's
+    // alternating calls otherwise start in phase, parse beside parse). MV_BLK_PIPE=0: one
+    // stream. Not under stage timing, whose per-stage events need the stages in sequence.
+    const uint32_t h = ((n / 2) + 63) & ~63u;
+    for (int k = 0; k < 2; k++) {
+      if (!dev.pstream[k]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking));
+      if (!dev.pipe_ev[k]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pipe_ev[k], hipEventDisableTiming));
+    }
+    hipStream_t aux = s == dev.pstream[0] ? dev.pstream[1] : dev.pstream[0];
+    auto parse = [&](uint32_t lo, uint32_t hi, hipStream_t st) {
+      return mvk::launch_block_parse(d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
+                                     com.epoch, com.quorum_threshold, stage, poff + lo, plen + lo, sig + 64 * (size_t)lo,
+                                     kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
+    };
+    HIPCHK(ctx, parse(0, h, s));
+    HIPCHK(ctx, hipEventRecord(dev.pipe_ev[0], s));
+    HIPCHK(ctx, hipStreamWaitEvent(aux, dev.pipe_ev[0], 0));
+    HIPCHK(ctx, parse(h, n, aux));
+    HIPCHK(ctx, hipEventRecord(dev.pipe_ev[1], aux));
+    HIPCHK(ctx, mark(1));
+    HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, h, md, bd, s));
+    HIPCHK(ctx, hipStreamWaitEvent(s, dev.pipe_ev[1], 0));
+    HIPCHK(ctx, mvk::launch_block_hash(stage, poff + h, plen + h, n - h, md + 32 * (size_t)h, bd + 32 * (size_t)h, s));
   } else {
     HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                         com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));

@@ -243,3 +243,30 @@ def test_pinned_caller_buffer_is_read_in_place(engine):
     assert int(st1[123]) != 0 and (np.delete(st1, 123) == 0).all()
     ost, omd, obd = O.block_verify(bins[123], pks, stakes, 0)
     assert int(st1[123]) == ost and md1[123].tobytes() == omd and bd1[123].tobytes() == obd
+
+
+def test_batch_call_in_two_halves_matches_small_calls(engine):
+    """8,200 config-4-shaped blocks in one call (>= 2 x MV_BATCH_MIN: the parse of the second
+    half runs on another stream beside the hash of the first, engine.cpp enqueue_blocks), with
+    tampered and truncated blocks in both halves: every verdict and digest equals the one the
+    same block gets in 64-block calls (the comb path, held to the oracle by the tests above)."""
+    import mysticeti_amd.blocks as MB
+
+    base = MB.config4(engine, rounds=41)
+    pks, stakes = MB.committee(engine, 100, distinct=True)
+    engine.set_committee(pks, stakes, 0)
+    bins = list(base) + list(base)
+    for i in (10, 4200, 8100):  # stale digest
+        t = bytearray(bins[i])
+        t[-20] ^= 0x10
+        bins[i] = bytes(t)
+    for i in (3000, 7000):  # truncated
+        bins[i] = bins[i][: len(bins[i]) // 2]
+    st, md, bd = engine.verify_blocks(bins)
+    assert st.shape == (8200,)
+    assert (st[[10, 4200, 8100]] == 2).all() and st[3000] != 0 and st[7000] != 0
+    for lo in list(range(0, 256, 64)) + list(range(4096, 4352, 64)) + list(range(7936, 8200, 64)) + [2944, 6976]:
+        s2, m2, b2 = engine.verify_blocks(bins[lo:lo + 64])
+        assert (s2 == st[lo:lo + 64]).all(), lo
+        ok = s2 == 0
+        assert (m2[ok] == md[lo:lo + 64][ok]).all() and (b2[ok] == bd[lo:lo + 64][ok]).all(), lo
