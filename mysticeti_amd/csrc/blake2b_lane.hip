@@ -101,8 +101,10 @@ MV_DEV void load_block(uint64_t (&m)[16], const uint8_t* p, uint64_t b, uint64_t
 // the staged P || sig with |P| = len; otherwise out0 = B2(string). The message block is loaded
 // at the top of its step (tools/gpu_r03z.sh: prefetching it during the previous compression
 // needs 134 VGPRs and 3 waves per SIMD and measured no faster; neither did a forced 5 waves per
-// SIMD (spills), a shift + add form of the 63-bit rotation, nor the four G's of a half-round
-// written in lock-step (the scheduler pairs them the same way).
+// SIMD (spills), a shift + add form of the 63-bit rotation, the four G's of a half-round
+// written in lock-step (the scheduler pairs them the same way), nor h parked in LDS during the
+// rounds (84 VGPRs, 5 waves per SIMD: 4.06 ms per 2^20 either way). The kernel is bound by VALU
+// issue: ~2,000 instructions per compression per wave, 20 per G, no cross-lane or LDS work.
 template <bool DUAL>
 __global__ void __launch_bounds__(64) k_b2_lane(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                 const uint64_t* __restrict__ len, uint32_t n,
