@@ -1462,6 +1462,7 @@ void mv_destroy(mv_ctx* ctx) {
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
       for (hipEvent_t ev : dev.chunk_ev[k])
         if (ev) (void)hipEventDestroy(ev);
+      if (dev.pipe_ev[k]) (void)hipEventDestroy(dev.pipe_ev[k]);
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);
