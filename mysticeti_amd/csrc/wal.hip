@@ -180,6 +180,37 @@ MV_DEV uint64_t le64_bounded(const uint8_t* img, uint64_t size, uint64_t p) {
 }
 
 // record = position | status << 60 (status: MV_WAL_OK for an entry whose crc is still to check)
+// The walk is a chain of dependent header reads (~1 us of HBM latency each, ~1,800 per 16-MiB map
+// of config-4 blocks). It runs ahead speculatively: the headers at p + k * stride, k < WALK_AHEAD,
+// are loaded together, stride = the last entry's length (WAL entries of one kind share a length);
+// they are then consumed in order while each entry's length equals the stride, and the walk
+// re-aims at the first that differs. The checks, records and flags are those of the one-at-a-time
+// walk (wal.rs:285-346) in the same order; a mispredicted header is never used.
+constexpr int WALK_AHEAD = 8;
+// a header's 16 bytes at q as five aligned dwords, loaded without a branch (so the run-ahead
+// loads are all in flight together); `fast` false (the header would reach past the image, or the
+// image is shorter than 20 bytes): the consumer reads it byte-wise (le64_bounded)
+struct WalkHdr {
+  uint32_t w[5];
+  bool fast;
+};
+MV_DEV void hdr_load(WalkHdr& h, const uint8_t* img, uint64_t size, uint64_t q) {
+  h.fast = size >= 20 && q <= size - 20;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(img + (h.fast ? (q & ~3ull) : 0ull));
+#pragma unroll
+  for (int i = 0; i < 5; i++) h.w[i] = w[i];
+}
+MV_DEV void hdr_get(const WalkHdr& h, const uint8_t* img, uint64_t size, uint64_t q, uint64_t& crc, uint64_t& hi) {
+  if (h.fast) {
+    const uint32_t s = (uint32_t)(q & 3);
+    auto fn = [&](int i) { return s ? __builtin_amdgcn_alignbyte(h.w[i + 1], h.w[i], s) : h.w[i]; };
+    crc = ((uint64_t)fn(1) << 32) | fn(0);
+    hi = ((uint64_t)fn(3) << 32) | fn(2);
+  } else {
+    crc = le64_bounded(img, size, q);
+    hi = le64_bounded(img, size, q + 8);
+  }
+}
 __global__ void __launch_bounds__(64) k_wal_walk(const uint8_t* __restrict__ img, uint64_t size, uint64_t end_pos,
                                                  uint32_t map_bits, uint32_t nmaps, uint32_t cap_pm,
                                                  const uint64_t* __restrict__ moff,
@@ -188,44 +219,75 @@ __global__ void __launch_bounds__(64) k_wal_walk(const uint8_t* __restrict__ img
   const uint32_t m = blockIdx.x * 64 + threadIdx.x;
   if (m >= nmaps) return;
   const uint64_t msize = 1ull << map_bits, start = (uint64_t)m << map_bits;
-  uint64_t p = start;
+  uint64_t p = start, stride = 0;
   uint32_t count = 0;
-  uint8_t flag;
+  uint8_t flag = MAP_NEXT;
   // moff (the second walk): map m's records at rec + moff[m], as many as the first walk counted
   unsigned long long* r = moff ? rec + moff[m] : rec + (size_t)m * cap_pm;
   if (moff) cap_pm = mcount[m];
-  for (;;) {
-    if (p >= end_pos) {
-      flag = p == start ? MAP_EMPTY : MAP_END;
-      break;
+  bool done = false, have_next = false;
+  WalkHdr hd[WALK_AHEAD], hn[WALK_AHEAD];
+  while (!done) {
+    if (have_next) {
+#pragma unroll
+      for (int k = 0; k < WALK_AHEAD; k++) hd[k] = hn[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < WALK_AHEAD; k++) hdr_load(hd[k], img, size, p + (uint64_t)k * stride);
     }
-    const uint64_t boff = p - start;
-    if (msize - boff < 16) {  // no room for a header (wal.rs:297-300)
-      flag = MAP_NEXT;
-      break;
+    const int ahead = stride ? WALK_AHEAD : 1;
+    // the round after this one, in flight while this one is consumed (it is used only if all of
+    // this round's entries have the stride)
+    have_next = stride != 0;
+    if (have_next) {
+#pragma unroll
+      for (int k = 0; k < WALK_AHEAD; k++) hdr_load(hn[k], img, size, p + (uint64_t)(WALK_AHEAD + k) * stride);
     }
-    const uint64_t crc = le64_bounded(img, size, p), hi = le64_bounded(img, size, p + 8);
-    const uint64_t len = hi & 0xffffffffull;
-    (void)crc;
-    if (len == 0) {
-      if (crc == 0) {
-        flag = boff == 0 ? MAP_EMPTY : MAP_NEXT;
+#pragma unroll
+    for (int k = 0; k < WALK_AHEAD; k++) {
+      if (k >= ahead) break;
+      // the entry at p (= the k-th speculative position: the lengths so far equal the stride)
+      if (p >= end_pos) {
+        flag = p == start ? MAP_EMPTY : MAP_END;
+        done = true;
         break;
       }
-      if (count < cap_pm) r[count] = p | ((unsigned long long)MV_WAL_NONZERO_CRC_LEN0 << 60);
+      const uint64_t boff = p - start;
+      if (msize - boff < 16) {  // no room for a header (wal.rs:297-300)
+        flag = MAP_NEXT;
+        done = true;
+        break;
+      }
+      uint64_t crc, hi;
+      hdr_get(hd[k], img, size, p, crc, hi);
+      const uint64_t len = hi & 0xffffffffull;
+      if (len == 0) {
+        if (crc == 0) {
+          flag = boff == 0 ? MAP_EMPTY : MAP_NEXT;
+        } else {
+          if (count < cap_pm) r[count] = p | ((unsigned long long)MV_WAL_NONZERO_CRC_LEN0 << 60);
+          count++;
+          flag = MAP_BAD;
+        }
+        done = true;
+        break;
+      }
+      if (len < 16 || boff + len > msize) {
+        if (count < cap_pm) r[count] = p | ((unsigned long long)MV_WAL_BAD_LENGTH << 60);
+        count++;
+        flag = MAP_BAD;
+        done = true;
+        break;
+      }
+      if (count < cap_pm) r[count] = p;
       count++;
-      flag = MAP_BAD;
-      break;
+      p += len;
+      if (len != stride) {  // the next speculative header is not at p: re-aim
+        stride = len;
+        have_next = false;
+        break;
+      }
     }
-    if (len < 16 || boff + len > msize) {
-      if (count < cap_pm) r[count] = p | ((unsigned long long)MV_WAL_BAD_LENGTH << 60);
-      count++;
-      flag = MAP_BAD;
-      break;
-    }
-    if (count < cap_pm) r[count] = p;
-    count++;
-    p += len;
   }
   mcount[m] = count;
   mflag[m] = flag;
