@@ -41,7 +41,7 @@ constexpr int T_WORDS = 256;                 // the byte table (1-byte shift), g
 constexpr uint32_t PREFIX = 0x9226f562u;     // crc_raw(0, PREFIX as 4 LE bytes) = 0xFFFFFFFF
 constexpr int WG = 1024;                     // threads per crc workgroup
 #ifndef MV_WAL_ROWS
-#define MV_WAL_ROWS 8
+#define MV_WAL_ROWS 16  // 16 and 32: crc 2.47-2.51 ms per 2^20 entries; 8: 2.62-2.67; 12, 24: ~3.0 (tools/gpu_r03ah.sh)
 #endif
 constexpr int WAL_ROWS = MV_WAL_ROWS;        // 256-B rows in flight per wave
 
