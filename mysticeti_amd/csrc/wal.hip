@@ -72,7 +72,7 @@ MV_DEV uint32_t shiftk(const Lds& L, int k, uint32_t u) {
   const uint32_t* s = L.s + k * 1024;
   return s[u & 255] ^ s[256 + ((u >> 8) & 255)] ^ s[512 + ((u >> 16) & 255)] ^ s[768 + (u >> 24)];
 }
-MV_DEV uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+MV_DEV uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }  // (nt loads: no gain)
 
 // crc_raw(0xFFFFFFFF, base[a, b)) (the CRC register before the final xor), on the whole wave.
 // Reads only the aligned dwords that hold bytes of [a, b).
