@@ -95,13 +95,9 @@ hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uin
   }();
   if (lane_kernel)
     hipLaunchKernelGGL(mv::k_block_parse, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, cv, io);
-  else {
-    // MV_INGEST_LDS_PAD=<bytes> (A/B): extra dynamic LDS per workgroup, which caps the ingest
-    // workgroups per CU and leaves CU room for the other stream's VALU-bound kernels
-    const char* pe = getenv("MV_INGEST_LDS_PAD");
-    const size_t pad = pe ? (size_t)atoll(pe) : 0;
-    hipLaunchKernelGGL(mv::k_block_ingest, dim3(n), dim3(64), pad, s, buf, off, len, n, cv, io);
-  }
+  else  // (capping its workgroups per CU with padded LDS, to leave room for the other stream's
+        // kernels, measured slower: 79 vs 103 M config-4 blocks/s, profiles/r03/ab/)
+    hipLaunchKernelGGL(mv::k_block_ingest, dim3(n), dim3(64), 0, s, buf, off, len, n, cv, io);
   return hipGetLastError();
 }
 
