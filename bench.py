@@ -209,7 +209,7 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     import mysticeti_amd as M
-    from mysticeti_amd.dist import all_ranks_ok, shard_range, timed_region
+    from mysticeti_amd.dist import all_ranks_ok, footprint, hbm_sample, rss_mark, shard_range, timed_region
 
     eng = M.Engine(devices=(local_rank,))
     n = args.batch
@@ -254,6 +254,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    hbm_sample(torch, dev, "config2")
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev_side = [torch.cuda.Event() for _ in range(nstreams)]
 
@@ -389,6 +390,7 @@ def main():
         # the legs below measure the unguarded default
         eng.set_batch_groups(args.groups)
 
+    rss_mark("adversarial")
     # PCIe-inclusive rates (host buffers through the C ABI)
     e2e = None
     if rank == 0 and not args.no_e2e:
@@ -415,6 +417,7 @@ def main():
                        "memory (mv_host_alloc), chunked copies beside the verify; pageable: plain numpy arrays",
                "pageable": round(v_page, 1), "accepted": acc_pin, "accepted_pageable": acc_page}
 
+    rss_mark("end_to_end")
     # config 4 (the largest workload): whole-block verification of HBM-resident 100-validator
     # blocks, measured in the same run (bench_blocks.config4_measure)
     cfg4 = None
@@ -422,11 +425,12 @@ def main():
         import bench_blocks
 
         cfg4 = bench_blocks.config4_measure(eng, torch, local_rank, world, dist, n=args.config4_batch,
-                                            steps=max(3, min(args.steps, 100)), warmup=max(1, min(args.warmup, 3)),
+                                            steps=max(3, min(args.steps, 100)), warmup=max(4, min(args.warmup, 8)),
                                             nstreams=nstreams,
                                             cpu=args.cpu_sample > 0, host_blocks=args.host_fed_blocks)
         ok = ok and cfg4["correct"]
 
+    rss_mark("config4")
     # f4: the WAL replay check over an HBM-resident WAL of config-4 blocks (bench_wal.wal_measure)
     walr = None
     if args.wal and args.path == "batch" and not args.corrupt:
@@ -436,6 +440,7 @@ def main():
                                      steps=max(3, min(args.steps // 4, 50)), warmup=1, cpu=args.cpu_sample > 0)
         ok = ok and walr["correct"]
 
+    rss_mark("wal")
     # config 5 (the online path): latency of 64-block calls and concurrent 1-block callers through
     # mv_verify_blocks on host buffers, GPU and CPU in the same run (bench_blocks.config5_measure);
     # rank 0 only (the host CPU legs would otherwise compete across ranks)
@@ -448,11 +453,15 @@ def main():
                                             cpu=args.cpu_sample > 0)
         ok = ok and cfg5["correct"]
 
+    rss_mark("config5")
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0:
+        cpu = cpu_baseline(d_pk.cpu().numpy(), d_sig.cpu().numpy(), msg_h, min(args.cpu_sample, n))
+        rss_mark("cpu_baseline")
+    # per-rank peak host RSS and HBM in use (all ranks; the line must hold at 8 ranks per node)
+    fp = footprint(rank, dist)
     out = None
     if rank == 0:
-        cpu = None
-        if args.cpu_sample > 0:
-            cpu = cpu_baseline(d_pk.cpu().numpy(), d_sig.cpu().numpy(), msg_h, min(args.cpu_sample, n))
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -500,6 +509,9 @@ def main():
             "config5": cfg5,
             "wal": walr,
             "end_to_end": e2e,
+            "footprint": {"per_rank": fp, "note": "host_rss_peak_GB: getrusage ru_maxrss (pinned staging included); "
+                                                  "hbm_peak_GB: largest hipMemGetInfo total - free seen after each "
+                                                  "leg's warm-up (device-wide)"},
             "correct": bool(ok),
             "path": args.path,
             "batch_equation_held": batch_ok,

@@ -118,16 +118,23 @@ struct Device {
   hipEvent_t sscr_done[kSlots] = {};
   bool sscr_used[kSlots] = {};
   int sscr_next = 0;
-  // block-pipeline scratch: one slot per pass set, so passes on different streams never
-  // wait for each other's scratch
-  static constexpr int kBlkSlots = 4;
+  // device-API block-pipeline scratch: a ring of two slots (a caller alternating two streams
+  // keeps one call running beside the next), all grown together on first use so no slot is
+  // allocated inside a caller's steady state (a 2^21-block slot is ~21 GB; round 3's four
+  // lazily grown slots put one ~0.8 s allocation into the driver's timed steps)
+  static constexpr int kBlkSlots = 2;
   DevBuf blk[kBlkSlots];
   hipEvent_t blk_done[kBlkSlots] = {};
   bool blk_used[kBlkSlots] = {};
   int blk_next = 0;
-  // batch-size block calls: the second half's parse on another stream beside the first half's
-  // hash (enqueue_blocks); the two events order it after the first parse and before the hash
-  hipEvent_t pipe_ev[2] = {};
+  // batch-size block calls: the second half's parse on an aux stream beside the first half's
+  // hash (enqueue_blocks). One aux stream and event pair per scratch owner (ring slot or pass
+  // set), so two calls in flight never queue their second halves behind each other.
+  struct BlkAux {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[2] = {};
+  };
+  BlkAux blk_aux[kBlkSlots];
   HostBuf h_in, h_out;
   // mv_verify_blocks passes (the submission queue): kPassSets sets of pinned staging, device
   // buffers and a stream each, so pass k + 1 is packed and enqueued while passes k, k - 1, ...
@@ -137,6 +144,7 @@ struct Device {
   struct PassSet {
     HostBuf h_in, h_out;
     DevBuf bytes, out2, scr;  // scr: the block pipeline's scratch for this set's passes
+    BlkAux aux;               // the two-halves parse of a large host-fed chunk
     hipStream_t stream = nullptr;  // set 0: `stream`, set 1: pstream[1], set k >= 2: qstream[k]
     hipEvent_t done = nullptr;
     // the chunk in flight: items [lo, lo + m) of `it`, outputs in h_out when finished
@@ -436,7 +444,7 @@ static bool blk_pipe() {  // MV_BLK_PIPE=0 (A/B): batch-size block calls on one 
 
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
                          const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
-                         hipStream_t s, DevBuf* own = nullptr) {
+                         hipStream_t s, DevBuf* own = nullptr, Device::BlkAux* own_aux = nullptr) {
   if (n == 0) return MV_OK;
   const mvh::Committee& com = ctx->committee;
   int slot = -1;
@@ -494,6 +502,12 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   o += al(32 * nn);
   const size_t o_q = o;
   if (split) o += 2 * al(144 * nn) + al(nn);
+  if (!own && scr.cap < o) {
+    // grow every ring slot at once (one device drain: another slot may still be read by a call
+    // on another stream), so the ring never allocates again at this size
+    HIPCHK(ctx, hipDeviceSynchronize());
+    for (DevBuf& x : dev.blk) HIPCHK(ctx, x.ensure(o));
+  }
   HIPCHK(ctx, scr.ensure(o));
   char* b = scr.as<char>();
   uint8_t* stage = (uint8_t*)(b + o_stage);
@@ -532,30 +546,31 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
     HIPCHK(ctx, mark(1));
-  } else if (batch && !split && !ctx->stage_timing && n >= 2 * MV_BATCH_MIN && blk_pipe()) {
+  } else if (batch && !split && !ctx->stage_timing && n >= 2 * MV_BATCH_MIN + 64 && blk_pipe() && (!own || own_aux)) {
     // Batch-size calls, two halves: the HBM-bound parse of the second half runs on another
     // stream beside the VALU-bound hash of the first (the two streams of a caller's
     // alternating calls otherwise start in phase, parse beside parse). MV_BLK_PIPE=0: one
     // stream. Not under stage timing, whose per-stage events need the stages in sequence.
+    // both halves >= MV_BATCH_MIN, so both hash on the batch-size kernel (n >= 2 MV_BATCH_MIN + 64)
     const uint32_t h = ((n / 2) + 63) & ~63u;
-    for (int k = 0; k < 2; k++) {
-      if (!dev.pstream[k]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking));
-      if (!dev.pipe_ev[k]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pipe_ev[k], hipEventDisableTiming));
-    }
-    hipStream_t aux = s == dev.pstream[0] ? dev.pstream[1] : dev.pstream[0];
+    Device::BlkAux& ax = own ? *own_aux : dev.blk_aux[slot];
+    if (!ax.stream) HIPCHK(ctx, hipStreamCreateWithFlags(&ax.stream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++)
+      if (!ax.ev[k]) HIPCHK(ctx, hipEventCreateWithFlags(&ax.ev[k], hipEventDisableTiming));
+    hipStream_t aux = ax.stream;
     auto parse = [&](uint32_t lo, uint32_t hi, hipStream_t st) {
       return mvk::launch_block_parse(d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
                                      com.epoch, com.quorum_threshold, stage, poff + lo, plen + lo, sig + 64 * (size_t)lo,
                                      kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
     };
     HIPCHK(ctx, parse(0, h, s));
-    HIPCHK(ctx, hipEventRecord(dev.pipe_ev[0], s));
-    HIPCHK(ctx, hipStreamWaitEvent(aux, dev.pipe_ev[0], 0));
+    HIPCHK(ctx, hipEventRecord(ax.ev[0], s));
+    HIPCHK(ctx, hipStreamWaitEvent(aux, ax.ev[0], 0));
     HIPCHK(ctx, parse(h, n, aux));
-    HIPCHK(ctx, hipEventRecord(dev.pipe_ev[1], aux));
+    HIPCHK(ctx, hipEventRecord(ax.ev[1], aux));
     HIPCHK(ctx, mark(1));
     HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, h, md, bd, s));
-    HIPCHK(ctx, hipStreamWaitEvent(s, dev.pipe_ev[1], 0));
+    HIPCHK(ctx, hipStreamWaitEvent(s, ax.ev[1], 0));
     HIPCHK(ctx, mvk::launch_block_hash(stage, poff + h, plen + h, n - h, md + 32 * (size_t)h, bd + 32 * (size_t)h, s));
   } else {
     HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
@@ -807,6 +822,7 @@ mv_status ensure_pass_set(mv_ctx* ctx, Device& dev, int s) {
 }
 
 bool host_pinned(const void* p);
+bool pinned_range_holds(const void* p, uint64_t bytes);
 
 // Packs items [lo, hi) into pass set s of dev and enqueues the device pipeline on its stream
 // (no wait). The set must be idle. A large chunk whose blocks already lie in page-locked
@@ -840,7 +856,10 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   }
   // any alignment (the ingest kernels read from the aligned word at or below a block's start);
   // gaps between blocks are copied too, so they must stay small
-  direct = direct && span && span <= 2 * bytes + 4096 && host_pinned(base + span - 1);
+  // ... and [base, base + span) must lie inside ONE page-locked allocation: a pass merges
+  // several callers' items, and two callers' buffers may sit close together with unpinned (or
+  // unmapped) memory between them
+  direct = direct && span && span <= 2 * bytes + 4096 && pinned_range_holds(base, span);
   const size_t buf_bytes = direct ? (span + 16 + 15) & ~(size_t)15 : (bytes + 16 + 15) & ~(size_t)15;
   const size_t o_off = buf_bytes, o_len = o_off + 8 * (size_t)m, total = o_len + 8 * (size_t)m;
   HIPCHK(ctx, ps.h_in.ensure(direct ? 16 * (size_t)m : total));
@@ -887,7 +906,7 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   const double t2 = trace ? now() : 0;
   uint8_t* dout = hout_dev ? hout_dev : ps.out2.as<uint8_t>();
   rc = enqueue_blocks(ctx, dev, dbuf, buf_bytes, (const uint64_t*)(dbuf + o_off), (const uint64_t*)(dbuf + o_len), m,
-                      dout + 64 * (size_t)m, dout, dout + 32 * (size_t)m, ps.stream, &ps.scr);
+                      dout + 64 * (size_t)m, dout, dout + 32 * (size_t)m, ps.stream, &ps.scr, &ps.aux);
   if (rc != MV_OK) {
     (void)hipStreamSynchronize(ps.stream);  // what was queued reads the staging
     return rc;
@@ -1070,6 +1089,22 @@ bool host_pinned(const void* p) {
     return false;
   }
   return a.type == hipMemoryTypeHost;
+}
+
+// True if [p, p + bytes) lies inside the one page-locked host allocation that holds p (the
+// allocation's address range from the runtime). False when the runtime cannot say.
+bool pinned_range_holds(const void* p, uint64_t bytes) {
+  if (!host_pinned(p)) return false;
+  void* start = nullptr;
+  size_t size = 0;
+  hipDeviceptr_t q = const_cast<void*>(p);
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, q) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, q) != hipSuccess || !start || !size) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t a = reinterpret_cast<uintptr_t>(start), b = reinterpret_cast<uintptr_t>(p);
+  return b >= a && b - a <= size && bytes <= size - (b - a);
 }
 
 // mv_ed25519_verify's batch path over [lo, hi) of the caller's arrays, in chunks of
@@ -1462,12 +1497,18 @@ void mv_destroy(mv_ctx* ctx) {
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
       for (hipEvent_t ev : dev.chunk_ev[k])
         if (ev) (void)hipEventDestroy(ev);
-      if (dev.pipe_ev[k]) (void)hipEventDestroy(dev.pipe_ev[k]);
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);
     for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
+    auto drop_aux = [](Device::BlkAux& a) {
+      for (hipEvent_t ev : a.ev)
+        if (ev) (void)hipEventDestroy(ev);
+      if (a.stream) (void)hipStreamDestroy(a.stream);
+    };
+    for (auto& a : dev.blk_aux) drop_aux(a);
+    for (auto& ps : dev.pset) drop_aux(ps.aux);
     dev.h_in.release();
     dev.h_out.release();
     for (auto& ps : dev.pset) {

@@ -134,3 +134,41 @@ def cpu_share() -> Tuple[int, str]:
     if omp.isdigit() and 0 < int(omp) < cores:
         cores, src = int(omp), "OMP_NUM_THREADS"
     return cores, src
+
+
+# ---- per-rank footprint (host RSS, HBM) reported in the bench line
+_hbm_peak = {"bytes": 0, "where": ""}
+_rss_marks = []  # (leg, peak host RSS so far, GB): which leg raised the peak
+
+
+def _maxrss_gb() -> float:
+    import resource
+
+    return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024 / 1e9, 3)
+
+
+def rss_mark(where: str) -> None:
+    """Records the peak host RSS so far, after leg `where` (ru_maxrss only grows)."""
+    _rss_marks.append((where, _maxrss_gb()))
+
+
+def hbm_sample(torch, dev, where: str = "") -> None:
+    """Records the device's HBM in use now (total - free, hipMemGetInfo) if it is the largest
+    seen; call it where the bench holds the most (after each leg's buffers are live)."""
+    free, total = torch.cuda.mem_get_info(dev)
+    used = int(total - free)
+    if used > _hbm_peak["bytes"]:
+        _hbm_peak["bytes"], _hbm_peak["where"] = used, where
+
+
+def footprint(rank: int, dist=None):
+    """[{rank, host_rss_peak_GB, hbm_peak_GB, hbm_peak_at}] over all ranks (gloo all_gather of
+    small dicts; rank order)."""
+    me = {"rank": rank, "host_rss_peak_GB": _maxrss_gb(),
+          "hbm_peak_GB": round(_hbm_peak["bytes"] / 1e9, 2), "hbm_peak_at": _hbm_peak["where"],
+          "rss_after": dict(_rss_marks)}
+    if dist is None:
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out

@@ -11,6 +11,8 @@ const SOURCES: &[&str] = &[
     "kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "wal.hip", "engine.cpp",
     "block_codec.cpp",
 ];
+// per-source flags (mysticeti_amd/build.py SOURCE_FLAGS)
+const SOURCE_FLAGS: &[(&str, &[&str])] = &[("batch.hip", &["-mllvm", "-amdgpu-sched-strategy=max-ilp"])];
 
 fn main() {
     println!("cargo:rerun-if-env-changed=MYSTI_VERIFY_LIB_DIR");
@@ -35,6 +37,11 @@ fn main() {
         let obj = out.join(format!("{s}.o"));
         let mut cmd = Command::new(&hipcc);
         cmd.args(["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall", "-Wno-unused-function"]);
+        for (name, flags) in SOURCE_FLAGS {
+            if name == s {
+                cmd.args(*flags);
+            }
+        }
         if !s.ends_with(".hip") {
             cmd.args(["-x", "hip"]);
         }

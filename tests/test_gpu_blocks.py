@@ -246,7 +246,7 @@ def test_pinned_caller_buffer_is_read_in_place(engine):
 
 
 def test_batch_call_in_two_halves_matches_small_calls(engine):
-    """8,200 config-4-shaped blocks in one call (>= 2 x MV_BATCH_MIN: the parse of the second
+    """8,300 config-4-shaped blocks in one call (both halves >= MV_BATCH_MIN: the parse of the second
     half runs on another stream beside the hash of the first, engine.cpp enqueue_blocks), with
     tampered and truncated blocks in both halves: every verdict and digest equals the one the
     same block gets in 64-block calls (the comb path, held to the oracle by the tests above)."""
@@ -255,18 +255,60 @@ def test_batch_call_in_two_halves_matches_small_calls(engine):
     base = MB.config4(engine, rounds=41)
     pks, stakes = MB.committee(engine, 100, distinct=True)
     engine.set_committee(pks, stakes, 0)
-    bins = list(base) + list(base)
-    for i in (10, 4200, 8100):  # stale digest
+    bins = list(base) + list(base) + list(base)[:100]
+    for i in (10, 4200, 8100, 8290):  # stale digest
         t = bytearray(bins[i])
         t[-20] ^= 0x10
         bins[i] = bytes(t)
     for i in (3000, 7000):  # truncated
         bins[i] = bins[i][: len(bins[i]) // 2]
     st, md, bd = engine.verify_blocks(bins)
-    assert st.shape == (8200,)
-    assert (st[[10, 4200, 8100]] == 2).all() and st[3000] != 0 and st[7000] != 0
-    for lo in list(range(0, 256, 64)) + list(range(4096, 4352, 64)) + list(range(7936, 8200, 64)) + [2944, 6976]:
+    assert st.shape == (8300,)
+    assert (st[[10, 4200, 8100, 8290]] == 2).all() and st[3000] != 0 and st[7000] != 0
+    for lo in list(range(0, 256, 64)) + list(range(4096, 4352, 64)) + list(range(7936, 8300, 64)) + [2944, 6976]:
         s2, m2, b2 = engine.verify_blocks(bins[lo:lo + 64])
         assert (s2 == st[lo:lo + 64]).all(), lo
         ok = s2 == 0
         assert (m2[ok] == md[lo:lo + 64][ok]).all() and (b2[ok] == bd[lo:lo + 64][ok]).all(), lo
+
+
+def test_two_pinned_callers_at_once(engine):
+    """Two callers, each with its own page-locked buffer (> the zero-copy size, so each chunk is
+    a candidate for the in-place DMA), submit at the same time: a merged pass must not DMA the
+    span between the two allocations; verdicts equal the pageable path's."""
+    import threading
+
+    import mysticeti_amd.blocks as MB
+
+    base = MB.config4(engine, rounds=3)
+    pks, stakes = MB.committee(engine, 100, distinct=True)
+    engine.set_committee(pks, stakes, 0)
+    bins = list(base)
+    t = bytearray(bins[77])
+    t[-5] ^= 1
+    bins[77] = bytes(t)
+    flat, off, ln = MB.pack(bins)
+    want = engine.verify_blocks_packed(flat, off, ln)
+    bufs = [engine.host_empty(flat.shape) for _ in range(2)]
+    try:
+        for b in bufs:
+            b[:] = flat
+        for _ in range(4):
+            res = [None, None]
+
+            def run(k):
+                res[k] = engine.verify_blocks_packed(bufs[k], off, ln)
+
+            th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            for r in res:
+                assert r is not None
+                for a, b in zip(r, want):
+                    assert (a == b).all()
+    finally:
+        for b in bufs:
+            engine.host_free(b)
+    assert int(want[0][77]) != 0 and (np.delete(want[0], 77) == 0).all()

@@ -124,6 +124,11 @@ def test_build_rs_compiles_the_product_sources():
 
     rs = _sources_of(BUILD_RS, r"const SOURCES: &\[&str\] = &\[(.*?)\];")
     assert rs == BP.SOURCES
+    # per-source flags: build.rs's SOURCE_FLAGS table equals build.py's
+    src = open(BUILD_RS).read()
+    tab = re.search(r"const SOURCE_FLAGS: [^=]*= &\[(.*?)\];\n", src, re.S).group(1)
+    got = {m.group(1): re.findall(r'"([^"]+)"', m.group(2)) for m in re.finditer(r'\("([^"]+)",\s*&\[(.*?)\]\)', tab)}
+    assert got == BP.SOURCE_FLAGS
 
 
 def test_library_from_build_rs_list_has_no_undefined_launchers():

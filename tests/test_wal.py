@@ -70,6 +70,26 @@ def test_layout_matches_writer():
         assert oend == lend == w.pos
 
 
+def test_bench_device_image_matches_host_image():
+    """bench_wal builds its WAL image in HBM from the distinct entries by contiguous runs; on
+    torch's CPU device it must give the host builder's bytes (map padding, cycle wraps)."""
+    import os
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench_wal
+
+    rng = np.random.default_rng(11)
+    for bits, k, n in ((12, 7, 200), (16, 13, 500), (14, 1, 90)):
+        payloads = [rng.integers(0, 256, size=int(rng.integers(1, 900)), dtype=np.uint8).tobytes() for _ in range(k)]
+        img, pos, lens, end = bench_wal.build_image(payloads, n, bits)
+        d_img, dpos, dlens, dend = bench_wal.build_image_device(payloads, n, bits, torch, torch.device("cpu"))
+        assert dend == end and dpos.tolist() == pos.tolist() and dlens.tolist() == lens.tolist()
+        assert bytes(d_img.numpy()) == bytes(img)
+
+
 def test_header_combine_split():
     """wal.rs:511-521: header = crc | len << 64 | tag << 96, little-endian."""
     for crc in (0, 1, 12, (1 << 64) - 1):

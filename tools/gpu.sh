@@ -1,0 +1,151 @@
+#!/bin/bash
+# One parameterised GPU driver for every measurement this repo takes on the box (replaces the
+# round-2/3 one-shot gpu_r0x*.sh scripts).
+#
+#   tools/gpu.sh TAG TASK [TASK ...]        -> gpurun_out/TAG/
+#
+# Tasks run in order; the first failure (or time limit) ends the script, nothing more touches
+# the GPU after it. Every GPU step runs under its own `timeout -k 10`.
+#
+#   tests[:K]        pytest -m gpu (K: a -k expression)
+#   smoke            __graft_entry__.smoke()
+#   bench            the driver's default line: bench.py --gpus 1 --steps 20 --warmup 5
+#   bench100         the default line at 100 steps (steady-state cross-check of `bench`)
+#   c2[:ARGS]        config-2 line only (no legs); ARGS (comma-separated) appended
+#   c4[:ARGS]        --workload config4 (2^21 blocks, 20 steps); ARGS appended
+#   c5               --workload config5
+#   wal              --workload wal
+#   gpus2            --gpus 2 rehearsal (both ranks on the one GPU)
+#   ab:V[:ARGS]      config-2 line, product library vs experiment build V (MV_LIB), 2 interleaved reps
+#   abc4:V[:ARGS]    the same on config 4
+#   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c4, c4s1, c5, wal}
+#   pmc:W[:KERNELS]  separate --pmc passes (one counter group per run) of W in {c2s1, c4s1, wal} and
+#                    tools/pmc_summary.py for each kernel (comma-separated)
+#   teardown         tools/teardown_probe.py plain, then under rocprofv3 hip + kernel + memory-copy
+#                    trace (/proc maps at exit); run it LAST in a call (it may end in a teardown fault)
+set -o pipefail
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+
+C2ONLY="--cpu-sample 0 --no-e2e --sustain-repeats 0 --no-adversarial --no-config4 --no-wal --no-config5"
+declare -A W=(
+  [c2]="python bench.py --steps 5 --warmup 1 $C2ONLY"
+  [c2s1]="python bench.py --steps 5 --warmup 1 --streams 1 $C2ONLY"
+  [c4]="python bench.py --workload config4 --steps 6 --warmup 4 --cpu-sample 0 --host-fed-blocks 0 --batch 1048576"
+  [c4s1]="python bench.py --workload config4 --steps 3 --warmup 1 --cpu-sample 0 --streams 1 --host-fed-blocks 0 --batch 1048576"
+  [c5]="python bench.py --workload config5 --cpu-sample 0 --batches 1000 --conc-seconds 0.3"
+  [wal]="python bench.py --workload wal --steps 3 --warmup 1 --cpu-sample 0"
+)
+PMC_GROUPS=(
+  "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+  "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS"
+  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LEVEL_WAVES"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+)
+
+run() {  # run <seconds> <log> <cmd...>: stop the script on failure
+  local t=$1 log=$2
+  shift 2
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "FAILED rc=$rc: $*"
+    tail -8 "$log"
+    exit 1
+  fi
+}
+line() {  # line <json>: one-line digest of a bench JSON
+  python3 tools/line_digest.py "$1"
+}
+
+for T in "$@"; do
+  name=${T%%:*}
+  arg=""
+  [ "$T" != "$name" ] && arg=${T#*:}
+  case $name in
+    tests)
+      K=()
+      [ -n "$arg" ] && K=(-k "$arg")
+      run 900 "$OUT/pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${K[@]}"
+      tail -1 "$OUT/pytest_gpu.log" ;;
+    smoke)
+      run 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"
+      tail -1 "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench FAILED"; tail -8 "$OUT/bench.err"; exit 1; }
+      line "$OUT/bench.json" ;;
+    bench100)
+      timeout -k 10 900 python bench.py --steps 100 --warmup 5 > "$OUT/bench100.json" 2> "$OUT/bench100.err" || { echo "bench100 FAILED"; tail -8 "$OUT/bench100.err"; exit 1; }
+      line "$OUT/bench100.json" ;;
+    c2)
+      timeout -k 10 300 python bench.py --steps 600 --warmup 10 $C2ONLY ${arg//,/ } > "$OUT/c2.json" 2> "$OUT/c2.err" || { echo "c2 FAILED"; tail -8 "$OUT/c2.err"; exit 1; }
+      line "$OUT/c2.json" ;;
+    c4)
+      timeout -k 10 600 python bench.py --workload config4 --steps 20 --warmup 5 --cpu-sample 0 ${arg//,/ } > "$OUT/c4.json" 2> "$OUT/c4.err" || { echo "c4 FAILED"; tail -8 "$OUT/c4.err"; exit 1; }
+      line "$OUT/c4.json" ;;
+    c5)
+      timeout -k 10 600 python bench.py --workload config5 --cpu-sample 0 --batches 2000 --conc-seconds 2 ${arg//,/ } > "$OUT/c5.json" 2> "$OUT/c5.err" || { echo "c5 FAILED"; tail -8 "$OUT/c5.err"; exit 1; }
+      line "$OUT/c5.json" ;;
+    wal)
+      timeout -k 10 600 python bench.py --workload wal --steps 20 --warmup 2 --cpu-sample 0 > "$OUT/wal.json" 2> "$OUT/wal.err" || { echo "wal FAILED"; tail -8 "$OUT/wal.err"; exit 1; }
+      line "$OUT/wal.json" ;;
+    gpus2)
+      timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 --no-config5 --host-fed-blocks 0 --cpu-sample 0 --no-e2e --sustain-repeats 1 > "$OUT/gpus2.json" 2> "$OUT/gpus2.err" || { echo "gpus2 FAILED"; tail -8 "$OUT/gpus2.err"; exit 1; }
+      line "$OUT/gpus2.json" ;;
+    ab|abc4)
+      V=${arg%%:*}
+      A=""
+      [ "$arg" != "$V" ] && A=${arg#*:}
+      L=$GRAFT_REPO_ROOT/mysticeti_amd/_build/$V/libmysti_verify.so
+      [ -f "$L" ] || { echo "no variant build $L"; exit 1; }
+      for rep in 1 2; do
+        for lib in product "$V"; do
+          if [ $lib = product ]; then ML=""; else ML=$L; fi
+          if [ $name = ab ]; then
+            CMD="python bench.py --steps 600 --warmup 10 $C2ONLY ${A//,/ }"
+          else
+            CMD="python bench.py --workload config4 --steps 20 --warmup 5 --cpu-sample 0 --host-fed-blocks 0 ${A//,/ }"
+          fi
+          MV_LIB=$ML timeout -k 10 400 $CMD > "$OUT/${name}_${lib}_$rep.json" 2> "$OUT/${name}_${lib}_$rep.err" || { echo "$name $lib FAILED"; tail -8 "$OUT/${name}_${lib}_$rep.err"; exit 1; }
+          echo -n "rep $rep $lib: "
+          line "$OUT/${name}_${lib}_$rep.json"
+        done
+      done ;;
+    trace)
+      cmd=${W[$arg]}
+      [ -n "$cmd" ] || { echo "unknown workload $arg"; exit 1; }
+      run 400 "$OUT/trace_$arg.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$arg" -o run -- $cmd
+      python3 tools/trace_top.py "$OUT/trace_$arg" ;;
+    pmc)
+      wl=${arg%%:*}
+      ks=""
+      [ "$arg" != "$wl" ] && ks=${arg#*:}
+      cmd=${W[$wl]}
+      [ -n "$cmd" ] || { echo "unknown workload $wl"; exit 1; }
+      mkdir -p "$OUT/pmc_$wl"
+      run 400 "$OUT/pmc_$wl/trace.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_$wl/trace1" -o run -- $cmd
+      i=0
+      for group in "${PMC_GROUPS[@]}"; do
+        i=$((i + 1))
+        run 200 "$OUT/pmc_$wl/pmc$i.log" timeout -s KILL 190 rocprofv3 --pmc $group --output-format csv -d "$OUT/pmc_$wl/pmc$i" -o run -- $cmd
+      done
+      for k in ${ks//,/ }; do
+        python3 tools/pmc_summary.py "$OUT/pmc_$wl" "$k" --json "$OUT/pmc_${wl}_$k.json" > "$OUT/pmc_${wl}_$k.txt" || true
+        grep -E "valu_issue|WAIT_INST|clock|fetch_GB|write_GB|kernel_avg|LDS_BANK" "$OUT/pmc_${wl}_$k.txt" | sed "s/^/$k /"
+      done ;;
+    teardown)
+      run 300 "$OUT/teardown_plain.log" python tools/teardown_probe.py "$OUT/maps_plain.txt"
+      echo "plain: ok"
+      timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/teardown_prof" -o run -f csv -- python tools/teardown_probe.py "$OUT/maps_prof.txt" > "$OUT/teardown_prof.log" 2>&1
+      echo "under rocprofv3: rc=$?"
+      tail -25 "$OUT/teardown_prof.log" ;;
+    *)
+      echo "unknown task $T"
+      exit 1 ;;
+  esac
+done
+echo "gpu.sh $TAG done"
