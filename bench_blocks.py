@@ -206,7 +206,10 @@ def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None
         packed = MB.pack(blocks[:nb])
         res = {"bincode_bytes_per_block": int(packed[2].mean())}
         _drive(drv, 0, mv_fn, eng.ctx, packed, 64, 1, max_calls=max(8, nb // 64))  # warm-up
+        o0 = eng.online_stats()
         res["gpu"], g = _drive(drv, 0, mv_fn, eng.ctx, packed, 64, 1, max_calls=batches)
+        o1 = eng.online_stats()
+        res["gpu"]["online_requests"], res["gpu"]["online_launches"] = o1[0] - o0[0], o1[1] - o0[1]
         ok &= g
         comm = _Committee(olib, pks, stakes) if olib is not None else None
         if comm is not None:
@@ -220,10 +223,13 @@ def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None
                                            for k in ("cpu_1t", f"cpu_{threads}t")}
         # concurrent 1-block callers
         conc = {"callers": callers, "seconds": conc_seconds}
-        q0 = eng.queue_stats()
+        q0, o0 = eng.queue_stats(), eng.online_stats()
         conc["gpu"], g = _drive(drv, 0, mv_fn, eng.ctx, packed, 1, callers, seconds=conc_seconds)
-        q1 = eng.queue_stats()
-        conc["gpu"]["calls_per_device_pass"] = round((q1[0] - q0[0]) / max(1, q1[1] - q0[1]), 2)
+        q1, o1 = eng.queue_stats(), eng.online_stats()
+        conc["gpu"]["queue_calls"] = q1[0] - q0[0]
+        if q1[1] > q0[1]:
+            conc["gpu"]["calls_per_device_pass"] = round((q1[0] - q0[0]) / (q1[1] - q0[1]), 2)
+        conc["gpu"]["online_requests"], conc["gpu"]["online_launches"] = o1[0] - o0[0], o1[1] - o0[1]
         ok &= g
         if comm is not None:
             conc["cpu_own_core"], c = _drive(drv, 1, comm.fn, comm.ptr, packed, 1, callers, inner_threads=1,

@@ -90,6 +90,8 @@ typedef int32_t mv_status;
 #define MV_FLAG_NO_BATCH 1u /* host-buffer verify: never use the batch (random linear combination) path */
 #define MV_FLAG_NO_COMB 2u  /* committee-key verifies: never use the per-key comb tables (ladder per signature) */
 #define MV_FLAG_HOST_PARSE 4u /* mv_verify_blocks: parse the bincode on the host (block_codec.cpp), not on the GPU */
+#define MV_FLAG_NO_ONLINE 8u  /* mv_verify_blocks: never use the resident online service (every call goes
+                                 through the submission queue and launches its own kernels) */
 
 /* Host-buffer verify calls of at least this many signatures per device take the batch path
  * (one combined equation + exact fallback); smaller ones verify every signature alone. */
@@ -151,6 +153,17 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
 
 /* Submission-queue counters: mv_verify_blocks calls, and device passes that served them. */
 mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes);
+
+/* The resident online service (replaces the per-call device pass for the one-task-per-peer
+ * traffic of NetworkSyncer, net_sync.rs:214-221 / synchronizer.rs:146-164): mv_verify_blocks
+ * calls of <= 64 short blocks (< 2 KB each on average) are posted to a ring in page-locked
+ * memory that a kernel resident on a CU-masked stream polls; the caller's thread spins on its
+ * request's done word (no launch, no event, no wake-up per call). The kernel exits after
+ * MV_ONLINE_IDLE_US (default 2,000) without work and is relaunched by the next call; calls it
+ * does not take (larger, long blocks, MV_FLAG_NO_ONLINE) go through the submission queue.
+ * Verdicts and digests are those of the queue path. Counters: requests served by the service
+ * and kernel launches it needed, summed over the context's devices. */
+mv_status mv_online_stats(mv_ctx* ctx, uint64_t* requests, uint64_t* launches);
 
 /* Host-only helper (no device needed): the shard plan of the multi-device paths -- cut[0..parts]
  * splits items [0, n) into contiguous shards of about equal total weight (block calls weigh a

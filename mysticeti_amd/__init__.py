@@ -47,14 +47,14 @@ EXPORTS = [
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
     "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
     "mv_queue_stats", "mv_shard_plan", "mv_crc32", "mv_wal_verify", "mv_wal_layout", "mv_dev_wal_verify",
-    "mv_dev_crc32", "mv_host_alloc", "mv_host_free",
+    "mv_dev_crc32", "mv_host_alloc", "mv_host_free", "mv_online_stats",
 ]
 WAL_OK, WAL_CRC_MISMATCH, WAL_NONZERO_CRC_LEN0, WAL_BAD_LENGTH = range(4)
 WAL_MAP_BITS, WAL_MAP_BITS_TEST = 24, 16  # wal.rs:95-103
 # batch path stages, the block pipeline's, the WAL replay's (mv_stage_times order, MV_NSTAGES)
 STAGES = ["prep", "sort", "bucket", "reduce", "final", "fallback", "parse", "hash", "verify", "verdict", "wal_walk",
           "wal_crc"]
-FLAG_NO_BATCH, FLAG_NO_COMB, FLAG_HOST_PARSE = 1, 2, 4
+FLAG_NO_BATCH, FLAG_NO_COMB, FLAG_HOST_PARSE, FLAG_NO_ONLINE = 1, 2, 4, 8
 BATCH_MIN = 4096
 
 
@@ -96,6 +96,7 @@ def load_library(path: str = LIB_PATH):
     lib.mv_batch_counters.argtypes = [vp, vp]
     lib.mv_set_batch_groups.argtypes = [vp, u32]
     lib.mv_queue_stats.argtypes = [vp, vp, vp]
+    lib.mv_online_stats.argtypes = [vp, vp, vp]
     lib.mv_shard_plan.argtypes = [vp, u64, u32, vp]
     lib.mv_set_stage_timing.argtypes = [vp, ctypes.c_int]
     lib.mv_stage_times.argtypes = [vp, vp, vp, ctypes.c_int]
@@ -132,17 +133,20 @@ class Engine:
     """One mv_ctx: the devices it shards over, their streams and buffers."""
 
     def __init__(self, devices: Sequence[int] = (0,), max_batch: int = 0, batch: bool = True, comb: bool = True,
-                 host_parse: bool = False, shards_per_device: int = 1):
+                 host_parse: bool = False, shards_per_device: int = 1, online: bool = True):
         """batch=False sets MV_FLAG_NO_BATCH: host-buffer verifies check every signature alone.
         comb=False sets MV_FLAG_NO_COMB: committee keys go through the per-signature ladder,
         not the per-key comb tables. host_parse=True sets MV_FLAG_HOST_PARSE: verify_blocks
         parses the bincode on the host instead of on the GPU. shards_per_device > 1 makes
-        that many logical shards per device (host calls shard across them as across GPUs)."""
+        that many logical shards per device (host calls shard across them as across GPUs).
+        online=False sets MV_FLAG_NO_ONLINE: small verify_blocks calls skip the resident online
+        service and go through the submission queue."""
         self.lib = load_library()
         mask = 0
         for d in devices:
             mask |= 1 << int(d)
-        flags = (0 if batch else FLAG_NO_BATCH) | (0 if comb else FLAG_NO_COMB) | (FLAG_HOST_PARSE if host_parse else 0)
+        flags = (0 if batch else FLAG_NO_BATCH) | (0 if comb else FLAG_NO_COMB) | (FLAG_HOST_PARSE if host_parse else 0) \
+            | (0 if online else FLAG_NO_ONLINE)
         cfg = _Config(mask, max_batch, flags, shards_per_device)
         h = ctypes.c_void_p()
         rc = self.lib.mv_create(ctypes.byref(cfg), ctypes.byref(h))
@@ -297,6 +301,12 @@ class Engine:
         c, p = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.lib.mv_queue_stats(self.ctx, ctypes.byref(c), ctypes.byref(p)), "mv_queue_stats")
         return c.value, p.value
+
+    def online_stats(self) -> Tuple[int, int]:
+        """(verify_blocks calls served by the resident online service, its kernel launches)."""
+        r, l = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.mv_online_stats(self.ctx, ctypes.byref(r), ctypes.byref(l)), "mv_online_stats")
+        return r.value, l.value
 
     def set_stage_timing(self, enable: bool = True):
         self._check(self.lib.mv_set_stage_timing(self.ctx, 1 if enable else 0), "mv_set_stage_timing")

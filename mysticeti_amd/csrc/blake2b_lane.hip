@@ -77,6 +77,12 @@ MV_DEV void compress(uint64_t (&h)[8], const uint64_t (&m)[16], uint64_t t, bool
 // Block b of the string at p, zero past lim; a word is read only when it starts below lim (the
 // strings are 8-aligned and readable up to round-up(lim, 8), as for the quad form).
 MV_DEV void load_block(uint64_t (&m)[16], const uint8_t* p, uint64_t b, uint64_t lim) {
+#ifdef MV_B2L_NOLOAD  // experiment (tools/gpu.sh abc4): message words made in registers, no loads
+  const uint64_t x = reinterpret_cast<uint64_t>(p) ^ (b * 0x9e3779b97f4a7c15ull);
+#pragma unroll
+  for (int j = 0; j < 16; j++) m[j] = x + (uint64_t)j * 0x100000001ull + lim;
+  return;
+#endif
   const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + b * 16;
   const uint64_t base = b * 128;
   if (base + 128 <= lim) {

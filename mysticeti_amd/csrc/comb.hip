@@ -312,24 +312,21 @@ constexpr uint32_t C16_SIGS = 4;    // signatures per k_verify_comb16 workgroup
 constexpr uint32_t C16_TROLES = 8;  // table-sum roles: four over the B rows, four over the A rows
 // + one spare wave, which only ingests (with the other three) when the kernel parses its blocks
 constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS + 64;
-__global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* sig,  // not restrict: the ingest phase writes it
-                                                               const uint8_t* __restrict__ pk,
-                                                               const uint32_t* key_idx,  // likewise
-                                                               uint32_t n,
-                                                               const uint4* __restrict__ combB,
-                                                               const uint4* __restrict__ combA,
-                                                               const uint8_t* __restrict__ key_ok,
-                                                               uint8_t* __restrict__ status,
-                                                               const mvk::BlockVerdictOut bv,
-                                                               const mvk::BlockHashIn hin,
-                                                               const mvk::BlockIngestIn ing) {
+// One workgroup's share (signatures 4 wg .. 4 wg + 3) of the short-chain comb verify: the body
+// of k_verify_comb16, also run job by job by the resident online service (k_online below).
+// Every wave meets exactly three barriers.
+MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const uint8_t* __restrict__ pk,
+                      const uint32_t* key_idx, uint32_t n, const uint4* __restrict__ combB,
+                      const uint4* __restrict__ combA, const uint8_t* __restrict__ key_ok,
+                      uint8_t* __restrict__ status, const mvk::BlockVerdictOut& bv, const mvk::BlockHashIn& hin,
+                      const mvk::BlockIngestIn& ing) {
   __shared__ uint32_t part[C16_TROLES][C16_SIGS][36];  // table roles' sums, coordinate c at words 9c..
   constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);       // table rows per role
   const uint32_t t = threadIdx.x;
   static_assert(C16_THREADS == 4 * 64 && C16_SIGS == 4, "one ingest wave per block of the workgroup");
   if (ing.buf) {  // barrier 0: wave w parses block 4 b + w (ingest_dev.h) before anything reads it
     __shared__ IngestLds igl[C16_SIGS];
-    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), bi = blockIdx.x * C16_SIGS + w;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), bi = wg * C16_SIGS + w;
     const CommitteeView cv{ing.stakes, ing.n_auth, ing.epoch, ing.quorum_thr};
     const IngestOut io{ing.stage, ing.pre_off, ing.pre_len, ing.sig, ing.key_idx, ing.facts, ing.claimed};
     if (bi < n) ingest_block<true>(bi, ing.buf, ing.off, ing.len, cv, io, igl[w]);
@@ -344,7 +341,7 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
   const bool row_role = t < 16 * C16_SIGS;
   const uint32_t role = row_role ? 0u : 1u + (t - 16 * C16_SIGS) / (4 * C16_SIGS);
   const uint32_t sq = row_role ? t >> 4 : (t >> 2) & (C16_SIGS - 1), c = t & 3u;
-  const uint32_t gid = blockIdx.x * C16_SIGS + sq;
+  const uint32_t gid = wg * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
   fe v;  // coordinate c of this role's point
@@ -376,7 +373,7 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
       if (hin.stage) {
         // the block path's two digests of this workgroup's blocks first (one quad per block,
         // quads 0 .. C16_SIGS - 1 of the A wave): M = msg digest feeds the challenge below
-        b2q::quad_hash_range<true, 1, true, true>(blockIdx.x * C16_SIGS, C16_SIGS, hin.stage, hin.pre_off,
+        b2q::quad_hash_range<true, 1, true, true>(wg * C16_SIGS, C16_SIGS, hin.stage, hin.pre_off,
                                                    hin.pre_len, n, hin.msg_digest, hin.digest);
         __threadfence();  // the digests are read back below (other lanes) and by role 0's verdict
       }
@@ -434,6 +431,212 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
     const bool ident = (b0 & 1u) && (b1 & 2u);
     if ((t & 15u) == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
   }
+}
+
+__global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* msg, const uint8_t* sig,  // not restrict: the ingest phase writes it
+                                                               const uint8_t* __restrict__ pk,
+                                                               const uint32_t* key_idx,  // likewise
+                                                               uint32_t n,
+                                                               const uint4* __restrict__ combB,
+                                                               const uint4* __restrict__ combA,
+                                                               const uint8_t* __restrict__ key_ok,
+                                                               uint8_t* __restrict__ status,
+                                                               const mvk::BlockVerdictOut bv,
+                                                               const mvk::BlockHashIn hin,
+                                                               const mvk::BlockIngestIn ing) {
+  comb16_wg(blockIdx.x, msg, sig, pk, key_idx, n, combB, combA, key_ok, status, bv, hin, ing);
+}
+
+// The resident online service (kernels.h OnlineReq / OnlineCtl / OnlineDev). Every branch
+// around a barrier is uniform (the role is the workgroup's, the decision is broadcast through
+// LDS), and every exit test is made on each idle iteration, so all waves leave together.
+constexpr uint32_t ON_DW = sizeof(mvk::OnlineReq) / 4;
+static_assert(ON_DW <= C16_THREADS && sizeof(mvk::OnlineReq) % 16 == 0, "one dword per thread");
+constexpr uint32_t ON_BATCH = 32;  // requests the poller moves per pass
+
+MV_DEV uint64_t on_now() { return (uint64_t)wall_clock64(); }
+
+// Workgroup 0: moves published requests from page-locked memory into HBM and advances ready.
+MV_DEV void online_poller(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs, mvk::OnlineDev* dev, uint64_t idle_ticks,
+                          uint64_t max_ticks) {
+  __shared__ uint32_t sh[4];                // kind (0 idle, 1 move, 2 exit), first request lo / hi, count
+  __shared__ uint32_t pre[ON_BATCH + 1];    // 16-B chunk prefix over the batch's inputs
+  const uint32_t t = threadIdx.x;
+  const uint64_t t_start = on_now();
+  for (;;) {
+    if (t < 64) {  // wave 0: how many consecutive requests from `ready` are published
+      uint32_t kind = 0, cnt = 0;
+      const uint64_t rdy = __hip_atomic_load(&dev->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t tail = __hip_atomic_load(&ctl->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t avail = tail > rdy ? tail - rdy : 0;
+      const uint64_t m = avail < ON_BATCH ? avail : ON_BATCH;
+      bool ok = false;
+      if (t < m) {
+        const uint64_t q = rdy + t;
+        ok = __hip_atomic_load(&reqs[q % mvk::ONLINE_SLOTS].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
+      }
+      const uint64_t notok = __ballot(!ok);  // lanes >= m count as not ready
+      cnt = notok ? (uint32_t)__builtin_ctzll(notok) : 64u;
+      if (cnt > m) cnt = (uint32_t)m;
+      const uint64_t now = on_now();
+      if (cnt) {
+        kind = 1;
+      } else if (__hip_atomic_load(&dev->live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 ||
+                 now - t_start > max_ticks + idle_ticks) {
+        kind = 2;  // every worker has left (or a worker-less launch outlived its limits)
+      }
+      if (t == 0) {
+        sh[0] = kind;
+        sh[1] = (uint32_t)rdy;
+        sh[2] = (uint32_t)(rdy >> 32);
+        sh[3] = cnt;
+      }
+    }
+    __syncthreads();
+    const uint32_t kind = sh[0], cnt = sh[3];
+    const uint64_t rdy = (uint64_t)sh[1] | ((uint64_t)sh[2] << 32);
+    __syncthreads();
+    if (kind == 2) return;
+    if (kind == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    // descriptors: dword w of request i by thread i * ON_DW + w
+    for (uint32_t x = t; x < cnt * ON_DW; x += blockDim.x) {
+      const uint32_t i = x / ON_DW, w = x % ON_DW, slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS);
+      reinterpret_cast<uint32_t*>(&dev->desc[slot])[w] = reinterpret_cast<const uint32_t*>(&reqs[slot])[w];
+    }
+    __syncthreads();  // the HBM descriptors are read back below (workgroup scope)
+    if (t == 0) {
+      uint32_t c = 0;
+      for (uint32_t i = 0; i < cnt; i++) {
+        pre[i] = c;
+        c += (dev->desc[(rdy + i) % mvk::ONLINE_SLOTS].copy_bytes + 15) / 16;
+      }
+      pre[cnt] = c;
+    }
+    __syncthreads();
+    // inputs: 16-byte chunk k of the batch by thread k (mod the workgroup), all independent
+    const uint32_t total = pre[cnt];
+    for (uint32_t k = t; k < total; k += blockDim.x) {
+      uint32_t i = 0;
+      while (pre[i + 1] <= k) i++;
+      const mvk::OnlineReq& d = dev->desc[(rdy + i) % mvk::ONLINE_SLOTS];
+      const uint32_t c = k - pre[i];
+      reinterpret_cast<uint4*>(d.in_dev)[c] = reinterpret_cast<const uint4*>(d.in_host)[c];
+    }
+    __threadfence();  // the copies before ready (agent scope)
+    __syncthreads();
+    if (t == 0) {
+      for (uint32_t i = 0; i < cnt; i++) {
+        const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS);
+        dev->nj[slot] = (dev->desc[slot].n + C16_SIGS - 1) / C16_SIGS;
+      }
+      __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + cnt), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Workgroups 1..: claim a job from the ticket, run it from HBM, hand its outputs to the host.
+MV_DEV void online_worker(mvk::OnlineCtl* ctl, mvk::OnlineDev* dev, const uint4* __restrict__ combB,
+                          const uint4* __restrict__ combA, const uint8_t* __restrict__ key_ok,
+                          const uint8_t* __restrict__ pk, uint64_t idle_ticks, uint64_t max_ticks) {
+  constexpr uint32_t JB = mvk::ONLINE_JOB_BITS, JM = (1u << JB) - 1u;
+  __shared__ uint32_t job[4];  // kind (0 idle, 1 work, 2 exit), request lo / hi, job
+  __shared__ uint32_t dsc[ON_DW];
+  const uint32_t t = threadIdx.x;
+  const uint64_t t_start = on_now();
+  uint64_t t_busy = t_start;
+  for (;;) {
+    if (t == 0) {
+      uint32_t kind = 0, j = 0;
+      uint64_t q = 0;
+      for (int tries = 0; tries < 256; tries++) {
+        unsigned long long cur = __hip_atomic_load(&dev->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        q = cur >> JB;
+        j = (uint32_t)(cur & JM);
+        if (q >= __hip_atomic_load(&dev->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) break;
+        const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
+        const uint32_t nj = dev->nj[slot];
+        const unsigned long long next = j + 1 < nj ? cur + 1 : (unsigned long long)(q + 1) << JB;
+        if (__hip_atomic_compare_exchange_strong(&dev->ticket, &cur, next, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          if (nj == 0) {  // a void request: complete it here
+            __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+          }
+          kind = 1;
+          break;
+        }
+      }
+      const uint64_t now = on_now();
+      if (kind == 1) {
+        t_busy = now;
+      } else if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                 now - t_busy > idle_ticks || now - t_start > max_ticks) {
+        kind = 2;
+      }
+      job[0] = kind;
+      job[1] = (uint32_t)q;
+      job[2] = (uint32_t)(q >> 32);
+      job[3] = j;
+    }
+    __syncthreads();
+    const uint32_t kind = job[0];
+    const uint64_t q = (uint64_t)job[1] | ((uint64_t)job[2] << 32);
+    const uint32_t j = job[3];
+    if (kind == 1 && t < ON_DW)  // the HBM descriptor into LDS, then into scalar registers
+      dsc[t] = reinterpret_cast<const uint32_t*>(&dev->desc[q % mvk::ONLINE_SLOTS])[t];
+    __syncthreads();  // also: job[] is rewritten by the next claim only after every wave read it
+    if (kind == 2) {
+      if (t == 0) __hip_atomic_fetch_sub(&dev->live, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (kind == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    mvk::OnlineReq d;
+    uint32_t* dw = reinterpret_cast<uint32_t*>(&d);
+#pragma unroll
+    for (uint32_t k = 0; k < ON_DW; k++) dw[k] = __builtin_amdgcn_readfirstlane(dsc[k]);
+    const uint32_t ju = __builtin_amdgcn_readfirstlane(j);
+    comb16_wg(ju, d.msg, d.sig, pk, d.key_idx, d.n, combB, combA, key_ok, d.sst, d.bv, d.hin, d.ing);
+    __syncthreads();  // the job's digests and verdicts are in HBM (workgroup scope)
+    // this job's blocks: md and bd (8 words each), status -> page-locked output
+    const uint32_t b0 = ju * C16_SIGS, nb = d.n - b0 < C16_SIGS ? d.n - b0 : C16_SIGS;
+    if (t < 16 * nb) {
+      const uint32_t b = b0 + t / 16, w = t % 16;  // words 0..7 md, 8..15 bd
+      const size_t o = w < 8 ? 32 * (size_t)b + 4 * w : 32 * ((size_t)mvk::ONLINE_MAX_BLOCKS + b) + 4 * (w - 8);
+      *reinterpret_cast<uint32_t*>(d.out_host + o) = *reinterpret_cast<const uint32_t*>(d.out_dev + o);
+    } else if (t >= 64 && t < 64 + nb) {
+      const size_t o = 64 * (size_t)mvk::ONLINE_MAX_BLOCKS + b0 + (t - 64);
+      d.out_host[o] = d.out_dev[o];
+    }
+    __threadfence_system();  // the outputs before the done word
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
+      const uint32_t nj = (d.n + C16_SIGS - 1) / C16_SIGS;
+      const uint32_t prev = __hip_atomic_fetch_add(&dev->jobs_done[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev + 1 == nj) {
+        __hip_atomic_store(&dev->jobs_done[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(C16_THREADS) k_online(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs,
+                                                        mvk::OnlineDev* dev, const uint4* __restrict__ combB,
+                                                        const uint4* __restrict__ combA,
+                                                        const uint8_t* __restrict__ key_ok,
+                                                        const uint8_t* __restrict__ pk, uint64_t idle_ticks,
+                                                        uint64_t max_ticks) {
+  if (blockIdx.x == 0)
+    online_poller(ctl, reqs, dev, idle_ticks, max_ticks);
+  else
+    online_worker(ctl, dev, combB, combA, key_ok, pk, idle_ticks, max_ticks);
 }
 
 // The same predicate split in two, for small batches of long blocks (config 5, 8-KB
@@ -633,6 +836,17 @@ hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint
   else
     hipLaunchKernelGGL(mv::k_verify_comb, dim3((n + 63) / 64), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)combB, (const uint4*)combA, key_ok, status, bv ? *bv : none);
+  return hipGetLastError();
+}
+
+hipError_t launch_online(OnlineCtl* ctl, const OnlineReq* reqs, OnlineDev* dev, uint32_t grid, const void* combB,
+                         const void* combA, const uint8_t* key_ok, const uint8_t* pk, uint64_t idle_ticks,
+                         uint64_t max_ticks, hipStream_t s) {
+  if (grid < 2) return hipErrorInvalidValue;  // a poller and at least one worker
+  hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&dev->live), (int)(grid - 1), 1, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mv::k_online, dim3(grid), dim3(mv::C16_THREADS), 0, s, ctl, reqs, dev, (const uint4*)combB,
+                     (const uint4*)combA, key_ok, pk, idle_ticks, max_ticks);
   return hipGetLastError();
 }
 

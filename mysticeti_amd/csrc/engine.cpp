@@ -16,7 +16,9 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -80,6 +82,8 @@ struct HostBuf {
     return static_cast<T*>(p);
   }
 };
+
+struct OnlineSvc;
 
 struct Device {
   int id = 0;
@@ -160,6 +164,8 @@ struct Device {
   DevBuf wal_tab, wal_rec, wal_mcount, wal_mflag, wal_moff, wal_ent, wal_ff, wal_img, wal_pos, wal_tag, wal_len,
       wal_st;
   int cus = 0;
+  // the resident online service (k_online) of this device, made on first use
+  std::shared_ptr<OnlineSvc> online;
 };
 
 struct PendingEvents {
@@ -211,6 +217,10 @@ struct mv_ctx {
   bool q_lingering = false;
   size_t q_last_calls = 0;
   std::atomic<uint64_t> q_calls{0}, q_passes{0};
+  // online requests hold it shared for their whole life; mv_set_committee and mv_destroy take it
+  // exclusively (the resident kernel reads the committee's tables)
+  std::shared_mutex com_mu;
+  std::atomic<uint64_t> online_rr{0};
 };
 
 struct mv_ctx::BlockReq {
@@ -984,6 +994,289 @@ bool committee_ready(mv_ctx* ctx) {
   return true;
 }
 
+// ---- the resident online service (kernels.h k_online) -------------------------------------
+// One per device, made on the first eligible request. Page-locked coherent host memory holds
+// the control words, the request ring and each slot's bincode in / outputs out (the kernel
+// reads and writes them over PCIe, as the launched online path does); device memory holds the
+// ticket and each slot's ingest scratch. The kernel runs on its own stream, created with a CU
+// mask (a queue of its own, so kernels on other streams never wait behind it; and a bounded
+// share of the chip), and exits after MV_ONLINE_IDLE_US (default 2,000) without a job.
+constexpr uint32_t kOnSlots = mvk::ONLINE_SLOTS, kOnMax = mvk::ONLINE_MAX_BLOCKS;
+constexpr size_t kOnInCap = 128u << 10;                         // bincode bytes per request
+constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t kOnInStride = al256(16 * kOnMax + kOnInCap + 64);  // off[n] | len[n] | bincode | 16 zero B
+constexpr size_t kOnOutStride = al256(65 * kOnMax);                 // md[64] | bd[64] | status[64]
+constexpr size_t kOnStage = al256(kOnInCap + 4096);
+constexpr size_t kOnScrStride = kOnInStride + kOnOutStride + kOnStage + 2 * al256(8 * kOnMax) + al256(64 * kOnMax) +
+                                2 * al256(4 * kOnMax) + al256(32 * kOnMax) + al256(kOnMax);
+
+struct OnlineSvc {
+  std::mutex mu;
+  bool ready = false, failed = false, launched = false;
+  hipStream_t stream = nullptr;
+  hipEvent_t exited = nullptr;
+  mvk::OnlineCtl* ctl = nullptr;  // host view (pinned, coherent)
+  mvk::OnlineReq* req = nullptr;
+  uint8_t* in = nullptr;
+  uint8_t* out = nullptr;
+  void *ctl_d = nullptr, *req_d = nullptr, *in_d = nullptr, *out_d = nullptr;  // device views
+  DevBuf dctl, scr;
+  std::unique_ptr<std::atomic<uint64_t>[]> freed;  // slot released by its owner: request + 1
+  uint64_t next_q = 0;
+  uint32_t grid = 0;
+  std::atomic<uint64_t> requests{0}, launches{0};
+  // steady_clock ns of the last request seen done: a kernel that finished a request less than
+  // half its idle limit ago is still live (no runtime query on the request path)
+  std::atomic<int64_t> last_done_ns{0};
+  uint64_t idle_us = 2000;
+};
+
+int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+bool online_enabled_env() {
+  const char* e = getenv("MV_ONLINE");  // read per call: the tests switch it in-process
+  return !(e && e[0] == '0');
+}
+
+// Whether a request of n blocks, `bytes` of 8-aligned bincode, takes the online service: the
+// calls enqueue_blocks would run as one k_verify_comb16 launch (short blocks, the ingest and
+// hash folded in), small enough for one ring slot.
+bool online_eligible(mv_ctx* ctx, uint32_t n, uint64_t bytes) {
+  if ((ctx->flags & (MV_FLAG_NO_ONLINE | MV_FLAG_NO_COMB | MV_FLAG_HOST_PARSE)) || !online_enabled_env()) return false;
+  if (n == 0 || n > kOnMax || bytes > kOnInCap) return false;
+  const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
+  const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
+  const uint64_t buf_bytes = (bytes + 16 + 15) & ~15ull;
+  if (split_bytes && buf_bytes >= split_bytes * (uint64_t)n) return false;
+  const char* fe = getenv("MV_BLK_FUSED");
+  const char* hce = getenv("MV_HASH_IN_COMB");
+  const char* ice = getenv("MV_INGEST_IN_COMB");
+  if ((fe && fe[0] == '1') || (hce && hce[0] == '0') || (ice && ice[0] == '0')) return false;
+  return mvk::comb_short_chain(n);
+}
+
+// Allocations and the stream (o.mu held).
+mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
+  if (o.ready) return MV_OK;
+  HIPCHK(ctx, hipSetDevice(dev.id));
+  const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+  auto host = [&](void** h, void** d, size_t bytes) -> hipError_t {
+    hipError_t e = hipHostMalloc(h, bytes, fl);
+    if (e != hipSuccess) return e;
+    memset(*h, 0, bytes);
+    return hipHostGetDevicePointer(d, *h, 0);
+  };
+  HIPCHK(ctx, host((void**)&o.ctl, &o.ctl_d, sizeof(mvk::OnlineCtl)));
+  HIPCHK(ctx, host((void**)&o.req, &o.req_d, sizeof(mvk::OnlineReq) * kOnSlots));
+  HIPCHK(ctx, host((void**)&o.in, &o.in_d, kOnInStride * kOnSlots));
+  HIPCHK(ctx, host((void**)&o.out, &o.out_d, kOnOutStride * kOnSlots));
+  HIPCHK(ctx, o.dctl.ensure(sizeof(mvk::OnlineDev)));
+  HIPCHK(ctx, hipMemset(o.dctl.p, 0, sizeof(mvk::OnlineDev)));
+  HIPCHK(ctx, o.scr.ensure(kOnScrStride * kOnSlots));
+  o.freed.reset(new std::atomic<uint64_t>[kOnSlots]);
+  for (uint32_t k = 0; k < kOnSlots; k++) o.freed[k].store(0);
+  // CU mask: MV_ONLINE_CUS (default 64) CUs spread evenly over the chip; 0 = an ordinary stream
+  int cus = 0;
+  HIPCHK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev.id));
+  const char* ce = getenv("MV_ONLINE_CUS");
+  int want = ce ? atoi(ce) : 64;
+  if (want > cus) want = cus;
+  if (want > 0 && want < cus) {
+    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int k = 0; k < want; k++) {
+      const int cu = (int)((int64_t)k * cus / want);
+      mask[cu / 32] |= 1u << (cu % 32);
+    }
+    HIPCHK(ctx, hipExtStreamCreateWithCUMask(&o.stream, (uint32_t)mask.size(), mask.data()));
+  } else {
+    HIPCHK(ctx, hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking));
+  }
+  HIPCHK(ctx, hipEventCreateWithFlags(&o.exited, hipEventDisableTiming));
+  const char* ge = getenv("MV_ONLINE_WGS");  // resident workgroups (4-block jobs in flight)
+  o.grid = (uint32_t)(ge ? std::max(2, atoi(ge)) : (want > 0 ? want : 64));  // >= 2: the poller + workers
+  o.ready = true;
+  return MV_OK;
+}
+
+// Launches the kernel unless one is live (o.mu held).
+mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
+  if (o.launched && steady_ns() - o.last_done_ns.load(std::memory_order_relaxed) < (int64_t)o.idle_us * 500) return MV_OK;
+  if (o.launched) {
+    const hipError_t q = hipEventQuery(o.exited);
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return MV_OK;  // still running
+    }
+    if (q != hipSuccess) {
+      o.failed = true;
+      return set_err(ctx, MV_E_HIP, std::string("online service: ") + hipGetErrorString(q));
+    }
+  }
+  const char* ie = getenv("MV_ONLINE_IDLE_US");
+  const uint64_t idle_us = ie ? (uint64_t)atoll(ie) : 2000ull;
+  o.idle_us = idle_us;
+  __atomic_store_n(&o.ctl->stop, 0ull, __ATOMIC_RELEASE);
+  HIPCHK(ctx, hipSetDevice(dev.id));
+  // the kernel's wall clock (s_memrealtime) in kHz; a launch lives at most 60 s (callers relaunch)
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev.id) != hipSuccess || khz <= 0) {
+    (void)hipGetLastError();
+    khz = 100000;
+  }
+  const uint64_t per_us = (uint64_t)khz / 1000 ? (uint64_t)khz / 1000 : 1;
+  HIPCHK(ctx, mvk::launch_online((mvk::OnlineCtl*)o.ctl_d, (const mvk::OnlineReq*)o.req_d, o.dctl.as<mvk::OnlineDev>(),
+                                 o.grid, dev.combB.p, dev.combA.p, dev.keyok.as<uint8_t>(),
+                                 dev.committee_pk.as<uint8_t>(), idle_us * per_us, 60000000ull * per_us, o.stream));
+  HIPCHK(ctx, hipEventRecord(o.exited, o.stream));
+  o.launched = true;
+  o.launches++;
+  return MV_OK;
+}
+
+// Stops the kernel once it is idle and waits for it (o.mu held).
+void online_stop(OnlineSvc& o) {
+  if (!o.ready || !o.launched) return;
+  __atomic_store_n(&o.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(o.stream);
+  __atomic_store_n(&o.ctl->stop, 0ull, __ATOMIC_RELEASE);
+  o.launched = false;
+}
+
+void online_release(OnlineSvc& o) {
+  online_stop(o);
+  if (o.stream) (void)hipStreamDestroy(o.stream);
+  if (o.exited) (void)hipEventDestroy(o.exited);
+  for (void* h : {(void*)o.ctl, (void*)o.req, (void*)o.in, (void*)o.out})
+    if (h) (void)hipHostFree(h);
+  o.dctl.release();
+  o.scr.release();
+  o.ready = false;
+}
+
+// One request through the service: reserve a ring slot, pack the blocks into its page-locked
+// input, publish the descriptor, then poll the slot's done word (the caller's thread spins:
+// no launch, no event, no wake-up). ctx->com_mu is held shared by the caller.
+mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint64_t* off, const uint64_t* len,
+                        uint32_t n, uint8_t* status, uint8_t* md, uint8_t* bd) {
+  OnlineSvc& o = *dev.online;
+  uint64_t q;
+  {
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (o.failed) return set_err(ctx, MV_E_HIP, "online service failed earlier");
+    mv_status rc = online_init(ctx, dev, o);
+    if (rc != MV_OK) {
+      o.failed = true;
+      return rc;
+    }
+    q = o.next_q++;
+    __atomic_store_n(&o.ctl->tail, o.next_q, __ATOMIC_RELEASE);
+    rc = online_ensure_running(ctx, dev, o);
+    if (rc != MV_OK) return rc;  // request q is never served: the service is marked failed
+  }
+  o.requests++;
+  const uint32_t slot = (uint32_t)(q % kOnSlots);
+  if (q >= kOnSlots)  // the slot's previous request must have been read out by its owner
+    while (o.freed[slot].load(std::memory_order_acquire) != q - kOnSlots + 1) std::this_thread::yield();
+  // the slot's input: off[n] | len[n] | bincode (8-aligned blocks) | 16 zero bytes; the poller
+  // copies it to the slot's HBM scratch, which every device pointer below refers to
+  uint8_t* in = o.in + kOnInStride * slot;
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(in);
+  uint64_t* hlen = hoff + n;
+  uint8_t* bytes = in + 16 * (size_t)n;
+  uint64_t pos = 0;
+  for (uint32_t k = 0; k < n; k++) {
+    const uint64_t l = len[k];
+    hoff[k] = pos;
+    hlen[k] = l;
+    memcpy(bytes + pos, buf + off[k], l);
+    const uint64_t pl = (l + 7) & ~7ull;
+    memset(bytes + pos + l, 0, pl - l);
+    pos += pl;
+  }
+  memset(bytes + pos, 0, 16);  // 16 readable zero bytes past the last block
+  const uint32_t copy_bytes = (uint32_t)((16 * (size_t)n + pos + 16 + 15) & ~(size_t)15);
+  uint8_t* out = o.out + kOnOutStride * slot;
+  char* sc = o.scr.as<char>() + kOnScrStride * slot;
+  size_t so = 0;
+  auto take = [&](size_t b) {
+    char* p = sc + so;
+    so += al256(b);
+    return p;
+  };
+  uint8_t* in_dev = (uint8_t*)take(kOnInStride);
+  uint8_t* out_dev = (uint8_t*)take(kOnOutStride);
+  uint8_t* stage = (uint8_t*)take(kOnStage);
+  uint64_t* poff = (uint64_t*)take(8 * kOnMax);
+  uint64_t* plen = (uint64_t*)take(8 * kOnMax);
+  uint8_t* sig = (uint8_t*)take(64 * kOnMax);
+  uint32_t* kidx = (uint32_t*)take(4 * kOnMax);
+  uint32_t* facts = (uint32_t*)take(4 * kOnMax);
+  uint8_t* claimed = (uint8_t*)take(32 * kOnMax);
+  uint8_t* sst = (uint8_t*)take(kOnMax);
+  uint8_t* dmd = out_dev;
+  uint8_t* dbd = out_dev + 32 * kOnMax;
+  uint8_t* dst = out_dev + 64 * kOnMax;
+  const uint64_t* doff = reinterpret_cast<const uint64_t*>(in_dev);
+  const mvh::Committee& com = ctx->committee;
+  mvk::OnlineReq& r = o.req[slot];
+  r.n = n;
+  r.copy_bytes = copy_bytes;
+  r.in_host = static_cast<const uint8_t*>(o.in_d) + kOnInStride * slot;
+  r.in_dev = in_dev;
+  r.out_host = static_cast<uint8_t*>(o.out_d) + kOnOutStride * slot;
+  r.out_dev = out_dev;
+  r.msg = dmd;
+  r.sig = sig;
+  r.key_idx = kidx;
+  r.sst = sst;
+  r.bv = mvk::BlockVerdictOut{facts, claimed, dmd, dbd, dst};
+  r.hin = mvk::BlockHashIn{stage, poff, plen, dmd, dbd};
+  r.ing = mvk::BlockIngestIn{in_dev + 16 * (size_t)n, doff, doff + n, dev.stakes.as<uint64_t>(), (uint32_t)com.size(),
+                             com.epoch, com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed};
+  __atomic_store_n(&r.seq, q + 1, __ATOMIC_RELEASE);  // the descriptor and the bytes above first
+  // wait for the slot's done word; every ~100 us check that a kernel is still live (one that
+  // exited idle just before this request was published is relaunched)
+  auto t_last = std::chrono::steady_clock::now();
+  const auto t_start = t_last;
+  uint32_t spins = 0;
+  mv_status rc = MV_OK;
+  while (__atomic_load_n(&o.ctl->done[slot], __ATOMIC_ACQUIRE) != q + 1) {
+    if (++spins < 64) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    spins = 0;
+    std::this_thread::yield();
+    const auto now = std::chrono::steady_clock::now();
+    if (now - t_last < std::chrono::microseconds(100)) continue;
+    t_last = now;
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (o.failed) {
+      rc = set_err(ctx, MV_E_HIP, "online service failed");
+      break;
+    }
+    rc = online_ensure_running(ctx, dev, o);
+    if (rc == MV_OK && now - t_start > std::chrono::seconds(20)) {
+      o.failed = true;  // the slot may still be written: never reuse the service
+      rc = set_err(ctx, MV_E_HIP, "online service: request timed out");
+    }
+    if (rc != MV_OK) break;
+  }
+  if (rc != MV_OK) return rc;
+  const uint8_t* ho = out;
+  for (uint32_t k = 0; k < n; k++) {
+    status[k] = ho[64 * kOnMax + k];
+    if (md) memcpy(md + 32 * (size_t)k, ho + 32 * (size_t)k, 32);
+    if (bd) memcpy(bd + 32 * (size_t)k, ho + 32 * ((size_t)kOnMax + k), 32);
+  }
+  o.freed[slot].store(q + 1, std::memory_order_release);
+  o.last_done_ns.store(steady_ns(), std::memory_order_relaxed);
+  return MV_OK;
+}
+
 // One pass of the submission queue over the requests the combining caller took. set >= 0:
 // the pass fits one chunk per device and runs on that pass set: it is packed and enqueued
 // under ctx->mu, `enqueued()` is called, and the caller waits for the device without the
@@ -1472,6 +1765,15 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
 void mv_destroy(mv_ctx* ctx) {
   if (!ctx) return;
   (void)mv_stage_times(ctx, nullptr, nullptr, 1);  // drain pending stage events
+  {
+    std::unique_lock<std::shared_mutex> cl(ctx->com_mu);
+    for (auto& dev : ctx->devs)
+      if (dev.online) {
+        std::lock_guard<std::mutex> ol(dev.online->mu);
+        (void)hipSetDevice(dev.id);
+        online_release(*dev.online);  // before the device drain below: the kernel would hold it
+      }
+  }
   for (auto& dev : ctx->devs) {
     (void)hipSetDevice(dev.id);
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
@@ -1531,7 +1833,14 @@ const char* mv_last_error(const mv_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks, const uint64_t* stakes, uint32_t n, uint64_t epoch,
                            uint8_t* key_ok) {
   if (!ctx || !pks || !stakes || n == 0 || n > 512) return set_err(ctx, MV_E_INVALID_ARG, "bad committee args");
+  std::unique_lock<std::shared_mutex> cl(ctx->com_mu);  // no online request in flight
   std::lock_guard<std::mutex> lk(ctx->mu);
+  for (auto& dev : ctx->devs)
+    if (dev.online) {
+      std::lock_guard<std::mutex> ol(dev.online->mu);
+      (void)hipSetDevice(dev.id);
+      online_stop(*dev.online);  // the resident kernel reads the tables rebuilt below
+    }
   mvh::Committee c;
   c.pks.assign(pks, pks + 32 * (size_t)n);
   c.stakes.assign(stakes, stakes + n);
@@ -1715,6 +2024,30 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     std::lock_guard<std::mutex> lk(ctx->mu);
     return verify_blocks_host_parse(ctx, buf, off, len, n, status, msg_digest, block_digest);
   }
+  // the resident online service: small calls of short blocks, no queue, no launch
+  {
+    uint64_t bytes = 0;
+    for (uint32_t k = 0; k < n && bytes <= (128u << 10); k++) bytes += (len[k] + 7) & ~7ull;
+    if (online_eligible(ctx, n, bytes)) {
+      std::shared_lock<std::shared_mutex> cl(ctx->com_mu);
+      if (committee_ready(ctx)) {
+        Device& dev = ctx->devs[ctx->online_rr.fetch_add(1) % ctx->devs.size()];
+        {
+          std::lock_guard<std::mutex> lk(ctx->mu);  // the service object (devs is fixed after mv_create)
+          if (!dev.online) dev.online = std::make_shared<OnlineSvc>();
+        }
+        std::string err;
+        t_err = &err;
+        const mv_status rc = online_verify(ctx, dev, buf, off, len, n, status, msg_digest, block_digest);
+        t_err = nullptr;
+        if (rc != MV_OK) {
+          std::lock_guard<std::mutex> lk(ctx->mu);
+          ctx->err = err;
+        }
+        return rc;
+      }
+    }
+  }
   // Flat combining, pipelined: the request joins the queue; a caller that finds no pass being
   // packed and a free pass set takes every queued request (its own included) into one pass,
   // packs and enqueues it, then lets the next caller pack the following pass into the other
@@ -1810,6 +2143,19 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     ctx->err = req.err;
   }
   return req.rc;
+}
+
+mv_status mv_online_stats(mv_ctx* ctx, uint64_t* requests, uint64_t* launches) {
+  if (!ctx) return MV_E_INVALID_ARG;
+  uint64_t r = 0, l = 0;
+  for (auto& dev : ctx->devs)
+    if (dev.online) {
+      r += dev.online->requests.load();
+      l += dev.online->launches.load();
+    }
+  if (requests) *requests = r;
+  if (launches) *launches = l;
+  return MV_OK;
 }
 
 mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes) {

@@ -109,6 +109,55 @@ struct BlockIngestIn {
   uint32_t* facts;
   uint8_t* claimed;
 };
+// The resident online service (comb.hip k_online): one kernel that stays on the GPU while
+// online traffic flows and runs each mv_verify_blocks request of <= ONLINE_MAX_BLOCKS short
+// blocks as k_verify_comb16's workgroups would (ingest, both digests, challenge, comb sums,
+// verdict), with no launch and no event per request.
+//   host     writes request q's input (offsets, lengths, bincode) and descriptor into ring slot
+//            q % ONLINE_SLOTS of page-locked memory, then seq = q + 1; ctl.tail >= q + 1
+//   poller   workgroup 0 polls ctl.tail, copies every request whose seq is set -- descriptor
+//            and input -- into HBM (one pass for all of them), then advances dev.ready: the
+//            only PCIe reads on the request's path
+//   workers  workgroups 1.. claim 4-block jobs from the device ticket (HBM only), run them from
+//            the HBM copies, copy their blocks' digests and verdicts to the slot's page-locked
+//            output; the request's last job stores ctl.done[slot] = q + 1 (system-scope release)
+// Workers exit after idle_ticks without a job (or on ctl.stop when idle, or after max_ticks);
+// the poller exits once every worker has.
+constexpr uint32_t ONLINE_SLOTS = 64;
+constexpr uint32_t ONLINE_MAX_BLOCKS = 64;  // 16 jobs per request
+constexpr uint32_t ONLINE_JOB_BITS = 5;
+struct OnlineReq {
+  uint64_t seq;  // request number + 1 once the fields below are written (host: release store)
+  uint32_t n;    // blocks; 0 = a void request (completed without work)
+  uint32_t copy_bytes;       // input bytes of the slot (offsets, lengths, bincode + 16)
+  const uint8_t* in_host;    // the slot's input, page-locked (device view) ...
+  uint8_t* in_dev;           // ... and its HBM copy, which every pointer below refers to
+  uint8_t* out_host;         // md[64][32] | bd[64][32] | status[64], page-locked (device view)
+  uint8_t* out_dev;          // the same layout in HBM (where the kernel writes them first)
+  const uint8_t* msg;        // comb16 operands (HBM)
+  const uint8_t* sig;
+  const uint32_t* key_idx;
+  uint8_t* sst;
+  BlockVerdictOut bv;
+  BlockHashIn hin;
+  BlockIngestIn ing;
+};
+struct OnlineCtl {
+  uint64_t tail;  // requests published so far
+  uint64_t stop;  // nonzero: exit when idle
+  uint64_t done[ONLINE_SLOTS];
+};
+struct OnlineDev {
+  unsigned long long ticket;  // (request << ONLINE_JOB_BITS) | next job
+  unsigned long long ready;   // requests copied to HBM by the poller
+  uint32_t live;              // workers not yet exited (set to grid - 1 before each launch)
+  uint32_t jobs_done[ONLINE_SLOTS];
+  uint32_t nj[ONLINE_SLOTS];  // jobs of the slot's current request
+  OnlineReq desc[ONLINE_SLOTS];
+};
+hipError_t launch_online(OnlineCtl* ctl, const OnlineReq* reqs, OnlineDev* dev, uint32_t grid, const void* combB,
+                         const void* combA, const uint8_t* key_ok, const uint8_t* pk, uint64_t idle_ticks,
+                         uint64_t max_ticks, hipStream_t s);
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr,

@@ -50,6 +50,7 @@ pub const MV_WAL_BAD_LENGTH: u8 = 3;
 pub const MV_FLAG_NO_BATCH: u32 = 1;
 pub const MV_FLAG_NO_COMB: u32 = 2;
 pub const MV_FLAG_HOST_PARSE: u32 = 4;
+pub const MV_FLAG_NO_ONLINE: u32 = 8;
 pub const MV_BATCH_MIN: u32 = 4096;
 pub const MV_NSTAGES: usize = 12;
 
@@ -72,6 +73,7 @@ extern "C" {
                             status: *mut u8, msg_digest: *mut u8, block_digest: *mut u8) -> i32;
     pub fn mv_block_preimage(bincode: *const u8, len: u64, out: *mut u8, cap: u64) -> i64;
     pub fn mv_queue_stats(ctx: *mut mv_ctx, calls: *mut u64, passes: *mut u64) -> i32;
+    pub fn mv_online_stats(ctx: *mut mv_ctx, requests: *mut u64, launches: *mut u64) -> i32;
     pub fn mv_shard_plan(weights: *const u64, n: u64, parts: u32, cut: *mut u64) -> i32;
     pub fn mv_crc32(ctx: *mut mv_ctx, buf: *const u8, off: *const u64, len: *const u64, n: u32,
                     out: *mut u32) -> i32;

@@ -62,10 +62,11 @@ def test_logical_shards_match_one_device(engine, shards):
         assert int(st1[i]) == ost, i
 
 
-def test_concurrent_callers_are_coalesced(engine):
+def test_concurrent_callers_are_coalesced(engine, monkeypatch):
     """16 threads each submit 1-4 blocks at a time (the per-peer tasks of net_sync.rs); every
     verdict and digest equals the serial call's, and the queue served the calls in fewer
-    device passes than calls."""
+    device passes than calls (the resident online service is off: every call queues)."""
+    monkeypatch.setenv("MV_ONLINE", "0")
     bins, pks, stakes = ragged_blocks(n_rounds=40, seed=9)
     engine.set_committee(pks, stakes, 0)
     st_ref, md_ref, bd_ref = engine.verify_blocks(bins)
@@ -102,3 +103,127 @@ def test_concurrent_callers_are_coalesced(engine):
     assert (got_st == st_ref).all() and (got_md == md_ref).all() and (got_bd == bd_ref).all()
     assert len({int(s) for s in st_ref}) >= 3
     assert calls >= 16 * 3 * (n // 16) // 4 and passes < calls
+
+
+def _concurrent(engine, bins, threads=16, rounds=3, kmax=5):
+    n = len(bins)
+    got_st = np.full(n, 255, np.uint8)
+    got_md = np.zeros((n, 32), np.uint8)
+    got_bd = np.zeros((n, 32), np.uint8)
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(100 + t)
+        idx = list(range(t, n, threads))
+        try:
+            for _ in range(rounds):
+                i = 0
+                while i < len(idx):
+                    k = int(rng.integers(1, kmax))
+                    part = idx[i:i + k]
+                    st, md, bd = engine.verify_blocks([bins[j] for j in part])
+                    got_st[part], got_md[part], got_bd[part] = st, md, bd
+                    i += k
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    return got_st, got_md, got_bd
+
+
+def test_online_service_concurrent_callers(engine, monkeypatch):
+    """The resident online service (k_online): 16 threads posting 1-4 blocks at a time get the
+    verdicts and digests of the queue path (MV_ONLINE=0) and of the oracle; the service served
+    the short-block calls (the long ones, > 2 KB per block, still queue)."""
+    bins, pks, stakes = ragged_blocks(n_rounds=40, seed=13)
+    engine.set_committee(pks, stakes, 0)
+    monkeypatch.setenv("MV_ONLINE", "0")
+    st_ref, md_ref, bd_ref = engine.verify_blocks(bins)
+    monkeypatch.delenv("MV_ONLINE")
+    o0 = engine.online_stats()
+    st, md, bd = _concurrent(engine, bins)
+    o1 = engine.online_stats()
+    assert (st == st_ref).all() and (md == md_ref).all() and (bd == bd_ref).all()
+    assert o1[0] - o0[0] > 100 and o1[1] >= 1
+    for i in range(0, len(bins), 37):
+        ost, omd, obd = O.block_verify(bins[i], pks, stakes, 0)
+        assert int(st[i]) == ost and md[i].tobytes() == omd and bd[i].tobytes() == obd, i
+
+
+def test_online_service_edge_blocks_one_and_64_per_call(engine, golden, monkeypatch):
+    """Every golden edge-case block through the service one per call and in 64-block calls
+    (16 jobs of one request), against the fixture's verdicts and the queue path's digests."""
+    fx = golden("block_edge.json")
+    pks = np.array([bytes.fromhex(k) for k in fx["committee"]["pks"]], dtype=object)
+    pks = np.frombuffer(b"".join(pks), dtype=np.uint8).reshape(-1, 32)
+    stakes = np.array(fx["committee"]["stakes"], dtype=np.uint64)
+    engine.set_committee(pks, stakes, fx["committee"]["epoch"])
+    bins = [bytes.fromhex(c["bincode"]) for c in fx["cases"]]
+    want = np.array([c["status"] for c in fx["cases"]], dtype=np.uint8)
+    monkeypatch.setenv("MV_ONLINE", "0")
+    _, md_ref, bd_ref = engine.verify_blocks(bins)
+    monkeypatch.delenv("MV_ONLINE")
+    o0 = engine.online_stats()[0]
+    one = [engine.verify_blocks([b]) for b in bins]
+    st1 = np.array([r[0][0] for r in one], dtype=np.uint8)
+    assert (st1 == want).all()
+    for i, r in enumerate(one):
+        assert (r[1][0] == md_ref[i]).all() and (r[2][0] == bd_ref[i]).all(), i
+    reps = (bins * (64 // len(bins) + 1))[:64]
+    st64, md64, bd64 = engine.verify_blocks(reps)
+    w64 = (list(want) * (64 // len(bins) + 1))[:64]
+    assert (st64 == np.array(w64, np.uint8)).all()
+    assert engine.online_stats()[0] - o0 >= sum(1 for b in bins if len(b) < 1900)
+
+
+def test_online_service_relaunches_after_idle_exit(engine, monkeypatch):
+    """With a 300-us idle limit the kernel exits between calls 20 ms apart; the next call
+    relaunches it and gets the right verdicts."""
+    monkeypatch.setenv("MV_ONLINE_IDLE_US", "300")
+    bins, pks, stakes = ragged_blocks(n_rounds=8, seed=3)
+    engine.set_committee(pks, stakes, 0)  # stops a resident kernel (its idle limit was read at launch)
+    short = [b for b in bins if len(b) < 1500][:6]
+    l0 = engine.online_stats()[1]
+    ref = [O.block_verify(b, pks, stakes, 0)[0] for b in short]
+    import time
+
+    for b, w in zip(short, ref):
+        st, _, _ = engine.verify_blocks([b])
+        assert int(st[0]) == w
+        time.sleep(0.02)
+    assert engine.online_stats()[1] - l0 >= len(short) - 1
+
+
+def test_online_service_does_not_block_other_streams(engine, monkeypatch):
+    """The resident kernel sits on a CU-masked stream of its own: while it is live (idle limit
+    5 s here), a batch-path signature call and a queue-path block call on the engine's other
+    streams complete at once, and the service is still the same launch afterwards."""
+    import time
+
+    monkeypatch.setenv("MV_ONLINE_IDLE_US", "5000000")
+    bins, pks, stakes = ragged_blocks(n_rounds=8, seed=4)
+    engine.set_committee(pks, stakes, 0)
+    short = [b for b in bins if len(b) < 1500][:4]
+    st, _, _ = engine.verify_blocks(short)  # launches the service
+    l0 = engine.online_stats()[1]
+    n = M.BATCH_MIN + 100
+    rng = np.random.default_rng(8)
+    seed = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    t0 = time.perf_counter()
+    pk, sig = engine.ed25519_sign(seed, msg)
+    ss = engine.ed25519_verify(msg, sig, pk)
+    monkeypatch.setenv("MV_ONLINE", "0")
+    st_q, _, _ = engine.verify_blocks(short)
+    monkeypatch.delenv("MV_ONLINE")
+    dt = time.perf_counter() - t0
+    assert (ss == 0).all() and (st_q == st).all()
+    assert dt < 2.0, dt  # not serialised behind the resident kernel's 5-s idle limit
+    st2, _, _ = engine.verify_blocks(short)
+    assert (st2 == st).all() and engine.online_stats()[1] == l0
+    engine.set_committee(pks, stakes, 0)  # stops the service (no 5-s resident kernel left behind)

@@ -110,7 +110,10 @@ for T in "$@"; do
           else
             CMD="python bench.py --workload config4 --steps 20 --warmup 5 --cpu-sample 0 --host-fed-blocks 0 ${A//,/ }"
           fi
-          MV_LIB=$ML timeout -k 10 400 $CMD > "$OUT/${name}_${lib}_$rep.json" 2> "$OUT/${name}_${lib}_$rep.err" || { echo "$name $lib FAILED"; tail -8 "$OUT/${name}_${lib}_$rep.err"; exit 1; }
+          # exit 1 = verdicts wrong (an experiment build may compute garbage on purpose): kept
+          MV_LIB=$ML timeout -k 10 400 $CMD > "$OUT/${name}_${lib}_$rep.json" 2> "$OUT/${name}_${lib}_$rep.err"
+          rc=$?
+          if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "$name $lib FAILED rc=$rc"; tail -8 "$OUT/${name}_${lib}_$rep.err"; exit 1; fi
           echo -n "rep $rep $lib: "
           line "$OUT/${name}_${lib}_$rep.json"
         done

@@ -26,7 +26,7 @@ if c5:
     for k, v in c5["shapes"].items():
         c = v["concurrent_1_block_callers"]
         out.append(f"c5 {k} p50={v['gpu']['p50_us']} p99={v['gpu']['p99_us']} conc={c['gpu']['blocks_per_s']} "
-                   f"p50c={c['gpu']['p50_us']} cpp={c['gpu'].get('calls_per_device_pass')} cpu={c.get('cpu_own_core', {}).get('blocks_per_s')}")
+                   f"p50c={c['gpu']['p50_us']} cpp={c['gpu'].get('calls_per_device_pass')} onl={c['gpu'].get('online_requests')}/{c['gpu'].get('online_launches')} cpu={c.get('cpu_own_core', {}).get('blocks_per_s')}")
 w = d.get("wal") or (d if "WAL" in d.get("metric", "") else None)
 if w:
     out.append(f"wal {w['value']} GB/s stages={w.get('stage_ms')}")
