@@ -69,7 +69,7 @@ def slots(field_ops: int, hash_ops: int) -> int:
 
 def pmc_traffic(kernel: str, workload: str = "c2"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/<round>/
-    pmc_<workload>_<kernel>.json from tools/profile_r02.sh, or the round-1 pmc_<kernel>.json)."""
+    pmc_<workload>_<kernel>.json from tools/gpu.sh pmc:W, or the round-1 pmc_<kernel>.json)."""
     import glob
 
     files = []
@@ -290,7 +290,7 @@ def main():
     # With two streams a stage's events also count time its kernels share the chip with the
     # other stream's tail. Re-time the stages on ONE stream after the timed region (untimed
     # for `value`), so the dominant kernel's duration matches the single-stream rocprof trace
-    # (profiles/<round>/trace_single_stream, tools/profile.sh).
+    # (profiles/<round>/, tools/gpu.sh trace:c2s1).
     iso_ms = {}
     if args.path == "batch" and nstreams > 1:
         eng.stage_times(reset=True)

@@ -164,7 +164,7 @@ struct CommitteeA {
   const uint4* tab;  // nullptr: decode A per signature
   const uint8_t* ok;
   uint32_t stride;   // uint4 per key table
-  uint32_t aggregate;  // 1: A's term is summed per key (k_bv_keyacc / k_bv_keypts), no A points
+  uint32_t aggregate;  // 1: A's term is summed per key (k_bv_keyacc / keycol / keysum), no A points
 };
 
 #ifndef MV_PREP_OCC
@@ -680,29 +680,44 @@ __global__ void __launch_bounds__(PART_CHUNK) k_bv_keyacc(const uint4* __restric
   for (uint32_t i = threadIdx.x; i < nkeys * 8; i += PART_CHUNK) kpart[(size_t)blockIdx.x * nkeys * 8 + i] = ks[i];
 }
 
-// Block g = group: thread t takes keys t, t + 256, ...: c = sum over the group's chunks,
-// reduced mod l, [c](-A_b) from the key's comb table of -A, summed; a tree over the block
-// -> asum[g] = +sum_b [c_b] A_b (negated at the end).
-__global__ void __launch_bounds__(256) k_bv_keypts(const unsigned long long* __restrict__ kpart, uint32_t nchunk,
+// The per-key term in two launches, wide enough that neither is a latency chain on a few
+// lanes (round 3's one-workgroup-per-group form walked every chunk of every key on one lane:
+// 0.44 ms per 2^20 config-4 blocks):
+//   k_bv_keycol  workgroup (g, b): c_b = sum over the group's chunks of kpart (256 lanes, then
+//                an LDS tree), reduced mod l and recoded; then lane r < 32 adds table row r's
+//                entry of c_b's digit r to the identity and a 5-level tree sums the 32 rows:
+//                keyp[g][b] = [c_b](-A_b)
+//   k_bv_keysum  workgroup g: the group's keys' points by a tree -> asum[g] = +sum_b [c_b] A_b
+__global__ void __launch_bounds__(256) k_bv_keycol(const unsigned long long* __restrict__ kpart, uint32_t nchunk,
                                                    uint32_t cpg, uint32_t nkeys, const uint4* __restrict__ combA,
-                                                   uint4* __restrict__ asum) {
-  __shared__ uint4 red[P3_QUADS][256];
-  const uint32_t g = blockIdx.x, t = threadIdx.x;
+                                                   uint4* __restrict__ keyp) {
+  __shared__ unsigned long long cs[8][256];
+  __shared__ uint32_t sd_s[8];
+  __shared__ uint4 red[P3_QUADS][CT_ROWS];
+  const uint32_t g = blockIdx.x / nkeys, b = blockIdx.x % nkeys, t = threadIdx.x;
   const uint32_t c0 = g * cpg, c1 = min(nchunk, c0 + cpg);
-  p3 acc;
-  p3_identity(acc);
-  for (uint32_t b = t; b < nkeys; b += blockDim.x) {
-    unsigned long long col[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t c = c0; c < c1; c++) {
-      const unsigned long long* p = kpart + ((size_t)c * nkeys + b) * 8;
+  unsigned long long col[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t c = c0 + t; c < c1; c += blockDim.x) {
+    const unsigned long long* p = kpart + ((size_t)c * nkeys + b) * 8;
 #pragma unroll
-      for (int k = 0; k < 8; k++) col[k] += p[k];
+    for (int k = 0; k < 8; k++) col[k] += p[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) cs[k][t] = col[k];
+  __syncthreads();
+  for (uint32_t h = blockDim.x / 2; h > 0; h >>= 1) {
+    if (t < h) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) cs[k][t] += cs[k][t + h];
     }
+    __syncthreads();
+  }
+  if (t == 0) {
     uint32_t x[16], r[8], sd[8];
     unsigned long long carry = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const unsigned long long v = col[k] + carry;  // col < 2^52: no overflow
+      const unsigned long long v = cs[k][0] + carry;  // column sums < 2^62: no overflow
       x[k] = (uint32_t)v;
       carry = v >> 32;
     }
@@ -712,8 +727,51 @@ __global__ void __launch_bounds__(256) k_bv_keypts(const unsigned long long* __r
     for (int k = 10; k < 16; k++) x[k] = 0;
     sc_reduce512(r, x);
     sc_recode256(sd, r);
+#pragma unroll
+    for (int k = 0; k < 8; k++) sd_s[k] = sd[k];
+  }
+  __syncthreads();
+  if (t < CT_ROWS) {  // row t's entry of digit t, as a point
+    uint32_t sd[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) sd[k] = sd_s[k];
     p3 P;
-    ct_sum(P, combA + (size_t)b * CT_TABLE, sd, 0, CT_ROWS);
+    ct_sum(P, combA + (size_t)b * CT_TABLE, sd, (int)t, (int)t + 1);
+    uint4 q[9];
+    p3_to_quads(q, P);
+#pragma unroll
+    for (int k = 0; k < 9; k++) red[k][t] = q[k];
+  }
+  __syncthreads();
+  for (uint32_t h = CT_ROWS / 2; h > 0; h >>= 1) {
+    if (t < h) {
+      p3 A, B;
+      uint4 q[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) q[k] = red[k][t];
+      quads_to_p3(A, q);
+#pragma unroll
+      for (int k = 0; k < 9; k++) q[k] = red[k][t + h];
+      quads_to_p3(B, q);
+      p3_acc(A, B);
+      p3_to_quads(q, A);
+#pragma unroll
+      for (int k = 0; k < 9; k++) red[k][t] = q[k];
+    }
+    __syncthreads();
+  }
+  if (t < P3_QUADS) keyp[((size_t)g * BV_MAXKEYS + b) * P3_QUADS + t] = red[t][0];
+}
+
+__global__ void __launch_bounds__(256) k_bv_keysum(const uint4* __restrict__ keyp, uint32_t nkeys,
+                                                   uint4* __restrict__ asum) {
+  __shared__ uint4 red[P3_QUADS][256];
+  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  p3 acc;
+  p3_identity(acc);
+  for (uint32_t b = t; b < nkeys; b += blockDim.x) {
+    p3 P;
+    p3_load(P, keyp, (size_t)g * BV_MAXKEYS + b);
     p3_acc(acc, P);
   }
   uint4 q[9];
@@ -842,7 +900,7 @@ __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV
       qp_dbl_n(v, BV_C);
       qp_add(v, wv);
     }
-    if (asum) {  // the per-key A term of the group (k_bv_keypts)
+    if (asum) {  // the per-key A term of the group (k_bv_keysum)
       fe av;
       qp_load(av, asum, g);
       qp_add(v, av);
@@ -881,8 +939,8 @@ namespace mvk {
 namespace {
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BatchLayout {
-  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, kpart, asum,
-      flag, total;
+  size_t pts, scal, pcount, poff, ptot, pstart, tmp, offs, ents, segV, segT, rV0, rT0, rV1, rT1, bsum, kpart, keyp,
+      asum, flag, total;
   BatchLayout(uint32_t n, uint32_t groups) {
     using namespace mv;
     size_t o = 0;
@@ -903,6 +961,7 @@ struct BatchLayout {
     rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
     bsum = take((size_t)BV_MAXG * BSUM_WORDS * 8);  // per group
     kpart = take(nchunk * BV_MAXKEYS * 8 * 8);
+    keyp = take((size_t)BV_MAXG * BV_MAXKEYS * P3_QUADS * 16);
     asum = take((size_t)BV_MAXG * P3_QUADS * 16);
     flag = take((1 + BV_MAXG) * 4);
     total = o;
@@ -980,6 +1039,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   uint4* rt[2] = {(uint4*)(base + L.rT0), (uint4*)(base + L.rT1)};
   unsigned long long* bsum = (unsigned long long*)(base + L.bsum);
   unsigned long long* kpart = (unsigned long long*)(base + L.kpart);
+  uint4* keyp = (uint4*)(base + L.keyp);
   uint4* asum = (uint4*)(base + L.asum);
   uint32_t* flag = (uint32_t*)(base + L.flag);
   if (flag_out) *flag_out = flag;
@@ -1037,8 +1097,9 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
                      G.count, seg, nw, segV, segT);
   if (agg) {
     hipLaunchKernelGGL(k_bv_keyacc, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, key_idx, n, n_keys, kpart);
-    hipLaunchKernelGGL(k_bv_keypts, dim3(G.count), dim3(256), 0, s, kpart, nchunk, G.cpg, n_keys,
-                       static_cast<const uint4*>(comb_a), asum);
+    hipLaunchKernelGGL(k_bv_keycol, dim3(G.count * n_keys), dim3(256), 0, s, kpart, nchunk, G.cpg, n_keys,
+                       static_cast<const uint4*>(comb_a), keyp);
+    hipLaunchKernelGGL(k_bv_keysum, dim3(G.count), dim3(256), 0, s, keyp, n_keys, asum);
   }
   mark(3);
   const uint4* inV = seg > 1 ? segV : nullptr;  // one bucket per segment: V = T

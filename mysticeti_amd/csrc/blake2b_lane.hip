@@ -77,12 +77,6 @@ MV_DEV void compress(uint64_t (&h)[8], const uint64_t (&m)[16], uint64_t t, bool
 // Block b of the string at p, zero past lim; a word is read only when it starts below lim (the
 // strings are 8-aligned and readable up to round-up(lim, 8), as for the quad form).
 MV_DEV void load_block(uint64_t (&m)[16], const uint8_t* p, uint64_t b, uint64_t lim) {
-#ifdef MV_B2L_NOLOAD  // experiment (tools/gpu.sh abc4): message words made in registers, no loads
-  const uint64_t x = reinterpret_cast<uint64_t>(p) ^ (b * 0x9e3779b97f4a7c15ull);
-#pragma unroll
-  for (int j = 0; j < 16; j++) m[j] = x + (uint64_t)j * 0x100000001ull + lim;
-  return;
-#endif
   const uint64_t* src = reinterpret_cast<const uint64_t*>(p) + b * 16;
   const uint64_t base = b * 128;
   if (base + 128 <= lim) {
@@ -109,8 +103,13 @@ MV_DEV void load_block(uint64_t (&m)[16], const uint8_t* p, uint64_t b, uint64_t
 // needs 134 VGPRs and 3 waves per SIMD and measured no faster; neither did a forced 5 waves per
 // SIMD (spills), a shift + add form of the 63-bit rotation, the four G's of a half-round
 // written in lock-step (the scheduler pairs them the same way), nor h parked in LDS during the
-// rounds (84 VGPRs, 5 waves per SIMD: 4.06 ms per 2^20 either way). The kernel is bound by VALU
-// issue: ~2,000 instructions per compression per wave, 20 per G, no cross-lane or LDS work.
+// rounds (84 VGPRs, 5 waves per SIMD: 4.06 ms per 2^20 either way). Round 4: the message words
+// made in registers instead of loaded (no memory traffic at all) ran the hash in the same 4.12
+// ms, and the blocks moved one step ahead through LDS by direct-to-LDS loads (16 lines per load
+// instruction instead of 64, 16 KB LDS per wave) ran it in 4.9 ms (profiles/r04/ab_c4_hash.txt):
+// the loads are not what bounds it. The kernel is bound by VALU issue: ~2,000 instructions per
+// compression per wave, 20 per G (6 v_lshl_add_u64, 8 v_xor, 4 v_perm, 2 v_alignbit: the
+// instruction mix of the algorithm), no cross-lane or LDS work.
 template <bool DUAL>
 __global__ void __launch_bounds__(64) k_b2_lane(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                 const uint64_t* __restrict__ len, uint32_t n,

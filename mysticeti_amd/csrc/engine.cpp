@@ -91,12 +91,14 @@ struct Device {
   // host-buffer batch verifies: two compute streams and double-buffered device inputs, so
   // the (pageable) H2D of one chunk runs beside the previous chunk's verification
   hipStream_t pstream[2] = {nullptr, nullptr};
-  DevBuf pin_msg[2], pin_sig[2], pin_pk[2], pin_st[2];
+  // (three input buffer sets: the streamed pinned path's batches rotate over them)
+  static constexpr int kPinBufs = 3;
+  DevBuf pin_msg[kPinBufs], pin_sig[kPinBufs], pin_pk[kPinBufs], pin_st[kPinBufs];
   HostBuf h_stage[2];
-  hipEvent_t pin_free[2] = {nullptr, nullptr};
+  hipEvent_t pin_free[kPinBufs] = {};
   // pinned inputs: per-chunk "copied" events of the two input buffers (verify_host_streamed)
   static constexpr int kMaxChunks = 64;
-  hipEvent_t chunk_ev[2][kMaxChunks] = {};
+  hipEvent_t chunk_ev[kPinBufs][kMaxChunks] = {};
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
   DevBuf committee_pk, stakes, combA, keyok;
@@ -144,12 +146,12 @@ struct Device {
   // buffers and a stream each, so pass k + 1 is packed and enqueued while passes k, k - 1, ...
   // run (an online pass is a few workgroups: passes on distinct hardware queues run side by side)
   static constexpr int kPassSets = 4;
-  hipStream_t qstream[kPassSets] = {};  // sets 2 and up (0: `stream`, 1: pstream[1])
+  hipStream_t qstream[kPassSets] = {};  // one per pass set
   struct PassSet {
     HostBuf h_in, h_out;
     DevBuf bytes, out2, scr;  // scr: the block pipeline's scratch for this set's passes
     BlkAux aux;               // the two-halves parse of a large host-fed chunk
-    hipStream_t stream = nullptr;  // set 0: `stream`, set 1: pstream[1], set k >= 2: qstream[k]
+    hipStream_t stream = nullptr;  // qstream[k]
     hipEvent_t done = nullptr;
     // the chunk in flight: items [lo, lo + m) of `it`, outputs in h_out when finished
     const void* it = nullptr;
@@ -816,16 +818,9 @@ void pack_items(uint8_t* h, uint64_t* off, uint64_t* len, const BlockItem* it, u
 
 mv_status ensure_pass_set(mv_ctx* ctx, Device& dev, int s) {
   Device::PassSet& ps = dev.pset[s];
-  if (!ps.stream) {
-    if (s == 0) {
-      ps.stream = dev.stream;
-    } else if (s == 1) {
-      if (!dev.pstream[1]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[1], hipStreamNonBlocking));
-      ps.stream = dev.pstream[1];
-    } else {
-      if (!dev.qstream[s]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.qstream[s], hipStreamNonBlocking));
-      ps.stream = dev.qstream[s];
-    }
+  if (!ps.stream) {  // a stream of its own: not the host-buffer signature path's copy / compute streams
+    if (!dev.qstream[s]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.qstream[s], hipStreamNonBlocking));
+    ps.stream = dev.qstream[s];
   }
   if (!ps.done) HIPCHK(ctx, hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
   return MV_OK;
@@ -921,8 +916,13 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
     (void)hipStreamSynchronize(ps.stream);  // what was queued reads the staging
     return rc;
   }
-  if (!hout_dev) HIPCHK(ctx, hipMemcpyAsync(ps.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, ps.stream));
-  HIPCHK(ctx, hipEventRecord(ps.done, ps.stream));
+  // from here on an error must drain the stream first: the queued kernels read the staging
+  hipError_t e = hout_dev ? hipSuccess : hipMemcpyAsync(ps.h_out.p, dout, 65 * (size_t)m, hipMemcpyDeviceToHost, ps.stream);
+  if (e == hipSuccess) e = hipEventRecord(ps.done, ps.stream);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(ps.stream);
+    return set_err(ctx, MV_E_HIP, std::string("block pass: ") + hipGetErrorString(e));
+  }
   ps.it = it;
   ps.lo = lo;
   ps.m = m;
@@ -1554,37 +1554,47 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     const int v = e ? atoi(e) : 17;
     return v < 8 ? 8 : (v > 24 ? 24 : v);
   }();
-  static const uint64_t min_batches = [] {  // MV_STREAM_BATCHES (experiments): batches per call, at least
-    const char* e = getenv("MV_STREAM_BATCHES");
-    const int v = e ? atoi(e) : 2;
-    return (uint64_t)(v < 1 ? 1 : v);
-  }();
   const uint64_t m = hi - lo;
-  // at least two batches, on alternating compute streams: batch t's sort, buckets and tail
-  // run beside batch t + 1's copy and preparation
-  uint64_t nb = std::max<uint64_t>(min_batches, (m + ctx->max_batch - 1) / ctx->max_batch);
-  uint64_t bs64 = ((m + nb - 1) / nb + 1023) & ~1023ull;
-  if (bs64 < MV_BATCH_MIN) bs64 = MV_BATCH_MIN;
-  if (bs64 > ctx->max_batch) bs64 = ctx->max_batch;
-  uint32_t bs = (uint32_t)bs64;
-  // the first batch's share (MV_STREAM_FIRST, A/B): a larger first batch shortens the last
-  // batch's sort, buckets and tail, which follow the last copy
-  static const double first_frac = [] {  // default 0.7: 199.5 vs 191.6 M/s at 0.5 (same box)
-    const char* e = getenv("MV_STREAM_FIRST");
-    const double v = e ? atof(e) : 0.7;
-    return v > 0.0 && v < 1.0 ? v : 0.0;
+  // Batch sizes: shares of the call (MV_STREAM_FRACS, separated by ',' or '/'; default 0.7,0.3). The
+  // last batch's prep, sort, buckets and tail follow the last copy, so the shares decrease;
+  // every batch is whole 1,024s, >= MV_BATCH_MIN and <= max_batch (more batches when needed).
+  static const std::vector<double> fracs = [] {
+    std::vector<double> v;
+    const char* e = getenv("MV_STREAM_FRACS");
+    std::string x = e ? e : "0.7,0.3";
+    size_t q = 0;
+    while (q < x.size()) {
+      size_t c = x.find_first_of(",/", q);
+      if (c == std::string::npos) c = x.size();
+      const double f = atof(x.substr(q, c - q).c_str());
+      if (f > 0.0) v.push_back(f);
+      q = c + 1;
+    }
+    if (v.empty()) v.push_back(1.0);
+    return v;
   }();
-  uint32_t b0 = bs;
-  if (first_frac > 0.0 && nb == 2) {
-    uint64_t f = ((uint64_t)(m * first_frac) + 1023) & ~1023ull;
-    if (f < MV_BATCH_MIN) f = MV_BATCH_MIN;
-    if (f > ctx->max_batch) f = ctx->max_batch;
-    if (f < m && m - f >= MV_BATCH_MIN && m - f <= ctx->max_batch) {
-      b0 = (uint32_t)f;
-      bs = (uint32_t)std::max<uint64_t>(m - f, 1);
+  std::vector<uint32_t> sizes;
+  {
+    double tot = 0.0;
+    for (double f : fracs) tot += f;
+    uint64_t done = 0;
+    for (size_t k = 0; k < fracs.size() && done < m; k++) {
+      uint64_t want = k + 1 == fracs.size() ? m - done : (((uint64_t)(m * fracs[k] / tot)) + 1023) & ~1023ull;
+      if (want < MV_BATCH_MIN) want = MV_BATCH_MIN;
+      if (want > m - done) want = m - done;
+      if (m - done - want > 0 && m - done - want < MV_BATCH_MIN) want = m - done;  // no runt batch
+      if (want > ctx->max_batch) want = ctx->max_batch;
+      done += want;
+      sizes.push_back((uint32_t)want);
+    }
+    while (done < m) {  // larger than the shares allow (max_batch): whole max_batch batches
+      const uint64_t want = std::min<uint64_t>(m - done, ctx->max_batch);
+      sizes.push_back((uint32_t)want);
+      done += want;
     }
   }
-  const uint32_t cap = std::max(b0, bs);
+  uint32_t cap = 0;
+  for (uint32_t z : sizes) cap = std::max(cap, z);
   uint32_t chunk = 1u << chunk_log2;
   while ((cap + chunk - 1) / chunk > (uint32_t)Device::kMaxChunks / 2) chunk <<= 1;
   // chunk schedule: the first batch starts with small chunks (2^14, 2^15, ... signatures), so
@@ -1600,8 +1610,9 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     sched[b].push_back(cap);
   }
   const size_t kb = pk ? 32 : 4;  // pk rows or committee key indices
-  for (int b = 0; b < 2; b++) {
+  for (int b = 0; b < 2; b++)
     if (!dev.pstream[b]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[b], hipStreamNonBlocking));
+  for (int b = 0; b < Device::kPinBufs; b++) {
     if (!dev.pin_free[b]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[b], hipEventDisableTiming));
     for (int c = 0; c < Device::kMaxChunks; c++)
       if (!dev.chunk_ev[b][c]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.chunk_ev[b][c], hipEventDisableTiming));
@@ -1612,17 +1623,18 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   }
   HIPCHK(ctx, dev.h_out.ensure(m));
   uint8_t* hst = dev.h_out.as<uint8_t>();
-  // copies on the device stream (idle here: calls are serialised by ctx->mu); batch t computes on
-  // pstream[t & 1]. mv_create makes these three streams first, so they sit on three distinct
-  // hardware queues (GPU_MAX_HW_QUEUES = 4; later streams share queues round-robin, and a copy
-  // queued behind another stream's kernels would serialise the pipeline)
+  // copies on the device stream (host-buffer signature calls are serialised by ctx->mu, and the
+  // block passes have streams of their own); batch t computes on pstream[t & 1]. mv_create makes
+  // these three streams first, so they sit on three distinct hardware queues (GPU_MAX_HW_QUEUES
+  // = 4; later streams share queues round-robin, and a copy queued behind another stream's
+  // kernels would serialise the pipeline)
   hipStream_t xs = dev.stream;
-  uint64_t t = 0;
-  for (uint64_t i = lo; i < hi; i += (t == 0 ? b0 : bs), t++) {
-    const int b = (int)(t & 1);
-    hipStream_t cs = dev.pstream[b];
-    const uint32_t k = (uint32_t)std::min<uint64_t>(t == 0 ? b0 : bs, hi - i);
-    // buffer b is free once batch t - 2 (or the previous call's last batch on it) is done
+  uint64_t i = lo;
+  for (size_t t = 0; t < sizes.size(); i += sizes[t], t++) {
+    const int b = (int)(t % Device::kPinBufs);
+    hipStream_t cs = dev.pstream[t & 1];
+    const uint32_t k = sizes[t];
+    // buffer b is free once batch t - kPinBufs (or the previous call's batch on it) is done
     HIPCHK(ctx, hipStreamWaitEvent(xs, dev.pin_free[b], 0));
     const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);
     const std::vector<uint32_t>& cut = sched[t == 0 ? 0 : 1];
@@ -1793,12 +1805,14 @@ void mv_destroy(mv_ctx* ctx) {
       if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.sscr_done)
       if (ev) (void)hipEventDestroy(ev);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < Device::kPinBufs; k++) {
       for (DevBuf* b : {&dev.pin_msg[k], &dev.pin_sig[k], &dev.pin_pk[k], &dev.pin_st[k]}) b->release();
-      dev.h_stage[k].release();
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
       for (hipEvent_t ev : dev.chunk_ev[k])
         if (ev) (void)hipEventDestroy(ev);
+    }
+    for (int k = 0; k < 2; k++) {
+      dev.h_stage[k].release();
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);

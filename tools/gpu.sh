@@ -18,6 +18,7 @@
 #   gpus2            --gpus 2 rehearsal (both ranks on the one GPU)
 #   ab:V[:ARGS]      config-2 line, product library vs experiment build V (MV_LIB), 2 interleaved reps
 #   abc4:V[:ARGS]    the same on config 4
+#   e2e[:ENV=V,..]   tools/e2e_probe.py (pinned end-to-end signatures) under these settings
 #   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c4, c4s1, c5, wal}
 #   pmc:W[:KERNELS]  separate --pmc passes (one counter group per run) of W in {c2s1, c4s1, wal} and
 #                    tools/pmc_summary.py for each kernel (comma-separated)
@@ -118,6 +119,9 @@ for T in "$@"; do
           line "$OUT/${name}_${lib}_$rep.json"
         done
       done ;;
+    e2e)  # e2e[:ENV=V,ENV=V]: the pinned end-to-end probe under these environment settings
+      (export ${arg//,/ }; timeout -k 10 300 python tools/e2e_probe.py) >> "$OUT/e2e.log" 2>&1 || { echo "e2e FAILED"; tail -5 "$OUT/e2e.log"; exit 1; }
+      tail -1 "$OUT/e2e.log" ;;
     trace)
       cmd=${W[$arg]}
       [ -n "$cmd" ] || { echo "unknown workload $arg"; exit 1; }
