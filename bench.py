@@ -165,7 +165,7 @@ def main():
                     help="skip the config-4 (100-validator blocks) rate in the default line")
     ap.add_argument("--config4-batch", type=int, default=1 << 21,
                     help="config-4 blocks per GPU per step (2^21: BASELINE config 4's 16M blocks over 8 GPUs)")
-    ap.add_argument("--host-fed-blocks", type=int, default=1 << 18,
+    ap.add_argument("--host-fed-blocks", type=int, default=1 << 17,
                     help="config 4's PCIe-inclusive leg: blocks fed from host memory (0 disables)")
     ap.add_argument("--no-config5", dest="config5", action="store_false",
                     help="skip the config-5 (online latency) key of the default line")

@@ -447,22 +447,29 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
   comb16_wg(blockIdx.x, msg, sig, pk, key_idx, n, combB, combA, key_ok, status, bv, hin, ing);
 }
 
-// The resident online service (kernels.h OnlineReq / OnlineCtl / OnlineDev). Every branch
-// around a barrier is uniform (the role is the workgroup's, the decision is broadcast through
-// LDS), and every exit test is made on each idle iteration, so all waves leave together.
-constexpr uint32_t ON_DW = sizeof(mvk::OnlineReq) / 4;
-static_assert(ON_DW <= C16_THREADS && sizeof(mvk::OnlineReq) % 16 == 0, "one dword per thread");
+// The resident online service (kernels.h OnlineArgs). Every branch around a barrier is
+// uniform (the role is the workgroup's, decisions are broadcast through LDS), and every wait
+// loop also tests the launch's end, so all waves leave.
 constexpr uint32_t ON_BATCH = 32;  // requests the poller moves per pass
 
 MV_DEV uint64_t on_now() { return (uint64_t)wall_clock64(); }
 
-// Workgroup 0: moves published requests from page-locked memory into HBM and advances ready.
-MV_DEV void online_poller(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs, mvk::OnlineDev* dev, uint64_t idle_ticks,
-                          uint64_t max_ticks) {
-  __shared__ uint32_t sh[4];                // kind (0 idle, 1 move, 2 exit), first request lo / hi, count
-  __shared__ uint32_t pre[ON_BATCH + 1];    // 16-B chunk prefix over the batch's inputs
+// Workgroup 0: moves published requests from page-locked memory into HBM, appends their jobs.
+MV_DEV void online_poller(const mvk::OnlineArgs& A) {
+  mvk::OnlineCtl* ctl = A.ctl;
+  mvk::OnlineDev* dev = A.dev;
+  __shared__ uint32_t sh[4];              // kind (0 idle, 1 move, 2 exit), first request lo / hi, count
+  __shared__ uint32_t pre[ON_BATCH + 1];  // 16-B chunk prefix over the batch's inputs
+  __shared__ uint32_t nblk[ON_BATCH];
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
+  uint64_t t_busy = t_start;
+  if (t == 0) {  // this launch's setup: tickets of earlier launches are void
+    const unsigned long long tl = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dev->jobs_head, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dev->quit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dev->epoch, A.launch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (;;) {
     if (t < 64) {  // wave 0: how many consecutive requests from `ready` are published
       uint32_t kind = 0, cnt = 0;
@@ -471,19 +478,32 @@ MV_DEV void online_poller(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs, mvk::
       const uint64_t avail = tail > rdy ? tail - rdy : 0;
       const uint64_t m = avail < ON_BATCH ? avail : ON_BATCH;
       bool ok = false;
+      uint32_t nb = 0, cb = 0;
       if (t < m) {
         const uint64_t q = rdy + t;
-        ok = __hip_atomic_load(&reqs[q % mvk::ONLINE_SLOTS].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
+        const mvk::OnlineReq* r = A.reqs + (q % mvk::ONLINE_SLOTS);
+        ok = __hip_atomic_load(&r->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
+        if (ok) {
+          nb = r->n;
+          cb = r->copy_bytes;
+        }
       }
       const uint64_t notok = __ballot(!ok);  // lanes >= m count as not ready
       cnt = notok ? (uint32_t)__builtin_ctzll(notok) : 64u;
       if (cnt > m) cnt = (uint32_t)m;
       const uint64_t now = on_now();
+      if (t < cnt) {
+        nblk[t] = nb;
+        pre[t] = (cb + 15) / 16;  // chunk count, prefixed below
+        __hip_atomic_store(&ctl->trace[(rdy + t) % mvk::ONLINE_SLOTS][0], now, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       if (cnt) {
         kind = 1;
-      } else if (__hip_atomic_load(&dev->live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 ||
-                 now - t_start > max_ticks + idle_ticks) {
-        kind = 2;  // every worker has left (or a worker-less launch outlived its limits)
+        t_busy = now;
+      } else if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                 now - t_busy > A.idle_ticks || now - t_start > A.max_ticks) {
+        kind = 2;
       }
       if (t == 0) {
         sh[0] = kind;
@@ -495,23 +515,21 @@ MV_DEV void online_poller(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs, mvk::
     __syncthreads();
     const uint32_t kind = sh[0], cnt = sh[3];
     const uint64_t rdy = (uint64_t)sh[1] | ((uint64_t)sh[2] << 32);
-    __syncthreads();
-    if (kind == 2) return;
+    if (kind == 2) {
+      if (t == 0) __hip_atomic_store(&dev->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     if (kind == 0) {
+      __syncthreads();  // sh[] is rewritten by the next pass only after every wave read it
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    // descriptors: dword w of request i by thread i * ON_DW + w
-    for (uint32_t x = t; x < cnt * ON_DW; x += blockDim.x) {
-      const uint32_t i = x / ON_DW, w = x % ON_DW, slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS);
-      reinterpret_cast<uint32_t*>(&dev->desc[slot])[w] = reinterpret_cast<const uint32_t*>(&reqs[slot])[w];
-    }
-    __syncthreads();  // the HBM descriptors are read back below (workgroup scope)
     if (t == 0) {
       uint32_t c = 0;
       for (uint32_t i = 0; i < cnt; i++) {
+        const uint32_t k = pre[i];
         pre[i] = c;
-        c += (dev->desc[(rdy + i) % mvk::ONLINE_SLOTS].copy_bytes + 15) / 16;
+        c += k;
       }
       pre[cnt] = c;
     }
@@ -521,60 +539,73 @@ MV_DEV void online_poller(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs, mvk::
     for (uint32_t k = t; k < total; k += blockDim.x) {
       uint32_t i = 0;
       while (pre[i + 1] <= k) i++;
-      const mvk::OnlineReq& d = dev->desc[(rdy + i) % mvk::ONLINE_SLOTS];
-      const uint32_t c = k - pre[i];
-      reinterpret_cast<uint4*>(d.in_dev)[c] = reinterpret_cast<const uint4*>(d.in_host)[c];
+      const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS), c = k - pre[i];
+      reinterpret_cast<uint4*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot)[c] =
+          reinterpret_cast<const uint4*>(A.in_host + mvk::ONLINE_IN_STRIDE * slot)[c];
     }
-    __threadfence();  // the copies before ready (agent scope)
+    __threadfence();  // the inputs before the jobs (agent scope)
     __syncthreads();
     if (t == 0) {
+      unsigned long long jt = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (uint32_t i = 0; i < cnt; i++) {
-        const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS);
-        dev->nj[slot] = (dev->desc[slot].n + C16_SIGS - 1) / C16_SIGS;
+        const uint64_t q = rdy + i;
+        const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS), nj = (nblk[i] + C16_SIGS - 1) / C16_SIGS;
+        dev->n[slot] = nblk[i];
+        if (nj == 0)  // a void request: complete it here
+          __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (uint32_t j = 0; j < nj; j++, jt++) dev->jobs[jt % mvk::ONLINE_JOBS] = ((unsigned long long)q << 8) | j;
       }
-      __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + cnt), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dev->jobs_tail, jt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (t < cnt)
+      __hip_atomic_store(&ctl->trace[(rdy + t) % mvk::ONLINE_SLOTS][1], on_now(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();  // pre[] / nblk[] / sh[] are rewritten by the next pass
   }
 }
 
-// Workgroups 1..: claim a job from the ticket, run it from HBM, hand its outputs to the host.
-MV_DEV void online_worker(mvk::OnlineCtl* ctl, mvk::OnlineDev* dev, const uint4* __restrict__ combB,
-                          const uint4* __restrict__ combA, const uint8_t* __restrict__ key_ok,
-                          const uint8_t* __restrict__ pk, uint64_t idle_ticks, uint64_t max_ticks) {
-  constexpr uint32_t JB = mvk::ONLINE_JOB_BITS, JM = (1u << JB) - 1u;
-  __shared__ uint32_t job[4];  // kind (0 idle, 1 work, 2 exit), request lo / hi, job
-  __shared__ uint32_t dsc[ON_DW];
+// Workgroups 1..: take a ticket, wait until the ring's tail passes it, run that job from HBM,
+// hand its outputs to the host.
+MV_DEV void online_worker(const mvk::OnlineArgs& A) {
+  mvk::OnlineCtl* ctl = A.ctl;
+  mvk::OnlineDev* dev = A.dev;
+  __shared__ uint32_t job[4];  // kind (1 work, 2 exit), request lo / hi, job
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
-  uint64_t t_busy = t_start;
+  bool setup = false;
   for (;;) {
     if (t == 0) {
-      uint32_t kind = 0, j = 0;
+      uint32_t kind = 2, j = 0;
       uint64_t q = 0;
-      for (int tries = 0; tries < 256; tries++) {
-        unsigned long long cur = __hip_atomic_load(&dev->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        q = cur >> JB;
-        j = (uint32_t)(cur & JM);
-        if (q >= __hip_atomic_load(&dev->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) break;
-        const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
-        const uint32_t nj = dev->nj[slot];
-        const unsigned long long next = j + 1 < nj ? cur + 1 : (unsigned long long)(q + 1) << JB;
-        if (__hip_atomic_compare_exchange_strong(&dev->ticket, &cur, next, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          if (nj == 0) {  // a void request: complete it here
-            __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            continue;
-          }
-          kind = 1;
+      while (!setup) {  // the poller has voided earlier tickets
+        if (__hip_atomic_load(&dev->epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == A.launch) {
+          setup = true;
+        } else if (on_now() - t_start > A.max_ticks + A.idle_ticks) {
           break;
+        } else {
+          __builtin_amdgcn_s_sleep(2);
         }
       }
-      const uint64_t now = on_now();
-      if (kind == 1) {
-        t_busy = now;
-      } else if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
-                 now - t_busy > idle_ticks || now - t_start > max_ticks) {
-        kind = 2;
+      if (setup) {
+        const unsigned long long tk = __hip_atomic_fetch_add(&dev->jobs_head, 1ull, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+          if (tk < __hip_atomic_load(&dev->jobs_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+            const unsigned long long e = dev->jobs[tk % mvk::ONLINE_JOBS];
+            q = e >> 8;
+            j = (uint32_t)(e & 0xffu);
+            kind = 1;
+            break;
+          }
+          if (__hip_atomic_load(&dev->quit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+              on_now() - t_start > A.max_ticks + A.idle_ticks)
+            break;  // the launch is over (this ticket is voided by the next launch)
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (kind == 1 && j == 0)
+          __hip_atomic_store(&ctl->trace[q % mvk::ONLINE_SLOTS][2], on_now(), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
       }
       job[0] = kind;
       job[1] = (uint32_t)q;
@@ -584,59 +615,62 @@ MV_DEV void online_worker(mvk::OnlineCtl* ctl, mvk::OnlineDev* dev, const uint4*
     __syncthreads();
     const uint32_t kind = job[0];
     const uint64_t q = (uint64_t)job[1] | ((uint64_t)job[2] << 32);
-    const uint32_t j = job[3];
-    if (kind == 1 && t < ON_DW)  // the HBM descriptor into LDS, then into scalar registers
-      dsc[t] = reinterpret_cast<const uint32_t*>(&dev->desc[q % mvk::ONLINE_SLOTS])[t];
-    __syncthreads();  // also: job[] is rewritten by the next claim only after every wave read it
-    if (kind == 2) {
-      if (t == 0) __hip_atomic_fetch_sub(&dev->live, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    if (kind == 0) {
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    mvk::OnlineReq d;
-    uint32_t* dw = reinterpret_cast<uint32_t*>(&d);
-#pragma unroll
-    for (uint32_t k = 0; k < ON_DW; k++) dw[k] = __builtin_amdgcn_readfirstlane(dsc[k]);
-    const uint32_t ju = __builtin_amdgcn_readfirstlane(j);
-    comb16_wg(ju, d.msg, d.sig, pk, d.key_idx, d.n, combB, combA, key_ok, d.sst, d.bv, d.hin, d.ing);
+    const uint32_t j = __builtin_amdgcn_readfirstlane(job[3]);
+    __syncthreads();  // job[] is rewritten by the next claim only after every wave read it
+    if (kind == 2) return;
+    const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(q % mvk::ONLINE_SLOTS));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(dev->n[slot]);
+    // the slot's HBM scratch (kernels.h layout): everything below is uniform address arithmetic
+    uint8_t* sc = A.scr + mvk::ONLINE_SCR_STRIDE * slot;
+    const uint64_t* off = reinterpret_cast<const uint64_t*>(sc);
+    uint8_t* out = sc + mvk::ONLINE_O_OUT;
+    uint8_t* md = out;
+    uint8_t* bd = out + 32 * mvk::ONLINE_MAX_BLOCKS;
+    uint8_t* st = out + 64 * mvk::ONLINE_MAX_BLOCKS;
+    uint8_t* stage = sc + mvk::ONLINE_O_STAGE;
+    uint64_t* poff = reinterpret_cast<uint64_t*>(sc + mvk::ONLINE_O_POFF);
+    uint64_t* plen = reinterpret_cast<uint64_t*>(sc + mvk::ONLINE_O_PLEN);
+    uint8_t* sig = sc + mvk::ONLINE_O_SIG;
+    uint32_t* kidx = reinterpret_cast<uint32_t*>(sc + mvk::ONLINE_O_KIDX);
+    uint32_t* facts = reinterpret_cast<uint32_t*>(sc + mvk::ONLINE_O_FACTS);
+    uint8_t* claimed = sc + mvk::ONLINE_O_CLAIMED;
+    const mvk::BlockVerdictOut bv{facts, claimed, md, bd, st};
+    const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
+    const mvk::BlockIngestIn ing{sc + 16 * (size_t)n, off, off + n, A.stakes, A.n_auth, A.epoch, A.quorum_thr,
+                                 stage, poff, plen, sig, kidx, facts, claimed};
+    comb16_wg(j, md, sig, A.pk, kidx, n, (const uint4*)A.combB, (const uint4*)A.combA, A.key_ok,
+              sc + mvk::ONLINE_O_SST, bv, hin, ing);
     __syncthreads();  // the job's digests and verdicts are in HBM (workgroup scope)
     // this job's blocks: md and bd (8 words each), status -> page-locked output
-    const uint32_t b0 = ju * C16_SIGS, nb = d.n - b0 < C16_SIGS ? d.n - b0 : C16_SIGS;
+    uint8_t* oh = A.out_host + mvk::ONLINE_OUT_STRIDE * slot;
+    const uint32_t b0 = j * C16_SIGS, nb = n - b0 < C16_SIGS ? n - b0 : C16_SIGS;
     if (t < 16 * nb) {
       const uint32_t b = b0 + t / 16, w = t % 16;  // words 0..7 md, 8..15 bd
       const size_t o = w < 8 ? 32 * (size_t)b + 4 * w : 32 * ((size_t)mvk::ONLINE_MAX_BLOCKS + b) + 4 * (w - 8);
-      *reinterpret_cast<uint32_t*>(d.out_host + o) = *reinterpret_cast<const uint32_t*>(d.out_dev + o);
+      *reinterpret_cast<uint32_t*>(oh + o) = *reinterpret_cast<const uint32_t*>(out + o);
     } else if (t >= 64 && t < 64 + nb) {
       const size_t o = 64 * (size_t)mvk::ONLINE_MAX_BLOCKS + b0 + (t - 64);
-      d.out_host[o] = d.out_dev[o];
+      oh[o] = out[o];
     }
     __threadfence_system();  // the outputs before the done word
     __syncthreads();
     if (t == 0) {
-      const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
-      const uint32_t nj = (d.n + C16_SIGS - 1) / C16_SIGS;
+      const uint32_t nj = (n + C16_SIGS - 1) / C16_SIGS;
       const uint32_t prev = __hip_atomic_fetch_add(&dev->jobs_done[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (prev + 1 == nj) {
         __hip_atomic_store(&dev->jobs_done[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl->trace[slot][3], on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
 }
 
-__global__ void __launch_bounds__(C16_THREADS) k_online(mvk::OnlineCtl* ctl, const mvk::OnlineReq* reqs,
-                                                        mvk::OnlineDev* dev, const uint4* __restrict__ combB,
-                                                        const uint4* __restrict__ combA,
-                                                        const uint8_t* __restrict__ key_ok,
-                                                        const uint8_t* __restrict__ pk, uint64_t idle_ticks,
-                                                        uint64_t max_ticks) {
+__global__ void __launch_bounds__(C16_THREADS) k_online(const mvk::OnlineArgs A) {
   if (blockIdx.x == 0)
-    online_poller(ctl, reqs, dev, idle_ticks, max_ticks);
+    online_poller(A);
   else
-    online_worker(ctl, dev, combB, combA, key_ok, pk, idle_ticks, max_ticks);
+    online_worker(A);
 }
 
 // The same predicate split in two, for small batches of long blocks (config 5, 8-KB
@@ -839,14 +873,9 @@ hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint
   return hipGetLastError();
 }
 
-hipError_t launch_online(OnlineCtl* ctl, const OnlineReq* reqs, OnlineDev* dev, uint32_t grid, const void* combB,
-                         const void* combA, const uint8_t* key_ok, const uint8_t* pk, uint64_t idle_ticks,
-                         uint64_t max_ticks, hipStream_t s) {
+hipError_t launch_online(const OnlineArgs& a, uint32_t grid, hipStream_t s) {
   if (grid < 2) return hipErrorInvalidValue;  // a poller and at least one worker
-  hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&dev->live), (int)(grid - 1), 1, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mv::k_online, dim3(grid), dim3(mv::C16_THREADS), 0, s, ctl, reqs, dev, (const uint4*)combB,
-                     (const uint4*)combA, key_ok, pk, idle_ticks, max_ticks);
+  hipLaunchKernelGGL(mv::k_online, dim3(grid), dim3(mv::C16_THREADS), 0, s, a);
   return hipGetLastError();
 }
 

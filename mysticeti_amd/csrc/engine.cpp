@@ -1002,13 +1002,9 @@ bool committee_ready(mv_ctx* ctx) {
 // mask (a queue of its own, so kernels on other streams never wait behind it; and a bounded
 // share of the chip), and exits after MV_ONLINE_IDLE_US (default 2,000) without a job.
 constexpr uint32_t kOnSlots = mvk::ONLINE_SLOTS, kOnMax = mvk::ONLINE_MAX_BLOCKS;
-constexpr size_t kOnInCap = 128u << 10;                         // bincode bytes per request
-constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-constexpr size_t kOnInStride = al256(16 * kOnMax + kOnInCap + 64);  // off[n] | len[n] | bincode | 16 zero B
-constexpr size_t kOnOutStride = al256(65 * kOnMax);                 // md[64] | bd[64] | status[64]
-constexpr size_t kOnStage = al256(kOnInCap + 4096);
-constexpr size_t kOnScrStride = kOnInStride + kOnOutStride + kOnStage + 2 * al256(8 * kOnMax) + al256(64 * kOnMax) +
-                                2 * al256(4 * kOnMax) + al256(32 * kOnMax) + al256(kOnMax);
+constexpr size_t kOnInCap = mvk::ONLINE_IN_CAP;        // bincode bytes per request
+constexpr size_t kOnInStride = mvk::ONLINE_IN_STRIDE;  // off[n] | len[n] | bincode | 16 zero B
+constexpr size_t kOnOutStride = mvk::ONLINE_OUT_STRIDE;  // md[64] | bd[64] | status[64]
 
 struct OnlineSvc {
   std::mutex mu;
@@ -1023,12 +1019,19 @@ struct OnlineSvc {
   DevBuf dctl, scr;
   std::unique_ptr<std::atomic<uint64_t>[]> freed;  // slot released by its owner: request + 1
   uint64_t next_q = 0;
-  uint32_t grid = 0;
+  uint32_t grid = 0, launch_no = 0;
   std::atomic<uint64_t> requests{0}, launches{0};
   // steady_clock ns of the last request seen done: a kernel that finished a request less than
   // half its idle limit ago is still live (no runtime query on the request path)
   std::atomic<int64_t> last_done_ns{0};
   uint64_t idle_us = 2000;
+  // MV_ONLINE_TRACE: per-stage sums (us) -- host publish to done seen, and on the kernel's
+  // clock seen -> ready -> first claim -> last job done -- printed at release
+  bool trace = false;
+  double ticks_per_us = 100.0;
+  std::mutex tr_mu;
+  double tr_sum[5] = {0, 0, 0, 0, 0};
+  uint64_t tr_n = 0;
 };
 
 int64_t steady_ns() {
@@ -1075,7 +1078,7 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   HIPCHK(ctx, host((void**)&o.out, &o.out_d, kOnOutStride * kOnSlots));
   HIPCHK(ctx, o.dctl.ensure(sizeof(mvk::OnlineDev)));
   HIPCHK(ctx, hipMemset(o.dctl.p, 0, sizeof(mvk::OnlineDev)));
-  HIPCHK(ctx, o.scr.ensure(kOnScrStride * kOnSlots));
+  HIPCHK(ctx, o.scr.ensure(mvk::ONLINE_SCR_STRIDE * kOnSlots));
   o.freed.reset(new std::atomic<uint64_t>[kOnSlots]);
   for (uint32_t k = 0; k < kOnSlots; k++) o.freed[k].store(0);
   // CU mask: MV_ONLINE_CUS (default 64) CUs spread evenly over the chip; 0 = an ordinary stream
@@ -1095,6 +1098,14 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     HIPCHK(ctx, hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking));
   }
   HIPCHK(ctx, hipEventCreateWithFlags(&o.exited, hipEventDisableTiming));
+  o.trace = getenv("MV_ONLINE_TRACE") != nullptr;
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev.id) == hipSuccess && khz > 0)
+      o.ticks_per_us = khz / 1000.0;
+    else
+      (void)hipGetLastError();
+  }
   const char* ge = getenv("MV_ONLINE_WGS");  // resident workgroups (4-block jobs in flight)
   o.grid = (uint32_t)(ge ? std::max(2, atoi(ge)) : (want > 0 ? want : 64));  // >= 2: the poller + workers
   o.ready = true;
@@ -1127,9 +1138,26 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     khz = 100000;
   }
   const uint64_t per_us = (uint64_t)khz / 1000 ? (uint64_t)khz / 1000 : 1;
-  HIPCHK(ctx, mvk::launch_online((mvk::OnlineCtl*)o.ctl_d, (const mvk::OnlineReq*)o.req_d, o.dctl.as<mvk::OnlineDev>(),
-                                 o.grid, dev.combB.p, dev.combA.p, dev.keyok.as<uint8_t>(),
-                                 dev.committee_pk.as<uint8_t>(), idle_us * per_us, 60000000ull * per_us, o.stream));
+  mvk::OnlineArgs a{};
+  a.ctl = (mvk::OnlineCtl*)o.ctl_d;
+  a.reqs = (const mvk::OnlineReq*)o.req_d;
+  a.dev = o.dctl.as<mvk::OnlineDev>();
+  a.in_host = static_cast<const uint8_t*>(o.in_d);
+  a.out_host = static_cast<uint8_t*>(o.out_d);
+  a.scr = o.scr.as<uint8_t>();
+  a.combB = dev.combB.p;
+  a.combA = dev.combA.p;
+  a.key_ok = dev.keyok.as<uint8_t>();
+  a.pk = dev.committee_pk.as<uint8_t>();
+  a.stakes = dev.stakes.as<uint64_t>();
+  const mvh::Committee& com = ctx->committee;  // fixed while the launch lives (mv_set_committee stops it)
+  a.epoch = com.epoch;
+  a.quorum_thr = com.quorum_threshold;
+  a.n_auth = (uint32_t)com.size();
+  a.launch = ++o.launch_no;
+  a.idle_ticks = idle_us * per_us;
+  a.max_ticks = 60000000ull * per_us;
+  HIPCHK(ctx, mvk::launch_online(a, o.grid, o.stream));
   HIPCHK(ctx, hipEventRecord(o.exited, o.stream));
   o.launched = true;
   o.launches++;
@@ -1147,6 +1175,14 @@ void online_stop(OnlineSvc& o) {
 
 void online_release(OnlineSvc& o) {
   online_stop(o);
+  if (o.trace && o.tr_n) {
+    const double n = (double)o.tr_n;
+    fprintf(stderr,
+            "[online] %llu requests, mean us: host publish->done seen %.1f | kernel: seen->ready %.1f, "
+            "ready->claim %.1f, claim->done %.1f, seen->done %.1f\n",
+            (unsigned long long)o.tr_n, o.tr_sum[0] / n, o.tr_sum[1] / n, o.tr_sum[2] / n, o.tr_sum[3] / n,
+            o.tr_sum[4] / n);
+  }
   if (o.stream) (void)hipStreamDestroy(o.stream);
   if (o.exited) (void)hipEventDestroy(o.exited);
   for (void* h : {(void*)o.ctl, (void*)o.req, (void*)o.in, (void*)o.out})
@@ -1199,43 +1235,10 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
   memset(bytes + pos, 0, 16);  // 16 readable zero bytes past the last block
   const uint32_t copy_bytes = (uint32_t)((16 * (size_t)n + pos + 16 + 15) & ~(size_t)15);
   uint8_t* out = o.out + kOnOutStride * slot;
-  char* sc = o.scr.as<char>() + kOnScrStride * slot;
-  size_t so = 0;
-  auto take = [&](size_t b) {
-    char* p = sc + so;
-    so += al256(b);
-    return p;
-  };
-  uint8_t* in_dev = (uint8_t*)take(kOnInStride);
-  uint8_t* out_dev = (uint8_t*)take(kOnOutStride);
-  uint8_t* stage = (uint8_t*)take(kOnStage);
-  uint64_t* poff = (uint64_t*)take(8 * kOnMax);
-  uint64_t* plen = (uint64_t*)take(8 * kOnMax);
-  uint8_t* sig = (uint8_t*)take(64 * kOnMax);
-  uint32_t* kidx = (uint32_t*)take(4 * kOnMax);
-  uint32_t* facts = (uint32_t*)take(4 * kOnMax);
-  uint8_t* claimed = (uint8_t*)take(32 * kOnMax);
-  uint8_t* sst = (uint8_t*)take(kOnMax);
-  uint8_t* dmd = out_dev;
-  uint8_t* dbd = out_dev + 32 * kOnMax;
-  uint8_t* dst = out_dev + 64 * kOnMax;
-  const uint64_t* doff = reinterpret_cast<const uint64_t*>(in_dev);
-  const mvh::Committee& com = ctx->committee;
   mvk::OnlineReq& r = o.req[slot];
   r.n = n;
   r.copy_bytes = copy_bytes;
-  r.in_host = static_cast<const uint8_t*>(o.in_d) + kOnInStride * slot;
-  r.in_dev = in_dev;
-  r.out_host = static_cast<uint8_t*>(o.out_d) + kOnOutStride * slot;
-  r.out_dev = out_dev;
-  r.msg = dmd;
-  r.sig = sig;
-  r.key_idx = kidx;
-  r.sst = sst;
-  r.bv = mvk::BlockVerdictOut{facts, claimed, dmd, dbd, dst};
-  r.hin = mvk::BlockHashIn{stage, poff, plen, dmd, dbd};
-  r.ing = mvk::BlockIngestIn{in_dev + 16 * (size_t)n, doff, doff + n, dev.stakes.as<uint64_t>(), (uint32_t)com.size(),
-                             com.epoch, com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed};
+  const int64_t t_pub = o.trace ? steady_ns() : 0;
   __atomic_store_n(&r.seq, q + 1, __ATOMIC_RELEASE);  // the descriptor and the bytes above first
   // wait for the slot's done word; every ~100 us check that a kernel is still live (one that
   // exited idle just before this request was published is relaunched)
@@ -1266,6 +1269,18 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     if (rc != MV_OK) break;
   }
   if (rc != MV_OK) return rc;
+  if (o.trace) {
+    const double host_us = (steady_ns() - t_pub) / 1e3;
+    const uint64_t* tr = o.ctl->trace[slot];
+    const double k = 1.0 / o.ticks_per_us;
+    std::lock_guard<std::mutex> lk(o.tr_mu);
+    o.tr_sum[0] += host_us;
+    o.tr_sum[1] += (double)(int64_t)(tr[1] - tr[0]) * k;
+    o.tr_sum[2] += (double)(int64_t)(tr[2] - tr[1]) * k;
+    o.tr_sum[3] += (double)(int64_t)(tr[3] - tr[2]) * k;
+    o.tr_sum[4] += (double)(int64_t)(tr[3] - tr[0]) * k;
+    o.tr_n++;
+  }
   const uint8_t* ho = out;
   for (uint32_t k = 0; k < n; k++) {
     status[k] = ho[64 * kOnMax + k];

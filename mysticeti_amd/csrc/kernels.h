@@ -113,51 +113,77 @@ struct BlockIngestIn {
 // online traffic flows and runs each mv_verify_blocks request of <= ONLINE_MAX_BLOCKS short
 // blocks as k_verify_comb16's workgroups would (ingest, both digests, challenge, comb sums,
 // verdict), with no launch and no event per request.
-//   host     writes request q's input (offsets, lengths, bincode) and descriptor into ring slot
-//            q % ONLINE_SLOTS of page-locked memory, then seq = q + 1; ctl.tail >= q + 1
-//   poller   workgroup 0 polls ctl.tail, copies every request whose seq is set -- descriptor
-//            and input -- into HBM (one pass for all of them), then advances dev.ready: the
-//            only PCIe reads on the request's path
-//   workers  workgroups 1.. claim 4-block jobs from the device ticket (HBM only), run them from
-//            the HBM copies, copy their blocks' digests and verdicts to the slot's page-locked
-//            output; the request's last job stores ctl.done[slot] = q + 1 (system-scope release)
-// Workers exit after idle_ticks without a job (or on ctl.stop when idle, or after max_ticks);
-// the poller exits once every worker has.
+//   host     writes request q's input (offsets, lengths, bincode) into ring slot q % SLOTS of
+//            page-locked memory and its descriptor, then seq = q + 1; ctl.tail >= q + 1
+//   poller   workgroup 0 polls ctl.tail, copies the input of every request whose seq is set
+//            into the slot's HBM scratch (one pass for all of them) and appends the request's
+//            4-block jobs to a job ring in HBM: the only PCIe reads on the request's path
+//   workers  workgroups 1.. each hold a ticket (one atomic add on the ring's head) and start the
+//            job as soon as the ring's tail passes it, run it from HBM, copy its blocks' digests
+//            and verdicts to the slot's page-locked output; the request's last job stores
+//            ctl.done[slot] = q + 1 (system-scope release after the outputs)
+// The poller ends the launch (quit) after idle_ticks without a request, on ctl.stop, or after
+// max_ticks; workers leave when they see quit. A launch starts by discarding tickets of the
+// previous launch's workers (head = tail) before any worker takes one (epoch handshake).
+// The slot's HBM scratch layout is fixed (below), so a descriptor is 16 bytes.
 constexpr uint32_t ONLINE_SLOTS = 64;
 constexpr uint32_t ONLINE_MAX_BLOCKS = 64;  // 16 jobs per request
-constexpr uint32_t ONLINE_JOB_BITS = 5;
+constexpr uint32_t ONLINE_JOBS = 2048;      // job ring (>= SLOTS x 16)
+constexpr size_t ONLINE_IN_CAP = 128u << 10;  // bincode bytes per request
+constexpr size_t online_al(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t ONLINE_IN_STRIDE = online_al(16 * ONLINE_MAX_BLOCKS + ONLINE_IN_CAP + 64);  // off | len | bincode
+constexpr size_t ONLINE_OUT_STRIDE = online_al(65 * ONLINE_MAX_BLOCKS);  // md[64][32] | bd[64][32] | status[64]
+// slot scratch (HBM): in | out | stage | pre_off | pre_len | sig | key_idx | facts | claimed | sst
+constexpr size_t ONLINE_O_OUT = ONLINE_IN_STRIDE;
+constexpr size_t ONLINE_O_STAGE = ONLINE_O_OUT + ONLINE_OUT_STRIDE;
+constexpr size_t ONLINE_O_POFF = ONLINE_O_STAGE + online_al(ONLINE_IN_CAP + 4096);
+constexpr size_t ONLINE_O_PLEN = ONLINE_O_POFF + online_al(8 * ONLINE_MAX_BLOCKS);
+constexpr size_t ONLINE_O_SIG = ONLINE_O_PLEN + online_al(8 * ONLINE_MAX_BLOCKS);
+constexpr size_t ONLINE_O_KIDX = ONLINE_O_SIG + online_al(64 * ONLINE_MAX_BLOCKS);
+constexpr size_t ONLINE_O_FACTS = ONLINE_O_KIDX + online_al(4 * ONLINE_MAX_BLOCKS);
+constexpr size_t ONLINE_O_CLAIMED = ONLINE_O_FACTS + online_al(4 * ONLINE_MAX_BLOCKS);
+constexpr size_t ONLINE_O_SST = ONLINE_O_CLAIMED + online_al(32 * ONLINE_MAX_BLOCKS);
+constexpr size_t ONLINE_SCR_STRIDE = ONLINE_O_SST + online_al(ONLINE_MAX_BLOCKS);
 struct OnlineReq {
-  uint64_t seq;  // request number + 1 once the fields below are written (host: release store)
-  uint32_t n;    // blocks; 0 = a void request (completed without work)
-  uint32_t copy_bytes;       // input bytes of the slot (offsets, lengths, bincode + 16)
-  const uint8_t* in_host;    // the slot's input, page-locked (device view) ...
-  uint8_t* in_dev;           // ... and its HBM copy, which every pointer below refers to
-  uint8_t* out_host;         // md[64][32] | bd[64][32] | status[64], page-locked (device view)
-  uint8_t* out_dev;          // the same layout in HBM (where the kernel writes them first)
-  const uint8_t* msg;        // comb16 operands (HBM)
-  const uint8_t* sig;
-  const uint32_t* key_idx;
-  uint8_t* sst;
-  BlockVerdictOut bv;
-  BlockHashIn hin;
-  BlockIngestIn ing;
+  uint64_t seq;         // request number + 1 once the slot's input and n are written (release)
+  uint32_t n;           // blocks; 0 = a void request (completed without work)
+  uint32_t copy_bytes;  // input bytes of the slot (offsets, lengths, bincode + 16 zero bytes)
 };
 struct OnlineCtl {
   uint64_t tail;  // requests published so far
-  uint64_t stop;  // nonzero: exit when idle
+  uint64_t stop;  // nonzero: end the launch when idle
   uint64_t done[ONLINE_SLOTS];
+  // the kernel's wall clock at: the poller sees the request, its jobs are in the ring, its first
+  // job starts, its last job is done (diagnostics: MV_ONLINE_TRACE sums them per stage)
+  uint64_t trace[ONLINE_SLOTS][4];
 };
 struct OnlineDev {
-  unsigned long long ticket;  // (request << ONLINE_JOB_BITS) | next job
-  unsigned long long ready;   // requests copied to HBM by the poller
-  uint32_t live;              // workers not yet exited (set to grid - 1 before each launch)
+  unsigned long long ready;      // requests moved to HBM by the poller
+  unsigned long long jobs_head;  // next ticket
+  unsigned long long jobs_tail;  // jobs appended
+  uint32_t quit, epoch;          // quit: workers leave; epoch: the launch whose poller is set up
+  uint32_t n[ONLINE_SLOTS];
   uint32_t jobs_done[ONLINE_SLOTS];
-  uint32_t nj[ONLINE_SLOTS];  // jobs of the slot's current request
-  OnlineReq desc[ONLINE_SLOTS];
+  unsigned long long jobs[ONLINE_JOBS];  // (request << 8) | job
 };
-hipError_t launch_online(OnlineCtl* ctl, const OnlineReq* reqs, OnlineDev* dev, uint32_t grid, const void* combB,
-                         const void* combA, const uint8_t* key_ok, const uint8_t* pk, uint64_t idle_ticks,
-                         uint64_t max_ticks, hipStream_t s);
+struct OnlineArgs {
+  OnlineCtl* ctl;                 // page-locked (device view)
+  const OnlineReq* reqs;          // page-locked ring of descriptors
+  OnlineDev* dev;                 // HBM
+  const uint8_t* in_host;         // page-locked inputs, ONLINE_IN_STRIDE per slot
+  uint8_t* out_host;              // page-locked outputs, ONLINE_OUT_STRIDE per slot
+  uint8_t* scr;                   // HBM scratch, ONLINE_SCR_STRIDE per slot
+  const void* combB;
+  const void* combA;
+  const uint8_t* key_ok;
+  const uint8_t* pk;              // committee keys (32 B each)
+  const uint64_t* stakes;
+  uint64_t epoch, quorum_thr;     // the committee's
+  uint32_t n_auth;
+  uint32_t launch;                // launch number (the epoch handshake)
+  uint64_t idle_ticks, max_ticks;
+};
+hipError_t launch_online(const OnlineArgs& a, uint32_t grid, hipStream_t s);
 hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr,

@@ -18,6 +18,7 @@
 #   gpus2            --gpus 2 rehearsal (both ranks on the one GPU)
 #   ab:V[:ARGS]      config-2 line, product library vs experiment build V (MV_LIB), 2 interleaved reps
 #   abc4:V[:ARGS]    the same on config 4
+#   env:K=V          export K=V for the tasks that follow (SUF=x: later bench outputs are named <task>x.json)
 #   e2e[:ENV=V,..]   tools/e2e_probe.py (pinned end-to-end signatures) under these settings
 #   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c4, c4s1, c5, wal}
 #   pmc:W[:KERNELS]  separate --pmc passes (one counter group per run) of W in {c2s1, c4s1, wal} and
@@ -77,26 +78,26 @@ for T in "$@"; do
       run 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"
       tail -1 "$OUT/smoke.log" ;;
     bench)
-      timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench FAILED"; tail -8 "$OUT/bench.err"; exit 1; }
-      line "$OUT/bench.json" ;;
+      timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench$SUF.json" 2> "$OUT/bench$SUF.err" || { echo "bench FAILED"; tail -8 "$OUT/bench$SUF.err"; exit 1; }
+      line "$OUT/bench$SUF.json" ;;
     bench100)
-      timeout -k 10 900 python bench.py --steps 100 --warmup 5 > "$OUT/bench100.json" 2> "$OUT/bench100.err" || { echo "bench100 FAILED"; tail -8 "$OUT/bench100.err"; exit 1; }
-      line "$OUT/bench100.json" ;;
+      timeout -k 10 900 python bench.py --steps 100 --warmup 5 > "$OUT/bench100$SUF.json" 2> "$OUT/bench100$SUF.err" || { echo "bench100 FAILED"; tail -8 "$OUT/bench100$SUF.err"; exit 1; }
+      line "$OUT/bench100$SUF.json" ;;
     c2)
-      timeout -k 10 300 python bench.py --steps 600 --warmup 10 $C2ONLY ${arg//,/ } > "$OUT/c2.json" 2> "$OUT/c2.err" || { echo "c2 FAILED"; tail -8 "$OUT/c2.err"; exit 1; }
-      line "$OUT/c2.json" ;;
+      timeout -k 10 300 python bench.py --steps 600 --warmup 10 $C2ONLY ${arg//,/ } > "$OUT/c2$SUF.json" 2> "$OUT/c2$SUF.err" || { echo "c2 FAILED"; tail -8 "$OUT/c2$SUF.err"; exit 1; }
+      line "$OUT/c2$SUF.json" ;;
     c4)
-      timeout -k 10 600 python bench.py --workload config4 --steps 20 --warmup 5 --cpu-sample 0 ${arg//,/ } > "$OUT/c4.json" 2> "$OUT/c4.err" || { echo "c4 FAILED"; tail -8 "$OUT/c4.err"; exit 1; }
-      line "$OUT/c4.json" ;;
+      timeout -k 10 600 python bench.py --workload config4 --steps 20 --warmup 5 --cpu-sample 0 ${arg//,/ } > "$OUT/c4$SUF.json" 2> "$OUT/c4$SUF.err" || { echo "c4 FAILED"; tail -8 "$OUT/c4$SUF.err"; exit 1; }
+      line "$OUT/c4$SUF.json" ;;
     c5)
-      timeout -k 10 600 python bench.py --workload config5 --cpu-sample 0 --batches 2000 --conc-seconds 2 ${arg//,/ } > "$OUT/c5.json" 2> "$OUT/c5.err" || { echo "c5 FAILED"; tail -8 "$OUT/c5.err"; exit 1; }
-      line "$OUT/c5.json" ;;
+      timeout -k 10 600 python bench.py --workload config5 --cpu-sample 0 --batches 2000 --conc-seconds 2 ${arg//,/ } > "$OUT/c5$SUF.json" 2> "$OUT/c5$SUF.err" || { echo "c5 FAILED"; tail -8 "$OUT/c5$SUF.err"; exit 1; }
+      line "$OUT/c5$SUF.json" ;;
     wal)
-      timeout -k 10 600 python bench.py --workload wal --steps 20 --warmup 2 --cpu-sample 0 > "$OUT/wal.json" 2> "$OUT/wal.err" || { echo "wal FAILED"; tail -8 "$OUT/wal.err"; exit 1; }
-      line "$OUT/wal.json" ;;
+      timeout -k 10 600 python bench.py --workload wal --steps 20 --warmup 2 --cpu-sample 0 > "$OUT/wal$SUF.json" 2> "$OUT/wal$SUF.err" || { echo "wal FAILED"; tail -8 "$OUT/wal$SUF.err"; exit 1; }
+      line "$OUT/wal$SUF.json" ;;
     gpus2)
-      timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 --no-config5 --host-fed-blocks 0 --cpu-sample 0 --no-e2e --sustain-repeats 1 > "$OUT/gpus2.json" 2> "$OUT/gpus2.err" || { echo "gpus2 FAILED"; tail -8 "$OUT/gpus2.err"; exit 1; }
-      line "$OUT/gpus2.json" ;;
+      timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 --no-config5 --host-fed-blocks 0 --cpu-sample 0 --no-e2e --sustain-repeats 1 > "$OUT/gpus2$SUF.json" 2> "$OUT/gpus2$SUF.err" || { echo "gpus2 FAILED"; tail -8 "$OUT/gpus2$SUF.err"; exit 1; }
+      line "$OUT/gpus2$SUF.json" ;;
     ab|abc4)
       V=${arg%%:*}
       A=""
@@ -119,6 +120,9 @@ for T in "$@"; do
           line "$OUT/${name}_${lib}_$rep.json"
         done
       done ;;
+    env)  # env:K=V -- exported for the tasks after it
+      export "$arg"
+      echo "env $arg" ;;
     e2e)  # e2e[:ENV=V,ENV=V]: the pinned end-to-end probe under these environment settings
       (export ${arg//,/ }; timeout -k 10 300 python tools/e2e_probe.py) >> "$OUT/e2e.log" 2>&1 || { echo "e2e FAILED"; tail -5 "$OUT/e2e.log"; exit 1; }
       tail -1 "$OUT/e2e.log" ;;
