@@ -473,17 +473,20 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   for (;;) {
     if (t < 64) {  // wave 0: how many consecutive requests from `ready` are published
       uint32_t kind = 0, cnt = 0;
+      // polls are relaxed (an acquire invalidates the caches every time: the working
+      // workgroups' comb tables with them); one acquire fence once requests are seen
+      // the next ON_BATCH slots' seq words are read together (one PCIe round trip): a request is
+      // published once its seq holds its number + 1, which the host writes after its bytes
       const uint64_t rdy = __hip_atomic_load(&dev->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t tail = __hip_atomic_load(&ctl->tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint64_t avail = tail > rdy ? tail - rdy : 0;
-      const uint64_t m = avail < ON_BATCH ? avail : ON_BATCH;
+      const uint64_t m = ON_BATCH;
       bool ok = false;
       uint32_t nb = 0, cb = 0;
       if (t < m) {
         const uint64_t q = rdy + t;
         const mvk::OnlineReq* r = A.reqs + (q % mvk::ONLINE_SLOTS);
-        ok = __hip_atomic_load(&r->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
+        ok = __hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
         if (ok) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the slot's bytes after seq
           nb = r->n;
           cb = r->copy_bytes;
         }
@@ -579,7 +582,8 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
       uint32_t kind = 2, j = 0;
       uint64_t q = 0;
       while (!setup) {  // the poller has voided earlier tickets
-        if (__hip_atomic_load(&dev->epoch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == A.launch) {
+        if (__hip_atomic_load(&dev->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.launch) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           setup = true;
         } else if (on_now() - t_start > A.max_ticks + A.idle_ticks) {
           break;
@@ -590,15 +594,16 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
       if (setup) {
         const unsigned long long tk = __hip_atomic_fetch_add(&dev->jobs_head, 1ull, __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-          if (tk < __hip_atomic_load(&dev->jobs_tail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+        for (;;) {  // relaxed polls, one acquire fence when the ticket's job is there
+          if (tk < __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const unsigned long long e = dev->jobs[tk % mvk::ONLINE_JOBS];
             q = e >> 8;
             j = (uint32_t)(e & 0xffu);
             kind = 1;
             break;
           }
-          if (__hip_atomic_load(&dev->quit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+          if (__hip_atomic_load(&dev->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
               on_now() - t_start > A.max_ticks + A.idle_ticks)
             break;  // the launch is over (this ticket is voided by the next launch)
           __builtin_amdgcn_s_sleep(2);
@@ -652,7 +657,7 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
       const size_t o = 64 * (size_t)mvk::ONLINE_MAX_BLOCKS + b0 + (t - 64);
       oh[o] = out[o];
     }
-    __threadfence_system();  // the outputs before the done word
+    if (t < 128) __threadfence_system();  // the writers' outputs (waves 0, 1) before the done word
     __syncthreads();
     if (t == 0) {
       const uint32_t nj = (n + C16_SIGS - 1) / C16_SIGS;

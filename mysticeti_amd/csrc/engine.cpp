@@ -2065,6 +2065,7 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
           std::lock_guard<std::mutex> lk(ctx->mu);  // the service object (devs is fixed after mv_create)
           if (!dev.online) dev.online = std::make_shared<OnlineSvc>();
         }
+        if (dev.online->failed) goto queue_path;  // a failed service: the submission queue serves
         std::string err;
         t_err = &err;
         const mv_status rc = online_verify(ctx, dev, buf, off, len, n, status, msg_digest, block_digest);
@@ -2077,6 +2078,7 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
       }
     }
   }
+queue_path:
   // Flat combining, pipelined: the request joins the queue; a caller that finds no pass being
   // packed and a free pass set takes every queued request (its own included) into one pass,
   // packs and enqueues it, then lets the next caller pack the following pass into the other
