@@ -211,6 +211,10 @@ def main():
     import mysticeti_amd as M
     from mysticeti_amd.dist import all_ranks_ok, footprint, hbm_sample, rss_mark, shard_range, timed_region
 
+    def progress(what):  # one stderr line per leg (a long run shows it is alive)
+        if rank == 0:
+            print(f"bench: {what} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
+
     eng = M.Engine(devices=(local_rank,))
     n = args.batch
 
@@ -273,6 +277,7 @@ def main():
             ev1.record(streams[0])
         torch.cuda.synchronize(dev)
 
+    progress("corpus ready, timed region")
     elapsed = timed_region(timed_step, args.steps, close_and_sync, dist)
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # device time per step on the launch streams
     stage_ms = {}
@@ -391,6 +396,7 @@ def main():
         eng.set_batch_groups(args.groups)
 
     rss_mark("adversarial")
+    progress("adversarial done")
     # PCIe-inclusive rates (host buffers through the C ABI)
     e2e = None
     if rank == 0 and not args.no_e2e:
@@ -418,6 +424,7 @@ def main():
                "pageable": round(v_page, 1), "accepted": acc_pin, "accepted_pageable": acc_page}
 
     rss_mark("end_to_end")
+    progress("end_to_end done")
     # config 4 (the largest workload): whole-block verification of HBM-resident 100-validator
     # blocks, measured in the same run (bench_blocks.config4_measure)
     cfg4 = None
@@ -431,6 +438,7 @@ def main():
         ok = ok and cfg4["correct"]
 
     rss_mark("config4")
+    progress("config4 done")
     # f4: the WAL replay check over an HBM-resident WAL of config-4 blocks (bench_wal.wal_measure)
     walr = None
     if args.wal and args.path == "batch" and not args.corrupt:
@@ -441,6 +449,7 @@ def main():
         ok = ok and walr["correct"]
 
     rss_mark("wal")
+    progress("wal done")
     # config 5 (the online path): latency of 64-block calls and concurrent 1-block callers through
     # mv_verify_blocks on host buffers, GPU and CPU in the same run (bench_blocks.config5_measure);
     # rank 0 only (the host CPU legs would otherwise compete across ranks)
@@ -454,6 +463,7 @@ def main():
         ok = ok and cfg5["correct"]
 
     rss_mark("config5")
+    progress("config5 done")
     cpu = None
     if rank == 0 and args.cpu_sample > 0:
         cpu = cpu_baseline(d_pk.cpu().numpy(), d_sig.cpu().numpy(), msg_h, min(args.cpu_sample, n))

@@ -1158,6 +1158,9 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   a.idle_ticks = idle_us * per_us;
   a.max_ticks = 60000000ull * per_us;
   HIPCHK(ctx, mvk::launch_online(a, o.grid, o.stream));
+  if (getenv("MV_ONLINE_DEBUG"))
+    fprintf(stderr, "[online] launch %u: grid %u, idle %llu us, wall clock %d kHz\n", a.launch, o.grid,
+            (unsigned long long)idle_us, khz);
   HIPCHK(ctx, hipEventRecord(o.exited, o.stream));
   o.launched = true;
   o.launches++;
@@ -1256,6 +1259,17 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     const auto now = std::chrono::steady_clock::now();
     if (now - t_last < std::chrono::microseconds(100)) continue;
     t_last = now;
+    static const bool dbg = getenv("MV_ONLINE_DEBUG") != nullptr;  // diagnostics: a request that waits long
+    if (dbg && now - t_start > std::chrono::milliseconds(500) &&
+        (now - t_start) % std::chrono::milliseconds(500) < std::chrono::microseconds(150)) {
+      const uint64_t* tr = o.ctl->trace[slot];
+      fprintf(stderr, "[online] q %llu slot %u waiting %.1f ms: done %llu seq %llu tail %llu trace %llu %llu %llu %llu\n",
+              (unsigned long long)q, slot,
+              std::chrono::duration<double, std::milli>(now - t_start).count(),
+              (unsigned long long)__atomic_load_n(&o.ctl->done[slot], __ATOMIC_ACQUIRE),
+              (unsigned long long)o.req[slot].seq, (unsigned long long)o.ctl->tail, (unsigned long long)tr[0],
+              (unsigned long long)tr[1], (unsigned long long)tr[2], (unsigned long long)tr[3]);
+    }
     std::lock_guard<std::mutex> lk(o.mu);
     if (o.failed) {
       rc = set_err(ctx, MV_E_HIP, "online service failed");
