@@ -2061,7 +2061,11 @@ mv_status mv_ed25519_sign(mv_ctx* ctx, const uint8_t* seed, const uint8_t* msg, 
 mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                            uint8_t* status, uint8_t* msg_digest, uint8_t* block_digest) {
   if (!ctx || (n && (!buf || !off || !len || !status))) return set_err(ctx, MV_E_INVALID_ARG, "bad block args");
-  if (!ctx->has_committee) return set_err(ctx, MV_E_NO_COMMITTEE, "mv_set_committee first");
+  if (!ctx->has_committee) {
+    // a committee change in progress holds com_mu: wait for it rather than fail the call
+    std::shared_lock<std::shared_mutex> cl(ctx->com_mu);
+    if (!ctx->has_committee) return set_err(ctx, MV_E_NO_COMMITTEE, "mv_set_committee first");
+  }
   if (n == 0) return MV_OK;
   if (ctx->flags & MV_FLAG_HOST_PARSE) {
     std::lock_guard<std::mutex> lk(ctx->mu);

@@ -227,3 +227,67 @@ def test_online_service_does_not_block_other_streams(engine, monkeypatch):
     st2, _, _ = engine.verify_blocks(short)
     assert (st2 == st).all() and engine.online_stats()[1] == l0
     engine.set_committee(pks, stakes, 0)  # stops the service (no 5-s resident kernel left behind)
+
+
+def test_online_service_size_limits_and_garbage(engine, monkeypatch):
+    """The service takes calls of <= 64 short blocks; 65 blocks, long blocks and mixed calls go
+    through the queue. Truncated, garbage and empty-length blocks give the queue path's verdicts
+    (PARSE_ERROR, zero digests) either way."""
+    bins, pks, stakes = ragged_blocks(n_rounds=20, seed=21)
+    engine.set_committee(pks, stakes, 0)
+    short = [b for b in bins if len(b) < 1200]
+    rng = np.random.default_rng(5)
+    calls = [short[:64], short[:65], short[:1], [bins[0][:10]] + short[:3], [bytes(8)] + short[:2],
+             [rng.integers(0, 256, size=300, dtype=np.uint8).tobytes()] + short[5:9],
+             [b for b in bins if len(b) > 2500][:3] + short[:1]]
+    monkeypatch.setenv("MV_ONLINE", "0")
+    want = [engine.verify_blocks(c) for c in calls]
+    monkeypatch.delenv("MV_ONLINE")
+    for c, w in zip(calls, want):
+        o0 = engine.online_stats()[0]
+        got = engine.verify_blocks(c)
+        took = engine.online_stats()[0] - o0
+        for a, b in zip(got, w):
+            assert (a == b).all()
+        packed = sum((len(x) + 7) & ~7 for x in c)
+        short_call = len(c) <= 64 and packed <= (128 << 10) and ((packed + 16 + 15) & ~15) < 2048 * len(c)
+        assert took == (1 if short_call else 0), (len(c), took)
+    assert int(want[3][0][0]) == M.BLOCK_PARSE_ERROR and not want[3][1][0].any()
+
+
+def test_online_service_survives_committee_changes(engine):
+    """Callers keep posting through the service while the committee is set again (the resident
+    kernel is stopped, the tables rebuilt, the next call relaunches it): no call hangs or fails,
+    and every verdict is the oracle's."""
+    import time
+
+    bins, pks, stakes = ragged_blocks(n_rounds=10, seed=22)
+    short = [b for b in bins if len(b) < 1200][:40]
+    engine.set_committee(pks, stakes, 0)
+    ref = [O.block_verify(b, pks, stakes, 0)[0] for b in short]
+    errors, stop = [], [False]
+
+    def worker(t):
+        try:
+            k = t
+            while not stop[0]:
+                st, _, _ = engine.verify_blocks([short[k % len(short)]])
+                assert int(st[0]) == ref[k % len(short)]
+                k += 7
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    l0 = engine.online_stats()[1]
+    for _ in range(3):
+        time.sleep(0.05)
+        engine.set_committee(pks, stakes, 0)
+    time.sleep(0.05)
+    stop[0] = True
+    for x in th:
+        x.join(timeout=60)
+    assert not any(x.is_alive() for x in th), "a caller hung"
+    assert not errors, errors
+    assert engine.online_stats()[1] - l0 >= 3  # relaunched after each stop
