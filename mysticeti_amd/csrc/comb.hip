@@ -305,6 +305,32 @@ MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int 
   }
 }
 
+// the same over rows r0 .. r0 + NR - 1 (r0 a multiple of 4) with every row's entry in flight
+// before the first addition: row I's entry is loaded, then rows I + 1 .. (recursively: no array,
+// whose unrolled indices the compiler left to scratch), then row I is added
+template <int I, int NR, bool FRESH>
+MV_DEV void q_ct_rows(fe& v, const uint4* tab, const uint32_t (&w)[NR / 4], int r0) {
+  const int d = ((int)(w[I >> 2] << (24 - 8 * (I & 3)))) >> 24;
+  fe op;
+  q_entry(op, tab + (size_t)(r0 + I) * CT_ROW, d);
+  if constexpr (I + 1 < NR) {
+    q_ct_rows<I + 1, NR, FRESH>(v, tab, w, r0);
+  } else if constexpr (FRESH) {
+    qp_identity(v);
+  }
+  q_entry_fix(op, d);
+  qp_madd(v, op);
+}
+// FRESH: v = the sum; else v += the sum
+template <int NR, bool FRESH = true>
+MV_DEV void q_ct_sum_pf(fe& v, const uint4* tab, const uint32_t sd[8], int r0) {
+  static_assert(NR % 4 == 0, "whole digit words");
+  uint32_t w[NR / 4];
+#pragma unroll
+  for (int i = 0; i < NR / 4; i++) w[i] = pick8(sd, (r0 >> 2) + i);
+  q_ct_rows<0, NR, FRESH>(v, tab, w, r0);
+}
+
 // 4 signatures per workgroup: one wave decodes (4 rows), one wave holds the four B roles and
 // one the four A roles (16 lanes each), so every wave has a SIMD of its own; with 16
 // signatures per workgroup (12 waves, 3 per SIMD) SHA-512 k took 27 us instead of ~10
@@ -312,18 +338,39 @@ constexpr uint32_t C16_SIGS = 4;    // signatures per k_verify_comb16 workgroup
 constexpr uint32_t C16_TROLES = 8;  // table-sum roles: four over the B rows, four over the A rows
 // + one spare wave, which only ingests (with the other three) when the kernel parses its blocks
 constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS + 64;
+// the kernel's wall clock (100 MHz): online-service diagnostics
+MV_DEV uint64_t on_now() { return (uint64_t)wall_clock64(); }
+
 // One workgroup's share (signatures 4 wg .. 4 wg + 3) of the short-chain comb verify: the body
 // of k_verify_comb16, also run job by job by the resident online service (k_online below).
-// Every wave meets exactly three barriers.
+// Two barriers: 0 after the ingest, 1 when role 0 has decoded R and the A wave has S = [s]B - [k]A.
+// Between them the waves meet through LDS flags (spins with s_sleep; every wave has its own
+// SIMD, the spare wave idles):
+//   role 0 (wave 0, one 16-lane row per signature)  the ZIP-215 decode of R
+//   B wave (four roles of quads)   8 B rows each; then, once the A wave has published k's
+//                                  digits, 4 A rows each (rows 16..31); a lane tree over its roles
+//   A wave (four roles of quads)   the blocks' digests, SHA-512 k, k's digits -> LDS; 4 A rows
+//                                  each (rows 0..15); a lane tree; + the B wave's total = S
+// then role 0: R - S, and the torsion test of qp_in_torsion (= [8](R - S) is the identity).
+// stamp (online job 0, MV_ONLINE_TRACE): barrier 0, the B rows done, S done, R decoded, barrier 1.
 MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const uint8_t* __restrict__ pk,
                       const uint32_t* key_idx, uint32_t n, const uint4* __restrict__ combB,
                       const uint4* __restrict__ combA, const uint8_t* __restrict__ key_ok,
                       uint8_t* __restrict__ status, const mvk::BlockVerdictOut& bv, const mvk::BlockHashIn& hin,
-                      const mvk::BlockIngestIn& ing) {
-  __shared__ uint32_t part[C16_TROLES][C16_SIGS][36];  // table roles' sums, coordinate c at words 9c..
-  constexpr int ROWS = CT_ROWS / (C16_TROLES / 2);       // table rows per role
+                      const mvk::BlockIngestIn& ing, uint64_t* stamp = nullptr) {
+  __shared__ uint32_t part_b[C16_SIGS][36];  // the B wave's total, coordinate c at words 9c..
+  __shared__ uint32_t part_s[C16_SIGS][36];  // S
+  __shared__ uint32_t kdl[C16_SIGS][8];      // k's radix-256 digits, A wave -> B wave
+  __shared__ uint32_t kflag, bflag;          // kdl written; part_b written
+  constexpr int BROWS = CT_ROWS / 4;         // B rows per role
+  constexpr int AROWS = CT_ROWS / 8;         // A rows per role (each wave takes half of them)
   const uint32_t t = threadIdx.x;
   static_assert(C16_THREADS == 4 * 64 && C16_SIGS == 4, "one ingest wave per block of the workgroup");
+  static_assert(4 * C16_SIGS * (C16_TROLES / 2) == 64, "the B roles fill one wave, the A roles another");
+  if (t == 0) {  // read after barrier 0
+    kflag = 0;
+    bflag = 0;
+  }
   if (ing.buf) {  // barrier 0: wave w parses block 4 b + w (ingest_dev.h) before anything reads it
     __shared__ IngestLds igl[C16_SIGS];
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), bi = wg * C16_SIGS + w;
@@ -333,8 +380,8 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
     __threadfence();  // its outputs are read by the other waves after the barrier
   }
   __syncthreads();  // barrier 0
-  if (__builtin_amdgcn_readfirstlane(t) >= C16_THREADS - 64) {  // the spare wave: barriers 1 and 2
-    __syncthreads();
+  if (stamp && t == 0) __hip_atomic_store(stamp, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (__builtin_amdgcn_readfirstlane(t) >= C16_THREADS - 64) {  // the spare wave: barrier 1
     __syncthreads();
     return;
   }
@@ -344,31 +391,34 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
   const uint32_t gid = wg * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
   const uint32_t key = key_idx[idx];
+  const uint4* tabA = combA + (size_t)key * CT_TABLE;
   fe v;  // coordinate c of this role's point
   bool okR = false, s_ok = false;
-  // Barrier 1 (inside role 0's decode, after 208 of its 263 products): every table role has
-  // written its sum. The B wave then folds in the A wave's sums and reduces its four roles by
-  // lane shuffles while role 0 finishes the decode. Barrier 2: the total is in LDS.
-  // the branches around the barriers are wave-uniform (readfirstlane: scalar branches), so
-  // every wave meets exactly two barriers
-  static_assert(4 * C16_SIGS * (C16_TROLES / 2) == 64, "the B roles fill one wave, the A roles another");
+  // the branches around the barriers and the flags are wave-uniform (readfirstlane: scalar branches)
   if (__builtin_amdgcn_readfirstlane(role) == 0) {  // every lane of the row holds the signature's R and s
     uint32_t rw[8], sw[8];
     load8(rw, sig + 64 * (size_t)idx);
     load8(sw, sig + 64 * (size_t)idx + 32);
     s_ok = sc_is_canonical(sw);
     p3 R;
-    decompress1_r16(R, okR, rw, [] { __syncthreads(); });  // barrier 1
+    decompress1_r16(R, okR, rw);
     fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
+    if (stamp && t == 0) __hip_atomic_store(stamp + 3, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
-    const uint32_t tr = role - 1;  // 0 .. C16_TROLES / 2 - 1: B rows; then A rows
+    const uint32_t tr = role - 1;  // 0 .. 3: the B wave's roles; 4 .. 7: the A wave's
     const bool b_wave = __builtin_amdgcn_readfirstlane(tr) < C16_TROLES / 2;
+    const uint32_t wr = tr & 3u;  // the role within its wave: lanes 16 wr .. 16 wr + 15
     if (b_wave) {
-      uint32_t sw[8], sd[8];
+      uint32_t sw[8], sd[8], kd[8];
       load8(sw, sig + 64 * (size_t)idx + 32);
       sc_recode256(sd, sw);
-      const int r0 = (int)tr * ROWS;
-      q_ct_sum(v, combB, sd, r0, r0 + ROWS);
+      q_ct_sum_pf<BROWS>(v, combB, sd, (int)wr * BROWS);
+      if (stamp && t == 64) __hip_atomic_store(stamp + 1, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      while (__hip_atomic_load(&kflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+      for (int i = 0; i < 8; i++) kd[i] = kdl[sq][i];
+      q_ct_sum_pf<AROWS, false>(v, tabA, kd, CT_ROWS / 2 + (int)wr * AROWS);
     } else {
       if (hin.stage) {
         // the block path's two digests of this workgroup's blocks first (one quad per block,
@@ -385,51 +435,55 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
       sha512_short(h, kin, 96);
       sc_reduce512(k, h);
       sc_recode256(kd, k);
-      const int r0 = (int)(tr - C16_TROLES / 2) * ROWS;
-      q_ct_sum(v, combA + (size_t)key * CT_TABLE, kd, r0, r0 + ROWS);
-    }
+      if (wr == 0 && c == 0) {
 #pragma unroll
-    for (int i = 0; i < 9; i++) part[tr][sq][9 * c + i] = v.v[i];
-    __syncthreads();  // barrier 1
-    if (b_wave) {  // the B wave: + the A role of the same rank, then the lane tree
+        for (int i = 0; i < 8; i++) kdl[sq][i] = kd[i];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (t == 128) __hip_atomic_store(&kflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      q_ct_sum_pf<AROWS>(v, tabA, kd, (int)wr * AROWS);
+    }
+    // the wave's four roles -> role 0 of the wave (lanes 16 h up)
+    for (uint32_t h = 2; h >= 1; h >>= 1) {
       fe w;
 #pragma unroll
-      for (int i = 0; i < 9; i++) w.v[i] = part[tr + C16_TROLES / 2][sq][9 * c + i];
+      for (int i = 0; i < 9; i++) w.v[i] = (uint32_t)__shfl_down((int)v.v[i], 4 * C16_SIGS * h, 64);
+      if (wr < h) qp_add(v, w);
+    }
+    if (b_wave) {
+      if (wr == 0) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) part_b[sq][9 * c + i] = v.v[i];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (t == 64) __hip_atomic_store(&bflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      while (__hip_atomic_load(&bflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      fe w;
+#pragma unroll
+      for (int i = 0; i < 9; i++) w.v[i] = part_b[sq][9 * c + i];
       qp_add(v, w);
-      for (uint32_t h = C16_TROLES / 4; h >= 1; h >>= 1) {  // role tr + h is 4 C16_SIGS h lanes up
+      if (wr == 0) {
 #pragma unroll
-        for (int i = 0; i < 9; i++) w.v[i] = (uint32_t)__shfl_down((int)v.v[i], 4 * C16_SIGS * h, 64);
-        if (tr < h) qp_add(v, w);
+        for (int i = 0; i < 9; i++) part_s[sq][9 * c + i] = v.v[i];
       }
-      if (tr == 0) {
-#pragma unroll
-        for (int i = 0; i < 9; i++) part[0][sq][9 * c + i] = v.v[i];
-      }
+      if (stamp && t == 128) __hip_atomic_store(stamp + 2, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  __syncthreads();  // barrier 2
+  __syncthreads();  // barrier 1
+  if (stamp && t == 0) __hip_atomic_store(stamp + 4, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (role == 0) {  // lanes 0..3 of each row form the quad (the other lanes repeat it)
     fe S;
 #pragma unroll
-    for (int i = 0; i < 9; i++) S.v[i] = part[0][sq][9 * c + i];
+    for (int i = 0; i < 9; i++) S.v[i] = part_s[sq][9 * c + i];
     // R' = S = [s]B - [k]A (the A tables hold -A); R - R': -S has X and T negated
     fe nS;
     fe_neg(nS, S);
     fe_cmov(S, nS, c == 0 || c == 3);
     qp_add(v, S);
-    qp_dbl(v);  // cofactor
-    qp_dbl(v);
-    qp_dbl(v);
-    // identity: X == 0 and Y == Z
-    fe Z;
-    fe_qget<2>(Z, v);
-    const bool zx = fe_is_zero(v);   // meaningful in lane 0
-    const bool eyz = fe_eq(v, Z);    // meaningful in lane 1
-    const uint32_t bits = (zx ? 1u : 0u) | (eyz ? 2u : 0u);
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x00, 0xf, 0xf, false);  // lane 0's
-    const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xf, 0xf, false);  // lane 1's
-    const bool ident = (b0 & 1u) && (b1 & 2u);
-    if ((t & 15u) == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && ident) ? 0 : 1));
+    const bool small = qp_in_torsion(v);
+    if ((t & 15u) == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : ((s_ok && okR && small) ? 0 : 1));
   }
 }
 
@@ -451,8 +505,6 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // uniform (the role is the workgroup's, decisions are broadcast through LDS), and every wait
 // loop also tests the launch's end, so all waves leave.
 constexpr uint32_t ON_BATCH = 32;  // requests the poller moves per pass
-
-MV_DEV uint64_t on_now() { return (uint64_t)wall_clock64(); }
 
 // Workgroup 0: moves published requests from page-locked memory into HBM, appends their jobs.
 MV_DEV void online_poller(const mvk::OnlineArgs& A) {
@@ -643,9 +695,11 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
     const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
     const mvk::BlockIngestIn ing{sc + 16 * (size_t)n, off, off + n, A.stakes, A.n_auth, A.epoch, A.quorum_thr,
                                  stage, poff, plen, sig, kidx, facts, claimed};
+    uint64_t* stamp = j == 0 ? &ctl->trace[slot][4] : nullptr;
     comb16_wg(j, md, sig, A.pk, kidx, n, (const uint4*)A.combB, (const uint4*)A.combA, A.key_ok,
-              sc + mvk::ONLINE_O_SST, bv, hin, ing);
+              sc + mvk::ONLINE_O_SST, bv, hin, ing, stamp);
     __syncthreads();  // the job's digests and verdicts are in HBM (workgroup scope)
+    if (stamp && t == 0) __hip_atomic_store(stamp + 5, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // this job's blocks: md and bd (8 words each), status -> page-locked output
     uint8_t* oh = A.out_host + mvk::ONLINE_OUT_STRIDE * slot;
     const uint32_t b0 = j * C16_SIGS, nb = n - b0 < C16_SIGS ? n - b0 : C16_SIGS;
@@ -659,6 +713,7 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
     }
     if (t < 128) __threadfence_system();  // the writers' outputs (waves 0, 1) before the done word
     __syncthreads();
+    if (stamp && t == 0) __hip_atomic_store(stamp + 6, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (t == 0) {
       const uint32_t nj = (n + C16_SIGS - 1) / C16_SIGS;
       const uint32_t prev = __hip_atomic_fetch_add(&dev->jobs_done[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -820,19 +875,9 @@ __global__ void __launch_bounds__(4 * POST_SIGS * POST_ROLES) k_comb_post(const 
     fe_neg(nv, v);
     fe_cmov(v, nv, c == 0 || c == 3);
     qp_add(v, rs);
-    qp_dbl(v);  // cofactor
-    qp_dbl(v);
-    qp_dbl(v);
-    fe Z;
-    fe_qget<2>(Z, v);
-    const bool zx = fe_is_zero(v);  // meaningful in lane 0
-    const bool eyz = fe_eq(v, Z);   // meaningful in lane 1
-    const uint32_t bits = (zx ? 1u : 0u) | (eyz ? 2u : 0u);
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x00, 0xf, 0xf, false);
-    const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xf, 0xf, false);
-    const bool ident = (b0 & 1u) && (b1 & 2u);
+    const bool small = qp_in_torsion(v);  // [8](R - R') is the identity
     const uint8_t f = qflags[idx];
-    if (c == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : (((f & 3) == 3 && ident) ? 0 : 1));
+    if (c == 0 && gid < n) put_status(status, bv, gid, !key_ok[key] ? 2 : (((f & 3) == 3 && small) ? 0 : 1));
   }
 }
 

@@ -95,6 +95,24 @@ MV_DEV void qp_add(fe& v, const fe& w) {
   fe_mul(v, a1, a2);
 }
 
+// v = coordinate c of a curve point P -> whether [8]P is the identity (the same in every lane of
+// the quad), i.e. whether P lies in the 8-torsion E[8]. On -x^2 + y^2 = 1 + d x^2 y^2 those are
+// exactly the points with x = 0 (orders 1, 2), y = 0 (order 4: (+-sqrt(-1), 0)) or
+// x^2 + y^2 = 0 (order 8: 2P has y = (y^2 + x^2) / (2 + x^2 - y^2) = 0, i.e. 2P is of order 4;
+// conversely 2P of order 4 has y = 0). The three tests are homogeneous, so X and Y of the
+// extended point serve: one squaring deep, against [8]P's three doublings and the identity test
+// (tests/test_torsion_predicate.py checks the equivalence over E[8] + multiples of B).
+MV_DEV bool qp_in_torsion(const fe& v) {
+  fe sq, Y2, s;
+  fe_sq(sq, v);  // lane 0: X^2, lane 1: Y^2
+  fe_qget<1>(Y2, sq);
+  fe_addn(s, sq, Y2);  // lane 0: X^2 + Y^2
+  const uint32_t bits = (fe_is_zero(v) ? 1u : 0u) | (fe_is_zero(s) ? 2u : 0u);
+  const uint32_t b0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x00, 0xf, 0xf, false);  // lane 0's
+  const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xf, 0xf, false);  // lane 1's
+  return (b0 & 3u) != 0 || (b1 & 1u) != 0;  // X = 0 or X^2 + Y^2 = 0; Y = 0
+}
+
 // coordinate c of the extended point stored as 9 uint4 (p3_to_quads layout: X, Y, Z, T limbs)
 MV_DEV void qp_load(fe& v, const uint4* base, size_t idx) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(base + idx * 9) + 9 * qlane();
