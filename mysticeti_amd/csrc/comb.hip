@@ -352,7 +352,8 @@ MV_DEV uint64_t on_now() { return (uint64_t)wall_clock64(); }
 //   A wave (four roles of quads)   the blocks' digests, SHA-512 k, k's digits -> LDS; 4 A rows
 //                                  each (rows 0..15); a lane tree; + the B wave's total = S
 // then role 0: R - S, and the torsion test of qp_in_torsion (= [8](R - S) is the identity).
-// stamp (online job 0, MV_ONLINE_TRACE): barrier 0, the B rows done, S done, R decoded, barrier 1.
+// stamp (online job 0, MV_ONLINE_TRACE): barrier 0, the B rows done, S done, R decoded, barrier 1;
+// [7] digests done, [8] k's digits published.
 MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const uint8_t* __restrict__ pk,
                       const uint32_t* key_idx, uint32_t n, const uint4* __restrict__ combB,
                       const uint4* __restrict__ combA, const uint8_t* __restrict__ key_ok,
@@ -427,6 +428,7 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
                                                    hin.pre_len, n, hin.msg_digest, hin.digest);
         __threadfence();  // the digests are read back below (other lanes) and by role 0's verdict
       }
+      if (stamp && t == 128) __hip_atomic_store(stamp + 7, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's bytes)
       uint32_t kin[24], h[16], k[8], kd[8];
       load8(kin, sig + 64 * (size_t)idx);
@@ -441,6 +443,7 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (t == 128) __hip_atomic_store(&kflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (stamp && t == 128) __hip_atomic_store(stamp + 8, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       q_ct_sum_pf<AROWS>(v, tabA, kd, (int)wr * AROWS);
     }
     // the wave's four roles -> role 0 of the wave (lanes 16 h up)

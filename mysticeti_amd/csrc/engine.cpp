@@ -1030,7 +1030,7 @@ struct OnlineSvc {
   bool trace = false;
   double ticks_per_us = 100.0;
   std::mutex tr_mu;
-  double tr_sum[12] = {};
+  double tr_sum[14] = {};
   uint64_t tr_n = 0;
 };
 
@@ -1183,10 +1183,11 @@ void online_release(OnlineSvc& o) {
     fprintf(stderr,
             "[online] %llu requests, mean us: host publish->done seen %.1f | kernel: seen->ready %.1f, "
             "ready->claim %.1f, claim->done %.1f, seen->done %.1f | job 0 from its claim: barrier 0 %.1f, "
-            "B rows %.1f, S %.1f, R decoded %.1f, barrier 1 %.1f, verdict %.1f, fenced %.1f\n",
+            "B rows %.1f, S %.1f, R decoded %.1f, barrier 1 %.1f, verdict %.1f, fenced %.1f, digests %.1f, "
+            "k %.1f\n",
             (unsigned long long)o.tr_n, o.tr_sum[0] / n, o.tr_sum[1] / n, o.tr_sum[2] / n, o.tr_sum[3] / n,
             o.tr_sum[4] / n, o.tr_sum[5] / n, o.tr_sum[6] / n, o.tr_sum[7] / n, o.tr_sum[8] / n, o.tr_sum[9] / n,
-            o.tr_sum[10] / n, o.tr_sum[11] / n);
+            o.tr_sum[10] / n, o.tr_sum[11] / n, o.tr_sum[12] / n, o.tr_sum[13] / n);
   }
   if (o.stream) (void)hipStreamDestroy(o.stream);
   if (o.exited) (void)hipEventDestroy(o.exited);
@@ -1295,7 +1296,7 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     o.tr_sum[2] += (double)(int64_t)(tr[2] - tr[1]) * k;
     o.tr_sum[3] += (double)(int64_t)(tr[3] - tr[2]) * k;
     o.tr_sum[4] += (double)(int64_t)(tr[3] - tr[0]) * k;
-    for (int i = 0; i < 7; i++) o.tr_sum[5 + i] += (double)(int64_t)(tr[4 + i] - tr[2]) * k;
+    for (int i = 0; i < 9; i++) o.tr_sum[5 + i] += (double)(int64_t)(tr[4 + i] - tr[2]) * k;
     o.tr_n++;
   }
   const uint8_t* ho = out;

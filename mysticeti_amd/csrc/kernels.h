@@ -155,9 +155,9 @@ struct OnlineCtl {
   uint64_t done[ONLINE_SLOTS];
   // the kernel's wall clock at: the poller sees the request, its jobs are in the ring, its first
   // job starts, its last job is done; then job 0's barrier 0 (ingest done), B rows done, S done,
-  // R decoded, barrier 1, verdict written, outputs fenced (comb.hip comb16_wg; diagnostics:
-  // MV_ONLINE_TRACE sums them)
-  uint64_t trace[ONLINE_SLOTS][12];
+  // R decoded, barrier 1, verdict written, outputs fenced, digests done, k published (comb.hip
+  // comb16_wg; diagnostics: MV_ONLINE_TRACE sums them)
+  uint64_t trace[ONLINE_SLOTS][14];
 };
 struct OnlineDev {
   unsigned long long ready;      // requests moved to HBM by the poller
