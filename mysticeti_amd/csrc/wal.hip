@@ -15,7 +15,10 @@
 // funnel-shifts them (v_alignbyte_b32).
 // Tables in LDS: A256 (the hot one, 4 x 256 words) replicated 8 times so that lanes l and
 // l' with l != l' (mod 8) never hit one bank; the tree's six maps once (56 KiB in all, one
-// copy per 1024-thread workgroup).
+// copy per 1024-thread workgroup, two workgroups per CU). The kernel is bound by HBM latency,
+// not by the LDS: 32 bank-aligned copies (no conflicts at all, 152 KiB, one workgroup per CU)
+// measured 3.18 ms per 2^20 entries and 16 copies 2.52, against 2.31 for this form at 8 waves
+// per SIMD (profiles/r04/wal/ab_tables_occupancy_r04p.txt).
 //
 // Walk: one lane per map of 2^map_bits bytes. Every map that holds entries starts with one
 // (the writer pads an entry that would straddle a map, wal.rs:155-167), so maps walk
@@ -33,7 +36,10 @@
 namespace mv {
 namespace wal {
 
-constexpr int REP = 8;                       // copies of A256 (bank spread)
+#ifndef MV_WAL_REP
+#define MV_WAL_REP 8
+#endif
+constexpr int REP = MV_WAL_REP;              // copies of A256 (bank spread)
 constexpr int A_WORDS = 4 * 256 * REP;       // [byte t][value e][copy c]
 constexpr int S_LEVELS = 6;                  // shifts by 4 << k bytes, k < 6
 constexpr int S_WORDS = S_LEVELS * 4 * 256;  // [k][byte t][value e]
@@ -41,9 +47,13 @@ constexpr int T_WORDS = 256;                 // the byte table (1-byte shift), g
 constexpr uint32_t PREFIX = 0x9226f562u;     // crc_raw(0, PREFIX as 4 LE bytes) = 0xFFFFFFFF
 constexpr int WG = 1024;                     // threads per crc workgroup
 #ifndef MV_WAL_ROWS
-#define MV_WAL_ROWS 16  // 16 and 32: crc 2.47-2.51 ms per 2^20 entries; 8: 2.62-2.67; 12, 24: ~3.0 (tools/gpu_r03ah.sh)
+#define MV_WAL_ROWS 8  // rows in flight per batch; 8 fits the 64-VGPR budget of 8 waves per SIMD
 #endif
-constexpr int WAL_ROWS = MV_WAL_ROWS;        // 256-B rows in flight per wave
+constexpr int WAL_ROWS = MV_WAL_ROWS;
+#ifndef MV_WAL_WPE
+#define MV_WAL_WPE 8  // waves per SIMD the register budget is cut for: two 1024-thread workgroups per CU
+#endif
+#define MV_WAL_ATTR __attribute__((amdgpu_waves_per_eu(MV_WAL_WPE)))        // 256-B rows in flight per wave
 
 // a wave-uniform 64-bit value from lane 0
 MV_DEV uint64_t bcast64(uint64_t x) {
@@ -53,13 +63,17 @@ MV_DEV uint64_t bcast64(uint64_t x) {
 
 struct Lds {
   uint32_t a[A_WORDS];
+#ifndef MV_WAL_SGLOBAL
   uint32_t s[S_WORDS];
+#endif
 };
 
 MV_DEV void lds_fill(Lds& L, const uint32_t* __restrict__ tables) {
   for (int i = threadIdx.x; i < A_WORDS + S_WORDS; i += blockDim.x) {
     if (i < A_WORDS) L.a[i] = tables[i];
+#ifndef MV_WAL_SGLOBAL
     else L.s[i - A_WORDS] = tables[i];
+#endif
   }
   __syncthreads();
 }
@@ -68,15 +82,24 @@ MV_DEV uint32_t adv256(const Lds& L, uint32_t u, uint32_t c) {
   return L.a[(0 * 256 + (u & 255)) * REP + c] ^ L.a[(1 * 256 + ((u >> 8) & 255)) * REP + c] ^
          L.a[(2 * 256 + ((u >> 16) & 255)) * REP + c] ^ L.a[(3 * 256 + (u >> 24)) * REP + c];
 }
-MV_DEV uint32_t shiftk(const Lds& L, int k, uint32_t u) {
-  const uint32_t* s = L.s + k * 1024;
+// the tree's shift maps: in LDS, or (MV_WAL_SGLOBAL) read through the caches
+MV_DEV const uint32_t* s_tab(const Lds& L, const uint32_t* __restrict__ tables) {
+#ifdef MV_WAL_SGLOBAL
+  return tables + A_WORDS;
+#else
+  return L.s;
+#endif
+}
+MV_DEV uint32_t shiftk(const uint32_t* S, int k, uint32_t u) {
+  const uint32_t* s = S + k * 1024;
   return s[u & 255] ^ s[256 + ((u >> 8) & 255)] ^ s[512 + ((u >> 16) & 255)] ^ s[768 + (u >> 24)];
 }
 MV_DEV uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }  // (nt loads: no gain)
 
 // crc_raw(0xFFFFFFFF, base[a, b)) (the CRC register before the final xor), on the whole wave.
 // Reads only the aligned dwords that hold bytes of [a, b).
-MV_DEV uint32_t crc_raw_wave(const uint8_t* __restrict__ base, uint64_t a, uint64_t b, const Lds& L) {
+MV_DEV uint32_t crc_raw_wave(const uint8_t* __restrict__ base, uint64_t a, uint64_t b, const Lds& L,
+                              const uint32_t* S) {
   const uint32_t lane = threadIdx.x & 63, c = lane & (REP - 1);
   const uint64_t len = b - a;
   const uint64_t R = (len + 4 + 255) / 256;
@@ -84,59 +107,68 @@ MV_DEV uint32_t crc_raw_wave(const uint8_t* __restrict__ base, uint64_t a, uint6
   const int64_t a4 = (int64_t)(a & ~3ull);
   const uint64_t Z = (uint64_t)PREFIX << 32;  // virtual bytes a-8 .. a-1: 0 0 0 0 P0 P1 P2 P3
   uint32_t u = 0;
-  const uint64_t jm = R < 2 ? R : 2;
-  // rows 0, 1: may hold bytes before a (zeros, then the prefix P)
-  for (uint64_t j = 0; j < jm; j++) {
+  // rows 0, 1: may hold bytes before a (zeros, then the prefix P); their loads go out first
+  uint32_t w01[2] = {0u, 0u};
+  int64_t q01[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
     const int64_t x = (int64_t)b - 256 * (int64_t)(R - j) + 4 * (int64_t)lane;
-    const int64_t q = x - (int64_t)a;
-    uint32_t w = 0;
-    if (q > -4) {
+    q01[j] = x - (int64_t)a;
+    if ((uint64_t)j < R && q01[j] > -4) {
       const int64_t xa = x - sh;
       const uint32_t A = xa >= a4 ? ld32(base + xa) : 0u;
       const uint32_t B = sh ? ld32(base + xa + 4) : 0u;
-      w = sh ? __builtin_amdgcn_alignbyte(B, A, sh) : A;
+      w01[j] = sh ? __builtin_amdgcn_alignbyte(B, A, sh) : A;
     }
-    if (q < 0) {
-      const uint32_t keep = q <= -4 ? 0u : (0xffffffffu << (8 * (uint32_t)(-q)));
-      w = q < -8 ? 0u : ((w & keep) | (uint32_t)(Z >> (8 * (q + 8))));
-    }
-    u = adv256(L, u, c) ^ w;
   }
-  // rows 2 .. R-1: whole rows of D, WAL_ROWS in flight (the kernel is bound by HBM latency:
-  // ~1 us per round trip, so each lane keeps several rows' loads outstanding)
-  uint64_t j = jm;
-  const uint8_t* pr = base + (int64_t)b - 256 * (int64_t)(R - j) + 4 * (int64_t)lane - sh;
-  for (; j + WAL_ROWS <= R; j += WAL_ROWS, pr += 256 * WAL_ROWS) {
+  // rows 2 .. R-1 in batches of WAL_ROWS loads in flight (the kernel is bound by HBM latency:
+  // ~1-2 us per round trip, so each lane keeps a batch outstanding); the last batch is partial,
+  // its rows past R neither loaded nor folded: one round trip, not one per leftover row
+  const uint8_t* pr = base + (int64_t)b - 256 * (int64_t)(R - 2) + 4 * (int64_t)lane - sh;
+  for (uint64_t j0 = 2;; j0 += WAL_ROWS, pr += 256 * WAL_ROWS) {
     uint32_t A[WAL_ROWS], B[WAL_ROWS];
 #pragma unroll
     for (int k = 0; k < WAL_ROWS; k++) {
-      A[k] = ld32(pr + 256 * k);
-      B[k] = sh ? ld32(pr + 256 * k + 4) : 0u;
+      const bool live = j0 + k < R;  // wave-uniform
+      A[k] = live ? ld32(pr + 256 * k) : 0u;
+      B[k] = live && sh ? ld32(pr + 256 * k + 4) : 0u;
+    }
+    if (j0 == 2) {
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        if ((uint64_t)j >= R) break;
+        uint32_t w = w01[j];
+        const int64_t q = q01[j];
+        if (q < 0) {
+          const uint32_t keep = q <= -4 ? 0u : (0xffffffffu << (8 * (uint32_t)(-q)));
+          w = q < -8 ? 0u : ((w & keep) | (uint32_t)(Z >> (8 * (q + 8))));
+        }
+        u = adv256(L, u, c) ^ w;
+      }
     }
 #pragma unroll
-    for (int k = 0; k < WAL_ROWS; k++) u = adv256(L, u, c) ^ (sh ? __builtin_amdgcn_alignbyte(B[k], A[k], sh) : A[k]);
-  }
-  for (; j < R; j++, pr += 256) {
-    const uint32_t A = ld32(pr), B = sh ? ld32(pr + 4) : 0u;
-    u = adv256(L, u, c) ^ (sh ? __builtin_amdgcn_alignbyte(B, A, sh) : A);
+    for (int k = 0; k < WAL_ROWS; k++)
+      if (j0 + k < R) u = adv256(L, u, c) ^ (sh ? __builtin_amdgcn_alignbyte(B[k], A[k], sh) : A[k]);
+    if (j0 + WAL_ROWS >= R) break;
   }
   // lanes: val over [g, g + 2^(k+1)) = shift(val[g, g + 2^k), 4 * 2^k) ^ val[g + 2^k, ...)
 #pragma unroll
   for (int k = 0; k < S_LEVELS; k++) {
     const uint32_t v = (uint32_t)__shfl_down((int)u, 1 << k);
-    if ((lane & ((2u << k) - 1)) == 0) u = shiftk(L, k, u) ^ v;
+    if ((lane & ((2u << k) - 1)) == 0) u = shiftk(S, k, u) ^ v;
   }
-  u = shiftk(L, 0, u);  // lane 63's word ends 4 bytes before the end
+  u = shiftk(S, 0, u);  // lane 63's word ends 4 bytes before the end
   return (uint32_t)__shfl((int)u, 0);
 }
 
 // state <- state advanced over n zero bytes (crc_raw(state, 0^n)); rare paths only
-MV_DEV uint32_t zeros_shift(const Lds& L, const uint32_t* __restrict__ tbyte, uint32_t s, uint64_t n) {
+MV_DEV uint32_t zeros_shift(const Lds& L, const uint32_t* S, const uint32_t* __restrict__ tbyte, uint32_t s,
+                            uint64_t n) {
   const uint32_t c = threadIdx.x & (REP - 1);
   for (; n >= 256; n -= 256) s = adv256(L, s, c);
   for (int k = S_LEVELS - 1; k >= 0; k--)
     if (n >= (4u << k)) {
-      s = shiftk(L, k, s);
+      s = shiftk(S, k, s);
       n -= 4u << k;
     }
   for (; n; n--) s = (s >> 8) ^ tbyte[s & 255];
@@ -144,7 +176,7 @@ MV_DEV uint32_t zeros_shift(const Lds& L, const uint32_t* __restrict__ tbyte, ui
 }
 
 // ------------------------------------------------------------------ crc32 of n strings
-__global__ void __launch_bounds__(WG) k_crc32_batch(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+__global__ void __launch_bounds__(WG) MV_WAL_ATTR k_crc32_batch(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                                                     const uint64_t* __restrict__ len, uint32_t n,
                                                     const uint32_t* __restrict__ tables, uint32_t* __restrict__ out) {
   __shared__ Lds L;
@@ -153,7 +185,7 @@ __global__ void __launch_bounds__(WG) k_crc32_batch(const uint8_t* __restrict__ 
   const uint32_t waves = gridDim.x * (WG / 64);
   for (uint32_t i = blockIdx.x * (WG / 64) + threadIdx.x / 64; i < n; i += waves) {
     const uint64_t a = bcast64(off[i]), b = a + bcast64(len[i]);
-    const uint32_t r = crc_raw_wave(buf, a, b, L);
+    const uint32_t r = crc_raw_wave(buf, a, b, L, s_tab(L, tables));
     if (lane == 0) out[i] = ~r;
   }
 }
@@ -306,7 +338,7 @@ __global__ void __launch_bounds__(256) k_wal_compact(const unsigned long long* _
 
 // one wave per entry: header, crc of the payload, verdict; the first failing entry index
 // goes to *first_fail (atomic min)
-__global__ void __launch_bounds__(WG) k_wal_crc(const uint8_t* __restrict__ img, uint64_t size,
+__global__ void __launch_bounds__(WG) MV_WAL_ATTR k_wal_crc(const uint8_t* __restrict__ img, uint64_t size,
                                                 const unsigned long long* __restrict__ ent, uint64_t total,
                                                 const uint32_t* __restrict__ tables, uint64_t* __restrict__ out_pos,
                                                 uint32_t* __restrict__ out_tag, uint32_t* __restrict__ out_len,
@@ -317,6 +349,7 @@ __global__ void __launch_bounds__(WG) k_wal_crc(const uint8_t* __restrict__ img,
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t waves = (uint64_t)gridDim.x * (WG / 64);
   const uint32_t* tbyte = tables + A_WORDS + S_WORDS;
+  const uint32_t* S = s_tab(L, tables);
   for (uint64_t e = blockIdx.x * (WG / 64) + threadIdx.x / 64; e < total; e += waves) {
     const uint64_t r = bcast64(ent[e]);
     const uint64_t p = r & ((1ull << 60) - 1);
@@ -330,10 +363,10 @@ __global__ void __launch_bounds__(WG) k_wal_crc(const uint8_t* __restrict__ img,
       const uint64_t a = p + 16, b = p + len;
       uint32_t raw;
       if (b <= size) {
-        raw = crc_raw_wave(img, a, b, L);
+        raw = crc_raw_wave(img, a, b, L, S);
       } else {  // the file ends inside the payload: the rest reads as zeros
-        raw = a < size ? crc_raw_wave(img, a, size, L) : 0xffffffffu;
-        raw = zeros_shift(L, tbyte, raw, b - (a < size ? size : a));
+        raw = a < size ? crc_raw_wave(img, a, size, L, S) : 0xffffffffu;
+        raw = zeros_shift(L, S, tbyte, raw, b - (a < size ? size : a));
       }
       st = (uint64_t)(~raw) == crc ? MV_WAL_OK : MV_WAL_CRC_MISMATCH;
     }
@@ -383,7 +416,7 @@ void wal_build_tables(uint32_t* out) {
 static uint32_t crc_grid(uint64_t items, int cus) {
   const uint64_t per_wg = mv::wal::WG / 64;
   uint64_t g = (items + per_wg - 1) / per_wg;
-  const uint64_t cap = 2ull * (uint64_t)cus;  // two 1024-thread workgroups (56 KiB LDS each) per CU
+  const uint64_t cap = (uint64_t)(163840 / sizeof(mv::wal::Lds)) * (uint64_t)cus;  // 1024-thread workgroups per CU (LDS)
   return (uint32_t)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
