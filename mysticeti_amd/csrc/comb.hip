@@ -508,6 +508,7 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // uniform (the role is the workgroup's, decisions are broadcast through LDS), and every wait
 // loop also tests the launch's end, so all waves leave.
 constexpr uint32_t ON_BATCH = 32;  // requests the poller moves per pass
+static_assert(IG_WIN == mvk::INGEST_WINDOW_BYTES, "the host's eligibility test uses the ingest window");
 
 // Workgroup 0: moves published requests from page-locked memory into HBM, appends their jobs.
 MV_DEV void online_poller(const mvk::OnlineArgs& A) {

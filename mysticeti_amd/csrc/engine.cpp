@@ -1047,13 +1047,24 @@ bool online_enabled_env() {
 // Whether a request of n blocks, `bytes` of 8-aligned bincode, takes the online service: the
 // calls enqueue_blocks would run as one k_verify_comb16 launch (short blocks, the ingest and
 // hash folded in), small enough for one ring slot.
-bool online_eligible(mv_ctx* ctx, uint32_t n, uint64_t bytes) {
+// Long blocks (config-4 shape, ~9.5 KB) take the service too: a request is then one job whose
+// A wave hashes the whole pre-image (the R decode runs beside it), against the queue's split
+// launch pair: 16 one-block config-4-shape callers 80.8-81.0 k blocks/s, p50 197-198 us, against
+// 69.4-70.6 k / 223-225 us (profiles/r04/c5_online_long_r04s.txt). MV_ONLINE_LONG=0: short
+// blocks only (< MV_COMB_SPLIT_BYTES on average, as the queue's one-launch case). A block past
+// the wave-parallel ingest's LDS window (ingest_dev.h IG_WIN) goes through the queue.
+bool online_eligible(mv_ctx* ctx, uint32_t n, uint64_t bytes, uint64_t longest) {
   if ((ctx->flags & (MV_FLAG_NO_ONLINE | MV_FLAG_NO_COMB | MV_FLAG_HOST_PARSE)) || !online_enabled_env()) return false;
   if (n == 0 || n > kOnMax || bytes > kOnInCap) return false;
+  if (longest + 32 > mvk::INGEST_WINDOW_BYTES) return false;
+  static const bool longb = [] {
+    const char* e = getenv("MV_ONLINE_LONG");
+    return !(e && e[0] == '0');
+  }();
   const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
   const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
   const uint64_t buf_bytes = (bytes + 16 + 15) & ~15ull;
-  if (split_bytes && buf_bytes >= split_bytes * (uint64_t)n) return false;
+  if (!longb && split_bytes && buf_bytes >= split_bytes * (uint64_t)n) return false;
   const char* fe = getenv("MV_BLK_FUSED");
   const char* hce = getenv("MV_HASH_IN_COMB");
   const char* ice = getenv("MV_INGEST_IN_COMB");
@@ -1793,6 +1804,16 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
     hipError_t e = hipSetDevice(dev.id);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking);
     for (int k = 0; k < 2 && e == hipSuccess; k++) e = hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking);
+    // every other stream the engine uses, now: the runtime spreads streams over its hardware
+    // queues (GPU_MAX_HW_QUEUES) in creation order, and the online service's CU-masked stream
+    // must be created after all of them, or a stream made later can share its queue and wait
+    // behind the resident kernel (test_online_service_does_not_block_other_streams)
+    for (int k = 0; k < Device::kPassSets && e == hipSuccess; k++)
+      e = hipStreamCreateWithFlags(&dev.qstream[k], hipStreamNonBlocking);
+    for (int k = 0; k < Device::kPassSets && e == hipSuccess; k++)
+      e = hipStreamCreateWithFlags(&dev.pset[k].aux.stream, hipStreamNonBlocking);
+    for (int k = 0; k < Device::kBlkSlots && e == hipSuccess; k++)
+      e = hipStreamCreateWithFlags(&dev.blk_aux[k].stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = dev.btab.ensure(mvk::btable_bytes());
     if (e == hipSuccess) e = mvk::launch_btable_init(dev.btab.p, dev.stream);
     if (e == hipSuccess) e = dev.combB.ensure(mvk::comb_table_bytes(1));
@@ -2075,11 +2096,14 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     std::lock_guard<std::mutex> lk(ctx->mu);
     return verify_blocks_host_parse(ctx, buf, off, len, n, status, msg_digest, block_digest);
   }
-  // the resident online service: small calls of short blocks, no queue, no launch
+  // the resident online service: small calls, no queue, no launch
   {
-    uint64_t bytes = 0;
-    for (uint32_t k = 0; k < n && bytes <= (128u << 10); k++) bytes += (len[k] + 7) & ~7ull;
-    if (online_eligible(ctx, n, bytes)) {
+    uint64_t bytes = 0, longest = 0;
+    for (uint32_t k = 0; k < n && bytes <= (128u << 10); k++) {
+      bytes += (len[k] + 7) & ~7ull;
+      longest = std::max<uint64_t>(longest, len[k]);
+    }
+    if (online_eligible(ctx, n, bytes, longest)) {
       std::shared_lock<std::shared_mutex> cl(ctx->com_mu);
       if (committee_ready(ctx)) {
         Device& dev = ctx->devs[ctx->online_rr.fetch_add(1) % ctx->devs.size()];

@@ -144,6 +144,9 @@ constexpr size_t ONLINE_O_FACTS = ONLINE_O_KIDX + online_al(4 * ONLINE_MAX_BLOCK
 constexpr size_t ONLINE_O_CLAIMED = ONLINE_O_FACTS + online_al(4 * ONLINE_MAX_BLOCKS);
 constexpr size_t ONLINE_O_SST = ONLINE_O_CLAIMED + online_al(32 * ONLINE_MAX_BLOCKS);
 constexpr size_t ONLINE_SCR_STRIDE = ONLINE_O_SST + online_al(ONLINE_MAX_BLOCKS);
+// the wave-parallel ingest's LDS window per block (ingest_dev.h IG_WIN): longer blocks parse on
+// one lane, so the online service leaves them to the queue
+constexpr uint32_t INGEST_WINDOW_BYTES = 10240;
 struct OnlineReq {
   uint64_t seq;         // request number + 1 once the slot's input and n are written (release)
   uint32_t n;           // blocks; 0 = a void request (completed without work)

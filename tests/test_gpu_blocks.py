@@ -186,13 +186,14 @@ def test_comb_split_and_fused_paths_agree(engine, golden, monkeypatch, split):
     (k_comb_pre -- s < l, R decode, R - [s]B -- on a second stream beside the hash, k_comb_post
     after it); MV_COMB_SPLIT_BYTES=1 forces the split for every block, 0 the fused kernel: the
     edge cases, ragged lengths and config-4-shaped blocks with bad signatures keep the oracle's
-    verdicts and digests either way."""
+    verdicts and digests either way. (The queue's kernels: the resident service is off here.)"""
     import hashlib as H
 
     import mysticeti_amd as M
     import mysticeti_amd.blocks as MB
 
     monkeypatch.setenv("MV_COMB_SPLIT_BYTES", split)
+    monkeypatch.setenv("MV_ONLINE", "0")
     test_block_edge_cases(engine, golden)
     test_mixed_lengths_and_failures(engine)
     bins = list(MB.config4(engine, rounds=1))[:64]

@@ -230,9 +230,9 @@ def test_online_service_does_not_block_other_streams(engine, monkeypatch):
 
 
 def test_online_service_size_limits_and_garbage(engine, monkeypatch):
-    """The service takes calls of <= 64 short blocks; 65 blocks, long blocks and mixed calls go
-    through the queue. Truncated, garbage and empty-length blocks give the queue path's verdicts
-    (PARSE_ERROR, zero digests) either way."""
+    """The service takes calls of <= 64 blocks and <= 128 KB (long blocks included); 65 blocks
+    go through the queue (as do long blocks under MV_ONLINE_LONG=0). Truncated, garbage and
+    empty-length blocks give the queue path's verdicts (PARSE_ERROR, zero digests) either way."""
     bins, pks, stakes = ragged_blocks(n_rounds=20, seed=21)
     engine.set_committee(pks, stakes, 0)
     short = [b for b in bins if len(b) < 1200]
@@ -250,9 +250,44 @@ def test_online_service_size_limits_and_garbage(engine, monkeypatch):
         for a, b in zip(got, w):
             assert (a == b).all()
         packed = sum((len(x) + 7) & ~7 for x in c)
-        short_call = len(c) <= 64 and packed <= (128 << 10) and ((packed + 16 + 15) & ~15) < 2048 * len(c)
-        assert took == (1 if short_call else 0), (len(c), took)
+        small_call = len(c) <= 64 and packed <= (128 << 10) and max(len(x) for x in c) + 32 <= 10240
+        assert took == (1 if small_call else 0), (len(c), took)
     assert int(want[3][0][0]) == M.BLOCK_PARSE_ERROR and not want[3][1][0].any()
+
+
+def test_online_service_long_blocks(engine, monkeypatch):
+    """Config-4-shaped blocks (~9.5 KB, 66 VoteRanges, a 512-B share) take the service: one per
+    call, and 12 in one call (< 128 KB), with a bad signature and a tampered digest among them;
+    verdicts and both digests equal the queue path's and the oracle's."""
+    import hashlib as H
+
+    import mysticeti_amd.blocks as MB
+
+    bins = list(MB.config4(engine, rounds=1))[:12]
+    pks, stakes = MB.committee(engine, 100, distinct=True)
+    engine.set_committee(pks, stakes, 0)
+    b = bytearray(bins[3])  # an s bit: SIG_INVALID once the digest is recomputed
+    b[-20] ^= 0x10
+    b[24:56] = H.blake2b(M.block_preimage(bytes(b)) + bytes(b[-64:]), digest_size=32).digest()
+    bins[3] = bytes(b)
+    b = bytearray(bins[7])  # a stale claimed digest
+    b[30] ^= 1
+    bins[7] = bytes(b)
+    calls = [bins[:1], bins[3:4], bins[7:8], bins]
+    monkeypatch.setenv("MV_ONLINE", "0")
+    want = [engine.verify_blocks(c) for c in calls]
+    monkeypatch.delenv("MV_ONLINE")
+    for c, w in zip(calls, want):
+        o0 = engine.online_stats()[0]
+        got = engine.verify_blocks(c)
+        assert engine.online_stats()[0] - o0 == 1
+        for x, y in zip(got, w):
+            assert (x == y).all()
+    st, md, bd = want[-1]
+    for i in (0, 3, 7, 11):
+        ost, omd, obd = O.block_verify(bins[i], pks, stakes, 0)
+        assert int(st[i]) == ost and md[i].tobytes() == omd and bd[i].tobytes() == obd, i
+    assert int(st[3]) == 6 and int(st[7]) != 0
 
 
 def test_online_service_survives_committee_changes(engine):
