@@ -508,6 +508,7 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // uniform (the role is the workgroup's, decisions are broadcast through LDS), and every wait
 // loop also tests the launch's end, so all waves leave.
 constexpr uint32_t ON_BATCH = 32;  // requests the poller moves per pass
+constexpr uint32_t ON_COPY_UNROLL = 8;  // 16-B input loads per poller thread in flight
 static_assert(IG_WIN == mvk::INGEST_WINDOW_BYTES, "the host's eligibility test uses the ingest window");
 
 // Workgroup 0: moves published requests from page-locked memory into HBM, appends their jobs.
@@ -593,14 +594,44 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       pre[cnt] = c;
     }
     __syncthreads();
-    // inputs: 16-byte chunk k of the batch by thread k (mod the workgroup), all independent
+    // inputs: 16-byte chunk k of the batch by thread k (mod the workgroup), all independent;
+    // ON_COPY_UNROLL loads per thread in flight before their stores, so a round of PCIe reads
+    // moves 256 x 8 x 16 B = 32 KB (one round trip instead of one per 4 KB: a 64-block request
+    // of config-1 blocks is ~25 KB)
     const uint32_t total = pre[cnt];
-    for (uint32_t k = t; k < total; k += blockDim.x) {
-      uint32_t i = 0;
-      while (pre[i + 1] <= k) i++;
-      const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS), c = k - pre[i];
-      reinterpret_cast<uint4*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot)[c] =
-          reinterpret_cast<const uint4*>(A.in_host + mvk::ONLINE_IN_STRIDE * slot)[c];
+    // (a lane past the end copies its own 16 bytes of HBM sink onto themselves: no branch around
+    // the loads, so they all stay in registers and in flight together, and no extra PCIe read)
+    if (total <= blockDim.x) {  // one chunk per thread at most (a few small requests): one load each
+      if (t < total) {
+        uint32_t i = 0;
+        while (pre[i + 1] <= t) i++;
+        const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS), c = t - pre[i];
+        reinterpret_cast<uint4*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot)[c] =
+            reinterpret_cast<const uint4*>(A.in_host + mvk::ONLINE_IN_STRIDE * slot)[c];
+      }
+    } else for (uint32_t k0 = 0; k0 < total; k0 += blockDim.x * ON_COPY_UNROLL) {
+      uint64_t src[ON_COPY_UNROLL], dst[ON_COPY_UNROLL];
+#pragma unroll
+      for (uint32_t u = 0; u < ON_COPY_UNROLL; u++) {
+        const uint32_t kk = k0 + u * blockDim.x + t;
+        const bool live = kk < total;
+        const uint32_t k = live ? kk : 0u;
+        uint32_t i = 0;
+        while (pre[i + 1] <= k) i++;
+        const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS), c = k - pre[i];
+        const uint64_t sink = (uint64_t)(dev->sink + 2 * t);
+        src[u] = live ? (uint64_t)(A.in_host + mvk::ONLINE_IN_STRIDE * slot + 16 * (size_t)c) : sink;
+        dst[u] = live ? (uint64_t)(A.scr + mvk::ONLINE_SCR_STRIDE * slot + 16 * (size_t)c) : sink;
+      }
+      uint64_t lo[ON_COPY_UNROLL], hi[ON_COPY_UNROLL];
+#pragma unroll
+      for (uint32_t u = 0; u < ON_COPY_UNROLL; u++) {
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src[u]);
+        lo[u] = x.x;
+        hi[u] = x.y;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < ON_COPY_UNROLL; u++) *reinterpret_cast<ulonglong2*>(dst[u]) = make_ulonglong2(lo[u], hi[u]);
     }
     __threadfence();  // the inputs before the jobs (agent scope)
     __syncthreads();

@@ -170,6 +170,7 @@ struct OnlineDev {
   uint32_t n[ONLINE_SLOTS];
   uint32_t jobs_done[ONLINE_SLOTS];
   unsigned long long jobs[ONLINE_JOBS];  // (request << 8) | job
+  uint64_t sink[2 * 1024];               // 16 B per poller thread: where its copy lanes past the end go
 };
 struct OnlineArgs {
   OnlineCtl* ctl;                 // page-locked (device view)
