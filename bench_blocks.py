@@ -194,7 +194,8 @@ def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None
     out = {"unit": "us", "host_cpu": _host_cpu(), "cpu_threads": threads, "cpu_threads_source": share_src,
            "shapes": {}}
     ok = True
-    for shape in ("config1", "config4"):
+    shapes = [x for x in os.environ.get("MV_BENCH_C5_SHAPES", "config1,config4").split(",") if x]  # diagnostics
+    for shape in shapes:
         if shape == "config1":
             blocks = MB.config1(eng, rounds=64)
             pks, stakes = MB.committee(eng, 4, distinct=False)

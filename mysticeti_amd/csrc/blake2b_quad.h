@@ -257,7 +257,8 @@ MV_DEV void qh_sync() {
     __syncthreads();
   }
 }
-template <bool DUAL, int NS, bool HOIST = false, bool WAVE = false>
+// EXTRA: bytes hashed past len[i] (the staged signature after a pre-image: the block digest alone)
+template <bool DUAL, int NS, bool HOIST = false, bool WAVE = false, uint32_t EXTRA = 0>
 MV_DEV void quad_hash_range(uint32_t first, uint32_t count, const uint8_t* __restrict__ buf,
                             const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint32_t n,
                             uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
@@ -277,7 +278,7 @@ MV_DEV void quad_hash_range(uint32_t first, uint32_t count, const uint8_t* __res
     idx[k] = first + 16 * k + qd;
     live[k] = 16 * k + qd < count && idx[k] < n;
     p[k] = buf + (live[k] ? off[idx[k]] : 0);
-    pl[k].init(live[k] ? len[idx[k]] : 0, live[k]);
+    pl[k].init(live[k] ? len[idx[k]] + EXTRA : 0, live[k]);
     nsteps_max = max(nsteps_max, pl[k].nsteps);
     // whole 128-byte blocks that are neither final nor the message's last (the shared prefix)
     const uint64_t c = live[k] ? (DUAL ? pl[k].common : pl[k].last) : 0;

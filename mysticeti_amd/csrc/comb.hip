@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256) k_verify_comb(const uint8_t* msg, const u
 // (a barrier inside the power chain), then role 0's lanes 0..3 of each row subtract the sum
 // from R as a quad, clear the cofactor and test for the identity. Same predicate, same status
 // as k_verify_comb.
-template <class Mid = NoMid>
+template <int AT = 200, class Mid = NoMid>
 MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8], Mid mid = Mid()) {
   fe d, one, ya, ua, va, t, v3a, ea7, pa, xa, n;
   fe_const(d, K_D);
@@ -231,7 +231,7 @@ MV_DEV void decompress1_r16(p3& A, bool& okA, const uint32_t ea[8], Mid mid = Mi
   {
     fer x, r;
     fer_from_fe(x, ea7);
-    fer_pow_p58(r, x, mid);
+    fer_pow_p58<AT>(r, x, mid);
     fe_from_fer(pa, r);
   }
   fe_mul(pa, pa, v3a); fe_mul(pa, pa, ua);
@@ -336,23 +336,36 @@ MV_DEV void q_ct_sum_pf(fe& v, const uint4* tab, const uint32_t sd[8], int r0) {
 // signatures per workgroup (12 waves, 3 per SIMD) SHA-512 k took 27 us instead of ~10
 constexpr uint32_t C16_SIGS = 4;    // signatures per k_verify_comb16 workgroup
 constexpr uint32_t C16_TROLES = 8;  // table-sum roles: four over the B rows, four over the A rows
-// + one spare wave, which only ingests (with the other three) when the kernel parses its blocks
+// + one spare wave, which ingests (with the other three) when the kernel parses its blocks and
+// then hashes the block digests
 constexpr uint32_t C16_THREADS = 16 * C16_SIGS + C16_TROLES * 4 * C16_SIGS + 64;
 // the kernel's wall clock (100 MHz): online-service diagnostics
 MV_DEV uint64_t on_now() { return (uint64_t)wall_clock64(); }
+
+// 8 little-endian words at any byte address (9 aligned words funnel-shifted; the block buffers
+// are readable 16 bytes past each block)
+MV_DEV void load8_unaligned(uint32_t w[8], const uint8_t* p) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  uint32_t a[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a[i] = q[i];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sh ? __builtin_amdgcn_alignbyte(a[i + 1], a[i], sh) : a[i];
+}
 
 // One workgroup's share (signatures 4 wg .. 4 wg + 3) of the short-chain comb verify: the body
 // of k_verify_comb16, also run job by job by the resident online service (k_online below).
 // Two barriers: 0 after the ingest, 1 when role 0 has decoded R and the A wave has S = [s]B - [k]A.
 // Between them the waves meet through LDS flags (spins with s_sleep; every wave has its own
-// SIMD, the spare wave idles):
+// SIMD; the spare wave hashes the block digests):
 //   role 0 (wave 0, one 16-lane row per signature)  the ZIP-215 decode of R
 //   B wave (four roles of quads)   8 B rows each; then, once the A wave has published k's
 //                                  digits, 4 A rows each (rows 16..31); a lane tree over its roles
-//   A wave (four roles of quads)   the blocks' digests, SHA-512 k, k's digits -> LDS; 4 A rows
+//   A wave (four roles of quads)   the messages' digests, SHA-512 k, k's digits -> LDS; 4 A rows
 //                                  each (rows 0..15); a lane tree; + the B wave's total = S
 // then role 0: R - S, and the torsion test of qp_in_torsion (= [8](R - S) is the identity).
-// stamp (online job 0, MV_ONLINE_TRACE): barrier 0, the B rows done, S done, R decoded, barrier 1;
+// stamp (online job 0, MV_ONLINE_TRACE): barrier 0 (wave 1), the B rows done, S done, R decoded, barrier 1;
 // [7] digests done, [8] k's digits published.
 MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const uint8_t* __restrict__ pk,
                       const uint32_t* key_idx, uint32_t n, const uint4* __restrict__ combB,
@@ -372,17 +385,37 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
     kflag = 0;
     bflag = 0;
   }
-  if (ing.buf) {  // barrier 0: wave w parses block 4 b + w (ingest_dev.h) before anything reads it
-    __shared__ IngestLds igl[C16_SIGS];
-    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), bi = wg * C16_SIGS + w;
-    const CommitteeView cv{ing.stakes, ing.n_auth, ing.epoch, ing.quorum_thr};
-    const IngestOut io{ing.stage, ing.pre_off, ing.pre_len, ing.sig, ing.key_idx, ing.facts, ing.claimed};
-    if (bi < n) ingest_block<true>(bi, ing.buf, ing.off, ing.len, cv, io, igl[w]);
-    __threadfence();  // its outputs are read by the other waves after the barrier
+  // With the ingest (ing.buf), role 0 does not wait for it: it decodes R speculatively from the
+  // raw block's last 64 bytes (the signature is the bincode's last field, crypto.rs:309-347) and
+  // meets barrier 0 inside its power chain (after 45 of 263 products, about when the parse is
+  // done); waves 1..3 parse the blocks (wave 1 also the fourth) and meet it after. Role 0 then
+  // checks its R against the parsed signature and decodes again if a block differs (trailing
+  // bytes, a malformed block).
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (ing.buf) {
+    if (wv != 0) {  // barrier 0 after the parse (ingest_dev.h) of blocks 4 wg + wv - 1 (+ 3 for wave 1)
+      __shared__ IngestLds igl[C16_SIGS];
+      const CommitteeView cv{ing.stakes, ing.n_auth, ing.epoch, ing.quorum_thr};
+      const IngestOut io{ing.stage, ing.pre_off, ing.pre_len, ing.sig, ing.key_idx, ing.facts, ing.claimed};
+      for (uint32_t j = wv - 1; j < C16_SIGS; j += C16_SIGS - 1) {
+        const uint32_t bi = wg * C16_SIGS + j;
+        if (bi < n) ingest_block<true>(bi, ing.buf, ing.off, ing.len, cv, io, igl[wv]);
+      }
+      __threadfence();  // its outputs are read by the other waves after the barrier
+      __syncthreads();  // barrier 0
+    }
+  } else {
+    __syncthreads();  // barrier 0
   }
-  __syncthreads();  // barrier 0
-  if (stamp && t == 0) __hip_atomic_store(stamp, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (__builtin_amdgcn_readfirstlane(t) >= C16_THREADS - 64) {  // the spare wave: barrier 1
+  if (stamp && t == 64) __hip_atomic_store(stamp, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (__builtin_amdgcn_readfirstlane(t) >= C16_THREADS - 64) {  // the spare wave: the block digests, barrier 1
+    if (hin.stage) {
+      // B2(P || sig), the staged signature after each pre-image (one quad per block): off the
+      // A wave's chain, which then hashes P alone (DUAL's extra final blocks no longer delay k)
+      b2q::quad_hash_range<false, 1, true, true, 64>(wg * C16_SIGS, C16_SIGS, hin.stage, hin.pre_off, hin.pre_len,
+                                                     n, hin.digest, nullptr);
+      __threadfence();  // read by role 0's verdict after barrier 1
+    }
     __syncthreads();
     return;
   }
@@ -391,21 +424,37 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
   const uint32_t sq = row_role ? t >> 4 : (t >> 2) & (C16_SIGS - 1), c = t & 3u;
   const uint32_t gid = wg * C16_SIGS + sq;
   const uint32_t idx = gid < n ? gid : n - 1;
-  const uint32_t key = key_idx[idx];
-  const uint4* tabA = combA + (size_t)key * CT_TABLE;
+  uint32_t key = 0;  // role 0 reads it after barrier 0, inside its branch
   fe v;  // coordinate c of this role's point
   bool okR = false, s_ok = false;
   // the branches around the barriers and the flags are wave-uniform (readfirstlane: scalar branches)
   if (__builtin_amdgcn_readfirstlane(role) == 0) {  // every lane of the row holds the signature's R and s
     uint32_t rw[8], sw[8];
-    load8(rw, sig + 64 * (size_t)idx);
+    p3 R;
+    if (ing.buf) {
+      // speculative: the raw block's R (a block shorter than a signature reads a word of the
+      // signature array instead -- in bounds, wrong, decoded again below)
+      const uint64_t L = ing.len[idx];
+      load8_unaligned(rw, L >= 64 ? ing.buf + ing.off[idx] + L - 64 : sig + 64 * (size_t)idx);
+      decompress1_r16<40>(R, okR, rw, [&] { __syncthreads(); });        // barrier 0
+      uint32_t pw[8];
+      load8(pw, sig + 64 * (size_t)idx);  // the parsed R
+      bool same = true;
+#pragma unroll
+      for (int i = 0; i < 8; i++) same = same && pw[i] == rw[i];
+      if (__ballot(!same)) decompress1_r16(R, okR, pw);  // some row guessed wrong: decode the parsed R
+    } else {
+      load8(rw, sig + 64 * (size_t)idx);
+      decompress1_r16(R, okR, rw);
+    }
     load8(sw, sig + 64 * (size_t)idx + 32);
     s_ok = sc_is_canonical(sw);
-    p3 R;
-    decompress1_r16(R, okR, rw);
+    key = key_idx[idx];
     fe_qsel(v, c, R.X, R.Y, R.Z, R.T);
     if (stamp && t == 0) __hip_atomic_store(stamp + 3, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
+    key = key_idx[idx];
+    const uint4* tabA = combA + (size_t)key * CT_TABLE;
     const uint32_t tr = role - 1;  // 0 .. 3: the B wave's roles; 4 .. 7: the A wave's
     const bool b_wave = __builtin_amdgcn_readfirstlane(tr) < C16_TROLES / 2;
     const uint32_t wr = tr & 3u;  // the role within its wave: lanes 16 wr .. 16 wr + 15
@@ -422,10 +471,11 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
       q_ct_sum_pf<AROWS, false>(v, tabA, kd, CT_ROWS / 2 + (int)wr * AROWS);
     } else {
       if (hin.stage) {
-        // the block path's two digests of this workgroup's blocks first (one quad per block,
-        // quads 0 .. C16_SIGS - 1 of the A wave): M = msg digest feeds the challenge below
-        b2q::quad_hash_range<true, 1, true, true>(wg * C16_SIGS, C16_SIGS, hin.stage, hin.pre_off,
-                                                   hin.pre_len, n, hin.msg_digest, hin.digest);
+        // the signed message's digest of this workgroup's blocks first (one quad per block, quads
+        // 0 .. C16_SIGS - 1 of the A wave): M = B2(P) feeds the challenge below (the block digest
+        // B2(P || sig) is the spare wave's)
+        b2q::quad_hash_range<false, 1, true, true>(wg * C16_SIGS, C16_SIGS, hin.stage, hin.pre_off, hin.pre_len, n,
+                                                    hin.msg_digest, nullptr);
         __threadfence();  // the digests are read back below (other lanes) and by role 0's verdict
       }
       if (stamp && t == 128) __hip_atomic_store(stamp + 7, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
