@@ -479,12 +479,31 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
         __threadfence();  // the digests are read back below (other lanes) and by role 0's verdict
       }
       if (stamp && t == 128) __hip_atomic_store(stamp + 7, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's bytes)
-      uint32_t kin[24], h[16], k[8], kd[8];
-      load8(kin, sig + 64 * (size_t)idx);
-      load8(kin + 8, pk + 32 * (size_t)key);
-      load8(kin + 16, msg + 32 * (size_t)idx);
-      sha512_short(h, kin, 96);
+      // k = SHA-512(R || A || M) mod l over the encodings as received (A = the committee key's
+      // bytes). A workgroup with one distinct signature (a one-block request) runs it on the
+      // scalar unit (sha512s_96, wave-uniform operands); otherwise every lane runs its own
+      uint32_t h[16], k[8], kd[8];
+#ifndef MV_SCALAR_SHA
+#define MV_SCALAR_SHA 0
+#endif
+      if (MV_SCALAR_SHA && n - wg * C16_SIGS == 1) {
+        const uint32_t g2 = wg * C16_SIGS;
+        const uint32_t k2 = __builtin_amdgcn_readfirstlane(key_idx[g2]);
+        uint32_t kin[24];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          kin[i] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(sig + 64 * (size_t)g2)[i]);
+          kin[8 + i] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(pk + 32 * (size_t)k2)[i]);
+          kin[16 + i] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(msg + 32 * (size_t)g2)[i]);
+        }
+        sha512s_96(h, kin);
+      } else {
+        uint32_t kin[24];
+        load8(kin, sig + 64 * (size_t)idx);
+        load8(kin + 8, pk + 32 * (size_t)key);
+        load8(kin + 16, msg + 32 * (size_t)idx);
+        sha512_short(h, kin, 96);
+      }
       sc_reduce512(k, h);
       sc_recode256(kd, k);
       if (wr == 0 && c == 0) {

@@ -110,6 +110,59 @@ MV_DEV void sha512_compress(uint64_t st[8], uint64_t w_in[16]) {
   for (int i = 0; i < 8; i++) st[i] += v[i];
 }
 
+// The same compression in plain 64-bit C++ (shifts for the rotations, no VALU-only intrinsics):
+// called on wave-uniform values, it compiles to scalar-unit code (s_lshr_b64 / s_xor_b64 /
+// s_add_u32 + s_addc_u32), which a lone wave issues about one per cycle, against one VALU
+// instruction per 4 cycles -- the latency form for one signature (comb.hip's online job).
+MV_DEV uint64_t rotr64s(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+template <int T>
+MV_DEV void sha512s_round(uint64_t (&v)[8], uint64_t (&w)[16]) {
+  constexpr int j = T & 15, r = T & 7;
+  if constexpr (T >= 16) {
+    const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+    const uint64_t s0 = rotr64s(w15, 1) ^ rotr64s(w15, 8) ^ (w15 >> 7);
+    const uint64_t s1 = rotr64s(w2, 19) ^ rotr64s(w2, 61) ^ (w2 >> 6);
+    w[j] += s0 + w[(j + 9) & 15] + s1;
+  }
+  uint64_t& h = v[(15 - r) & 7];
+  uint64_t& d = v[(11 - r) & 7];
+  const uint64_t a = v[(8 - r) & 7], b = v[(9 - r) & 7], c = v[(10 - r) & 7];
+  const uint64_t e = v[(12 - r) & 7], f = v[(13 - r) & 7], g = v[(14 - r) & 7];
+  const uint64_t S1 = rotr64s(e, 14) ^ rotr64s(e, 18) ^ rotr64s(e, 41);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t t1 = h + S1 + ch + SHA512_K[T] + w[j];
+  const uint64_t S0 = rotr64s(a, 28) ^ rotr64s(a, 34) ^ rotr64s(a, 39);
+  const uint64_t maj = (a & b) | (c & (a | b));
+  d += t1;
+  h = t1 + S0 + maj;
+}
+template <int... T>
+MV_DEV void sha512s_rounds(uint64_t (&v)[8], uint64_t (&w)[16], std::integer_sequence<int, T...>) {
+  (sha512s_round<T>(v, w), ...);
+}
+// SHA-512 of 96 bytes given as 24 little-endian 32-bit words, all wave-uniform; out as
+// sha512_short's (16 little-endian words of the digest)
+MV_DEV void sha512s_96(uint32_t out[16], const uint32_t in[24]) {
+  uint64_t w[16], v[8], st[8];
+#pragma unroll
+  for (int i = 0; i < 12; i++)
+    w[i] = ((uint64_t)__builtin_bswap32(in[2 * i]) << 32) | __builtin_bswap32(in[2 * i + 1]);
+  w[12] = 0x8000000000000000ull;
+  w[13] = 0;
+  w[14] = 0;
+  w[15] = 96 * 8;
+  sha512_init(st);
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = st[i];
+  sha512s_rounds(v, w, std::make_integer_sequence<int, 80>{});
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t le = bswap64(st[i] + v[i]);
+    out[2 * i] = (uint32_t)le;
+    out[2 * i + 1] = (uint32_t)(le >> 32);
+  }
+}
+
 // SHA-512 of up to 111 bytes given as little-endian 32-bit words (nbytes % 4 == 0);
 // out = 16 little-endian 32-bit words of the 64-byte digest.
 MV_DEV void sha512_short(uint32_t out[16], const uint32_t* in, int nbytes) {
