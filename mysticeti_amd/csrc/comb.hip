@@ -387,7 +387,7 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
   }
   // With the ingest (ing.buf), role 0 does not wait for it: it decodes R speculatively from the
   // raw block's last 64 bytes (the signature is the bincode's last field, crypto.rs:309-347) and
-  // meets barrier 0 inside its power chain (after 45 of 263 products, about when the parse is
+  // meets barrier 0 inside its power chain (after 24 of 263 products, about when the parse is
   // done); waves 1..3 parse the blocks (wave 1 also the fourth) and meet it after. Role 0 then
   // checks its R against the parsed signature and decodes again if a block differs (trailing
   // bytes, a malformed block).
@@ -436,7 +436,10 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
       // signature array instead -- in bounds, wrong, decoded again below)
       const uint64_t L = ing.len[idx];
       load8_unaligned(rw, L >= 64 ? ing.buf + ing.off[idx] + L - 64 : sig + 64 * (size_t)idx);
-      decompress1_r16<40>(R, okR, rw, [&] { __syncthreads(); });        // barrier 0
+#ifndef MV_SPEC_AT
+#define MV_SPEC_AT 20  // barrier 0 after 24 of the chain's products (about when the parse is done; 40: +2% less, r04at)
+#endif
+      decompress1_r16<MV_SPEC_AT>(R, okR, rw, [&] { __syncthreads(); });  // barrier 0
       uint32_t pw[8];
       load8(pw, sig + 64 * (size_t)idx);  // the parsed R
       bool same = true;

@@ -140,14 +140,14 @@ MV_DEV void fe_from_fer(fe& r, const fer& x) {
 }
 
 // x^((p-5)/8) on one row: fe_pow22501's addition chain (fe_q4.h's feq_pow_p58). mid() runs
-// once x^(2^AT - 1) is formed: AT = 200 after 208 of 263 products, AT = 40 after 45 (a caller's
+// once x^(2^AT - 1) is formed: AT = 200 after 208 of 263 products, 40 after 45, 20 after 24 (a caller's
 // workgroup barrier there lets other waves sync while the chain goes on)
 struct NoMid {
   MV_DEV void operator()() const {}
 };
 template <int AT = 200, class Mid = NoMid>
 MV_DEV void fer_pow_p58(fer& r, const fer& x, Mid mid = Mid()) {
-  static_assert(AT == 40 || AT == 200, "mid() positions");
+  static_assert(AT == 20 || AT == 40 || AT == 200, "mid() positions");
   const r16::Consts K = r16::consts();
   fer t0, t1, t2, t3, t5, t7, t13, t15, a;
   fer_sq(t0, x, K);          // 2
@@ -160,6 +160,7 @@ MV_DEV void fer_pow_p58(fer& r, const fer& x, Mid mid = Mid()) {
   fer_mul(t7, a, t5, K);     // 2^10-1
   fer_sqn(a, t7, 10, K);
   fer_mul(t1, a, t7, K);     // 2^20-1
+  if constexpr (AT == 20) mid();
   fer_sqn(a, t1, 20, K);
   fer_mul(a, a, t1, K);      // 2^40-1
   if constexpr (AT == 40) mid();
