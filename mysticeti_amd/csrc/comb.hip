@@ -437,7 +437,7 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
       const uint64_t L = ing.len[idx];
       load8_unaligned(rw, L >= 64 ? ing.buf + ing.off[idx] + L - 64 : sig + 64 * (size_t)idx);
 #ifndef MV_SPEC_AT
-#define MV_SPEC_AT 20  // barrier 0 after 24 of the chain's products (about when the parse is done; 40: +2% less, r04at)
+#define MV_SPEC_AT 20  // barrier 0 after 24 of the chain's products, about when the parse is done (40: 2% fewer blocks/s, r04at)
 #endif
       decompress1_r16<MV_SPEC_AT>(R, okR, rw, [&] { __syncthreads(); });  // barrier 0
       uint32_t pw[8];
