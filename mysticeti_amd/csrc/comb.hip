@@ -392,19 +392,24 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
   // checks its R against the parsed signature and decodes again if a block differs (trailing
   // bytes, a malformed block).
   const uint32_t wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (ing.buf) {
-    if (wv != 0) {  // barrier 0 after the parse (ingest_dev.h) of blocks 4 wg + wv - 1 (+ 3 for wave 1)
-      __shared__ IngestLds igl[C16_SIGS];
-      const CommitteeView cv{ing.stakes, ing.n_auth, ing.epoch, ing.quorum_thr};
-      const IngestOut io{ing.stage, ing.pre_off, ing.pre_len, ing.sig, ing.key_idx, ing.facts, ing.claimed};
-      for (uint32_t j = wv - 1; j < C16_SIGS; j += C16_SIGS - 1) {
-        const uint32_t bi = wg * C16_SIGS + j;
-        if (bi < n) ingest_block<true>(bi, ing.buf, ing.off, ing.len, cv, io, igl[wv]);
-      }
-      __threadfence();  // its outputs are read by the other waves after the barrier
-      __syncthreads();  // barrier 0
+#ifndef MV_SPEC_MAX
+#define MV_SPEC_MAX 3  // blocks per workgroup up to which role 0 decodes speculatively
+#endif
+  // speculation when waves 1..3 can parse the workgroup's blocks one each; with four blocks all
+  // four waves parse (one each) and role 0 decodes after barrier 0
+  const bool spec = ing.buf && n - wg * C16_SIGS <= MV_SPEC_MAX;  // workgroup-uniform
+  if (ing.buf && (!spec || wv != 0)) {  // barrier 0 after the parse (ingest_dev.h)
+    __shared__ IngestLds igl[C16_SIGS];
+    const CommitteeView cv{ing.stakes, ing.n_auth, ing.epoch, ing.quorum_thr};
+    const IngestOut io{ing.stage, ing.pre_off, ing.pre_len, ing.sig, ing.key_idx, ing.facts, ing.claimed};
+    const uint32_t first = spec ? wv - 1 : wv, step = spec ? C16_SIGS - 1 : C16_SIGS;
+    for (uint32_t j = first; j < C16_SIGS; j += step) {
+      const uint32_t bi = wg * C16_SIGS + j;
+      if (bi < n) ingest_block<true>(bi, ing.buf, ing.off, ing.len, cv, io, igl[wv]);
     }
-  } else {
+    __threadfence();  // its outputs are read by the other waves after the barrier
+    __syncthreads();  // barrier 0
+  } else if (!ing.buf) {
     __syncthreads();  // barrier 0
   }
   if (stamp && t == 64) __hip_atomic_store(stamp, on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -431,7 +436,7 @@ MV_DEV void comb16_wg(uint32_t wg, const uint8_t* msg, const uint8_t* sig, const
   if (__builtin_amdgcn_readfirstlane(role) == 0) {  // every lane of the row holds the signature's R and s
     uint32_t rw[8], sw[8];
     p3 R;
-    if (ing.buf) {
+    if (spec) {
       // speculative: the raw block's R (a block shorter than a signature reads a word of the
       // signature array instead -- in bounds, wrong, decoded again below)
       const uint64_t L = ing.len[idx];
