@@ -598,6 +598,7 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
   uint64_t t_busy = t_start;
+  uint64_t why = 0;  // wave 0: why the launch ends (mvk::ONLINE_EXIT_*)
   if (t == 0) {  // this launch's setup: tickets of earlier launches are void
     const unsigned long long tl = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&dev->jobs_head, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -638,9 +639,15 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       if (cnt) {
         kind = 1;
         t_busy = now;
-      } else if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
-                 now - t_busy > A.idle_ticks || now - t_start > A.max_ticks) {
+      } else if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
         kind = 2;
+        why = mvk::ONLINE_EXIT_STOP;
+      } else if (now - t_busy > A.idle_ticks) {
+        kind = 2;
+        why = mvk::ONLINE_EXIT_IDLE;
+      } else if (now - t_start > A.max_ticks) {
+        kind = 2;
+        why = mvk::ONLINE_EXIT_MAX;
       }
       if (t == 0) {
         sh[0] = kind;
@@ -653,7 +660,18 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
     const uint32_t kind = sh[0], cnt = sh[3];
     const uint64_t rdy = (uint64_t)sh[1] | ((uint64_t)sh[2] << 32);
     if (kind == 2) {
-      if (t == 0) __hip_atomic_store(&dev->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(&dev->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        // the exit record for the host's bounded stop (diagnostics when a launch will not end)
+        __hip_atomic_store(&ctl->exit_why, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&ctl->exit_ready, rdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&ctl->exit_head,
+                           (uint64_t)__hip_atomic_load(&dev->jobs_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&ctl->exit_tail,
+                           (uint64_t)__hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       return;
     }
     if (kind == 0) {
@@ -839,10 +857,16 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
 }
 
 __global__ void __launch_bounds__(C16_THREADS) k_online(const mvk::OnlineArgs A) {
+  // liveness: this workgroup runs launch A.launch, then has left it (the host's bounded stop
+  // reads these words when a launch does not end in time)
+  uint32_t* live = &A.ctl->wg[blockIdx.x];
+  if (threadIdx.x == 0) __hip_atomic_store(live, A.launch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (blockIdx.x == 0)
     online_poller(A);
   else
     online_worker(A);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(live, A.launch | mvk::ONLINE_WG_LEFT, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The same predicate split in two, for small batches of long blocks (config 5, 8-KB

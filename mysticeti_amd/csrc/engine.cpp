@@ -1009,6 +1009,7 @@ constexpr size_t kOnOutStride = mvk::ONLINE_OUT_STRIDE;  // md[64] | bd[64] | st
 struct OnlineSvc {
   std::mutex mu;
   bool ready = false, failed = false, launched = false;
+  bool stuck = false;  // a launch that would not end: its stream and memory are never released
   hipStream_t stream = nullptr;
   hipEvent_t exited = nullptr;
   mvk::OnlineCtl* ctl = nullptr;  // host view (pinned, coherent)
@@ -1119,6 +1120,7 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   }
   const char* ge = getenv("MV_ONLINE_WGS");  // resident workgroups (4-block jobs in flight)
   o.grid = (uint32_t)(ge ? std::max(2, atoi(ge)) : (want > 0 ? want : 64));  // >= 2: the poller + workers
+  o.grid = std::min<uint32_t>(o.grid, mvk::ONLINE_MAX_WGS);
   o.ready = true;
   return MV_OK;
 }
@@ -1178,17 +1180,69 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   return MV_OK;
 }
 
-// Stops the kernel once it is idle and waits for it (o.mu held).
-void online_stop(OnlineSvc& o) {
-  if (!o.ready || !o.launched) return;
+// Polls ev until it completes or limit_ms pass (no blocking runtime wait, which cannot be
+// bounded); true once complete.
+bool event_done_within(hipEvent_t ev, int64_t limit_ms) {
+  const int64_t t0 = steady_ns();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return true;
+    (void)hipGetLastError();
+    if (q != hipErrorNotReady) return true;  // an error: nothing more will complete on it
+    if (steady_ns() - t0 > limit_ms * 1000000) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+// The service's state words, for a launch that does not end in time (stderr).
+void online_dump(const OnlineSvc& o, const char* why) {
+  const mvk::OnlineCtl* c = o.ctl;
+  uint32_t running = 0, left = 0, other = 0;
+  std::string stuck;
+  for (uint32_t g = 0; g < o.grid && g < mvk::ONLINE_MAX_WGS; g++) {
+    const uint32_t w = __atomic_load_n(&c->wg[g], __ATOMIC_ACQUIRE);
+    if (w == o.launch_no) {
+      running++;
+      if (stuck.size() < 96) stuck += " " + std::to_string(g);
+    } else if (w == (o.launch_no | mvk::ONLINE_WG_LEFT)) {
+      left++;
+    } else {
+      other++;
+    }
+  }
+  fprintf(stderr,
+          "[online] %s: launch %u grid %u: %u workgroups running (%s), %u left, %u not started; stop %llu tail %llu "
+          "next_q %llu; poller exit: why %llu ready %llu jobs_head %llu jobs_tail %llu\n",
+          why, o.launch_no, o.grid, running, stuck.empty() ? "-" : stuck.c_str() + 1, left, other,
+          (unsigned long long)c->stop, (unsigned long long)c->tail, (unsigned long long)o.next_q,
+          (unsigned long long)c->exit_why, (unsigned long long)c->exit_ready, (unsigned long long)c->exit_head,
+          (unsigned long long)c->exit_tail);
+}
+
+// Stops the kernel once it is idle and waits for it, bounded (o.mu held). The launch's own
+// limits end every wave within max_ticks + idle (60 s + MV_ONLINE_IDLE_US); a launch still
+// running well past that is reported (online_dump) and the service is left stuck: its memory is
+// then never freed (the kernel may still touch it). Returns false in that case.
+bool online_stop(OnlineSvc& o) {
+  if (!o.ready || !o.launched) return true;
   __atomic_store_n(&o.ctl->stop, 1ull, __ATOMIC_RELEASE);
-  (void)hipStreamSynchronize(o.stream);
+  bool done = event_done_within(o.exited, 2000);
+  if (!done) {
+    online_dump(o, "stop: no exit after 2 s");
+    done = event_done_within(o.exited, 70000);
+    if (!done) online_dump(o, "stop: no exit after 72 s, service abandoned");
+  }
+  if (!done) {
+    o.failed = o.stuck = true;
+    return false;
+  }
   __atomic_store_n(&o.ctl->stop, 0ull, __ATOMIC_RELEASE);
   o.launched = false;
+  return true;
 }
 
 void online_release(OnlineSvc& o) {
-  online_stop(o);
+  if (!online_stop(o)) return;  // stuck: leave its stream and memory alone
   if (o.trace && o.tr_n) {
     const double n = (double)o.tr_n;
     fprintf(stderr,
@@ -1828,22 +1882,65 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   return MV_OK;
 }
 
+// Names the step a teardown is in on stderr while it takes longer than 5 s (a stall in
+// mv_destroy otherwise looks like a silent hang to whoever waits for the process).
+class PhaseWatch {
+ public:
+  explicit PhaseWatch(const char* what) : what_(what), th_([this] { run(); }) {}
+  ~PhaseWatch() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      done_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void phase(const char* p) { phase_.store(p); }
+
+ private:
+  void run() {
+    std::unique_lock<std::mutex> lk(m_);
+    for (int s = 5; !cv_.wait_for(lk, std::chrono::seconds(5), [this] { return done_; }); s += 5)
+      fprintf(stderr, "[%s] still in '%s' after %d s\n", what_, phase_.load(), s);
+  }
+  const char* what_;
+  std::atomic<const char*> phase_{"start"};
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool done_ = false;
+  std::thread th_;
+};
+
 void mv_destroy(mv_ctx* ctx) {
   if (!ctx) return;
+  PhaseWatch watch("mv_destroy");
+  watch.phase("stage events");
   (void)mv_stage_times(ctx, nullptr, nullptr, 1);  // drain pending stage events
+  bool stuck = false;
   {
+    watch.phase("online service stop");
     std::unique_lock<std::shared_mutex> cl(ctx->com_mu);
     for (auto& dev : ctx->devs)
       if (dev.online) {
         std::lock_guard<std::mutex> ol(dev.online->mu);
         (void)hipSetDevice(dev.id);
         online_release(*dev.online);  // before the device drain below: the kernel would hold it
+        stuck |= dev.online->stuck;
       }
+  }
+  if (stuck) {
+    // a resident launch that would not end still reads the engine's buffers: freeing them (or a
+    // device drain, which would wait for it) is unsafe, so the context is abandoned, not freed
+    fprintf(stderr, "[mv_destroy] the online service did not stop: the context's device memory is leaked\n");
+    return;
   }
   for (auto& dev : ctx->devs) {
     (void)hipSetDevice(dev.id);
+    watch.phase("engine stream drain");
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
+    watch.phase("device drain");
     (void)hipDeviceSynchronize();  // device-API calls may have run on the caller's streams
+    watch.phase("frees");
     for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
                       &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
                       &dev.keyok, &dev.wal_tab, &dev.wal_rec, &dev.wal_mcount, &dev.wal_mflag,
@@ -1907,7 +2004,8 @@ mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks, const uint64_t* stak
     if (dev.online) {
       std::lock_guard<std::mutex> ol(dev.online->mu);
       (void)hipSetDevice(dev.id);
-      online_stop(*dev.online);  // the resident kernel reads the tables rebuilt below
+      if (!online_stop(*dev.online))  // the resident kernel reads the tables rebuilt below
+        return set_err(ctx, MV_E_HIP, "online service: the resident kernel did not stop");
     }
   mvh::Committee c;
   c.pks.assign(pks, pks + 32 * (size_t)n);

@@ -129,6 +129,9 @@ struct BlockIngestIn {
 constexpr uint32_t ONLINE_SLOTS = 64;
 constexpr uint32_t ONLINE_MAX_BLOCKS = 64;  // 16 jobs per request
 constexpr uint32_t ONLINE_JOBS = 2048;      // job ring (>= SLOTS x 16)
+constexpr uint32_t ONLINE_MAX_WGS = 256;    // resident workgroups at most (the poller + workers)
+constexpr uint32_t ONLINE_WG_LEFT = 0x80000000u;
+constexpr uint64_t ONLINE_EXIT_STOP = 1, ONLINE_EXIT_IDLE = 2, ONLINE_EXIT_MAX = 3;
 constexpr size_t ONLINE_IN_CAP = 128u << 10;  // bincode bytes per request
 constexpr size_t online_al(size_t x) { return (x + 255) & ~(size_t)255; }
 constexpr size_t ONLINE_IN_STRIDE = online_al(16 * ONLINE_MAX_BLOCKS + ONLINE_IN_CAP + 64);  // off | len | bincode
@@ -161,6 +164,11 @@ struct OnlineCtl {
   // R decoded, barrier 1, verdict written, outputs fenced, digests done, k published (comb.hip
   // comb16_wg; diagnostics: MV_ONLINE_TRACE sums them)
   uint64_t trace[ONLINE_SLOTS][14];
+  // liveness (plain system-scope stores, read by the host's bounded stop): the workgroup's launch
+  // number while it runs, | ONLINE_WG_LEFT once it has left; the poller's exit reason and its
+  // ring words at exit (ready, jobs_head, jobs_tail)
+  uint32_t wg[ONLINE_MAX_WGS];
+  uint64_t exit_why, exit_ready, exit_head, exit_tail;
 };
 struct OnlineDev {
   unsigned long long ready;      // requests moved to HBM by the poller
