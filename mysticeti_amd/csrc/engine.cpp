@@ -1940,22 +1940,26 @@ void mv_destroy(mv_ctx* ctx) {
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
     watch.phase("device drain");
     (void)hipDeviceSynchronize();  // device-API calls may have run on the caller's streams
-    watch.phase("frees");
+    watch.phase("frees: device buffers");
     for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
                       &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
                       &dev.keyok, &dev.wal_tab, &dev.wal_rec, &dev.wal_mcount, &dev.wal_mflag,
                       &dev.wal_moff, &dev.wal_ent, &dev.wal_ff, &dev.wal_img, &dev.wal_pos, &dev.wal_tag, &dev.wal_len,
                       &dev.wal_st})
       b->release();
+    watch.phase("frees: slot scratch");
     for (int k = 0; k < Device::kSlots; k++)
       for (DevBuf* b : {&dev.bscr[k], &dev.vscr[k], &dev.sscr[k]}) b->release();
+    watch.phase("frees: block scratch");
     for (DevBuf& b : dev.blk) b.release();
+    watch.phase("frees: slot events");
     for (hipEvent_t ev : dev.slot_done)
       if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.flag_ev)
       if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : dev.sscr_done)
       if (ev) (void)hipEventDestroy(ev);
+    watch.phase("frees: pinned-input buffers");
     for (int k = 0; k < Device::kPinBufs; k++) {
       for (DevBuf* b : {&dev.pin_msg[k], &dev.pin_sig[k], &dev.pin_pk[k], &dev.pin_st[k]}) b->release();
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
@@ -1963,10 +1967,14 @@ void mv_destroy(mv_ctx* ctx) {
         if (ev) (void)hipEventDestroy(ev);
     }
     for (int k = 0; k < 2; k++) {
+      watch.phase("frees: host staging");
       dev.h_stage[k].release();
+      watch.phase("frees: copy stream");
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
+    watch.phase("frees: host flag words");
     if (dev.h_flags) (void)hipHostFree(dev.h_flags);
+    watch.phase("frees: block events, aux streams");
     for (hipEvent_t ev : dev.blk_done)
       if (ev) (void)hipEventDestroy(ev);
     auto drop_aux = [](Device::BlkAux& a) {
@@ -1976,8 +1984,10 @@ void mv_destroy(mv_ctx* ctx) {
     };
     for (auto& a : dev.blk_aux) drop_aux(a);
     for (auto& ps : dev.pset) drop_aux(ps.aux);
+    watch.phase("frees: host in/out");
     dev.h_in.release();
     dev.h_out.release();
+    watch.phase("frees: pass sets");
     for (auto& ps : dev.pset) {
       ps.h_in.release();
       ps.h_out.release();
@@ -1986,10 +1996,13 @@ void mv_destroy(mv_ctx* ctx) {
       ps.scr.release();
       if (ps.done) (void)hipEventDestroy(ps.done);
     }
+    watch.phase("frees: queue streams");
     for (hipStream_t st : dev.qstream)
       if (st) (void)hipStreamDestroy(st);
+    watch.phase("frees: engine stream");
     if (dev.stream) (void)hipStreamDestroy(dev.stream);
   }
+  watch.phase("context");
   delete ctx;
 }
 

@@ -374,6 +374,137 @@ def gen_block_edge():
     return {"committee": committee_zero(4), "cases": cases}
 
 
+def gen_block_zip215():
+    """ZIP-215 signature edge cases inside whole StatementBlocks (crypto.rs:174-189: msg =
+    Blake2b-256(pre-image), then VerificationKey::verify; types.rs:346-348: any error ->
+    InvalidSignature, status 6). Every block passes the other checks, so its status is decided
+    by the signature alone: 0 iff the pure-Python ZIP-215 predicate accepts.
+
+    Committee: authorities 0..3 hold the zero-seed key with stake 100 each (their round-1
+    blocks are every block's includes, so the threshold clock always passes); then every
+    small-order encoding (canonical, y >= p, x = 0 with the sign bit set), a mixed-order key
+    A + T for two torsion points T, a y >= p key that decodes to a point of unknown discrete
+    log, and an undecodable key, stake 1 each."""
+    import copy
+
+    real_seed = B.ZERO_SEED
+    real_pk = Z.public_key(real_seed)
+    a_sc = Z._clamp(hashlib.sha512(real_seed).digest())
+    A = Z.scalarmult(Z.B_POINT, a_sc)
+    enc = Z.small_order_encodings()
+    tors = [p for _, p in sorted(Z.torsion_points().items()) if not Z.is_identity(p)]
+    keys, notes = [real_pk] * 4, ["zero-seed key"] * 4
+    for e, canon in enc:
+        keys.append(e)
+        notes.append(f"small-order key ({'canonical' if canon else 'non-canonical'})")
+    mixed_keys = []
+    for ti in (0, 3):
+        keys.append(Z.compress(Z.add(A, tors[ti])))
+        notes.append(f"mixed-order key A + T{ti}")
+        mixed_keys.append(len(keys) - 1)
+    odd_y = None
+    for y in range(2, 19):  # a y >= p encoding that decodes, not small order
+        e = (y + Z.P).to_bytes(32, "little")
+        pt = Z.decompress(e)
+        if pt is not None and not Z.is_identity(Z.scalarmult(pt, 8)):
+            odd_y = e
+            break
+    assert odd_y is not None
+    keys.append(odd_y)
+    notes.append("non-canonical key y >= p (decodes, unknown discrete log)")
+    bad_key = None
+    for y in range(2, 100):
+        e = y.to_bytes(32, "little")
+        if Z.decompress(e) is None:
+            bad_key = e
+            break
+    keys.append(bad_key)
+    notes.append("undecodable key")
+    small_key_ids = [4 + i for i in range(len(enc))]
+    stakes = [100] * 4 + [1] * (len(keys) - 4)
+
+    r1 = B.gen_config1(Z.sign, rounds=1)  # round-1 blocks of authorities 0..3 (zero seed)
+    incs = [b.reference() for b in r1]
+    base = B.StatementBlock(0, 2, incs, [("share", b"zip215")], 2 * 10**8, False, 0)
+    cases = []
+
+    def add(author: int, make_sig, note: str):
+        b = copy.deepcopy(base)
+        b.authority = author
+        b.meta_creation_time_ns = 2 * 10**8 + len(cases)  # every block distinct
+        msg = b.signed_message()
+        b.signature = make_sig(msg)
+        b.digest = b.compute_digest()
+        sig_st = Z.verify_status(keys[author], b.signature, msg)
+        st = 0 if sig_st == Z.SIG_OK else 6
+        cases.append({"bincode": b.bincode().hex(), "status": st, "msg_digest": msg.hex(),
+                      "block_digest": b.digest.hex(), "note": f"{note} [author {author}: {notes[author]}]"})
+
+    def ka_sig(R_enc: bytes, pk: bytes, msg: bytes) -> bytes:  # a signature with R of discrete log 0
+        k = Z.sha512_mod_l(R_enc, pk, msg)
+        return R_enc + (k * a_sc % Z.L).to_bytes(32, "little")
+
+    # 1. small-order key x every small-order R encoding, s = 0: accepted (ZIP-215)
+    for ai in small_key_ids:
+        for r, canon in enc:
+            add(ai, lambda m, r=r: r + bytes(32), f"small-order R ({'canonical' if canon else 'non-canonical'}), s = 0")
+    # 2. small-order key, a real signature's R and s: rejected
+    for ai in small_key_ids[:3]:
+        add(ai, lambda m: Z.sign(real_seed, m), "real (R, s) under a small-order key")
+    # 3. the real key: an honest signature, and R of discrete log 0 in every small-order encoding
+    #    (identity / order-4 / order-2 points, canonical and non-canonical) with S = k a: the
+    #    cofactored check accepts exactly those whose R is of order dividing 8
+    add(0, lambda m: Z.sign(real_seed, m), "honest signature")
+    for r, canon in enc:
+        add(1, lambda m, r=r: ka_sig(r, real_pk, m), f"R small-order ({'canonical' if canon else 'non-canonical'}), S = k a")
+    # 4. mixed-order R = rB + T with S re-derived: accepted (cofactored)
+    for ti, T in enumerate(tors):
+        def mixed_r(m, T=T, ti=ti):
+            r = Z.sha512_mod_l(b"blk-mixed", bytes([ti]))
+            Rb = Z.compress(Z.add(Z.scalarmult(Z.B_POINT, r), T))
+            k = Z.sha512_mod_l(Rb, real_pk, m)
+            return Rb + ((r + k * a_sc) % Z.L).to_bytes(32, "little")
+        add(2, mixed_r, f"mixed-order R (torsion {ti}), S re-derived")
+    # 5. mixed-order key A + T signed with a (k over the key's own encoding): accepted
+    for ai in mixed_keys:
+        def mixed_a(m, ai=ai):
+            r = Z.sha512_mod_l(b"blk-mixedA", m)
+            Rb = Z.compress(Z.scalarmult(Z.B_POINT, r))
+            k = Z.sha512_mod_l(Rb, keys[ai], m)
+            return Rb + ((r + k * a_sc) % Z.L).to_bytes(32, "little")
+        add(ai, mixed_a, "signed with a under k(A + T)")
+        add(ai, lambda m: Z.sign(real_seed, m), "RFC 8032 signature of A under A + T (k differs)")
+    # 6. the y >= p key and the undecodable key
+    oi, bi = len(keys) - 2, len(keys) - 1
+    add(oi, lambda m: enc[0][0] + bytes(32), "small-order R, s = 0 under a y >= p key")
+    add(oi, lambda m: Z.sign(real_seed, m), "real signature under a y >= p key")
+    add(bi, lambda m: Z.sign(real_seed, m), "real signature under an undecodable key (MalformedPublicKey)")
+    add(bi, lambda m: enc[0][0] + bytes(32), "small-order R, s = 0 under an undecodable key")
+    # 7. s out of range and undecodable R for the real key
+    for name, f in [("s = l", lambda s: Z.L), ("s + l", lambda s: s + Z.L), ("s = 2^255 - 1", lambda s: 2**255 - 1),
+                    ("s high bit", lambda s: s | (1 << 255))]:
+        def s_sig(m, f=f):
+            sg = Z.sign(real_seed, m)
+            return sg[:32] + f(int.from_bytes(sg[32:], "little")).to_bytes(32, "little")
+        add(3, s_sig, name)
+    add(3, lambda m: bad_key + Z.sign(real_seed, m)[32:], "R undecodable")
+    add(3, lambda m: (Z.P + 3).to_bytes(32, "little") + Z.sign(real_seed, m)[32:], "R y >= p (y = 3)")
+    add(0, lambda m: odd_y + bytes(32), "R y >= p of unknown discrete log, s = 0")
+    add(0, lambda m: enc[0][0] + bytes(32), "R small-order, s = 0 under the real key")
+    for bit in (0, 255, 256, 511):
+        def flip(m, bit=bit):
+            sg = bytearray(Z.sign(real_seed, m))
+            sg[bit // 8] ^= 1 << (bit % 8)
+            return bytes(sg)
+        add(0, flip, f"signature bit {bit} flipped")
+    return {
+        "committee": {"pks": [k.hex() for k in keys], "stakes": stakes, "epoch": 0, "notes": notes},
+        "round1_blocks": [b.bincode().hex() for b in r1],
+        "accepted": sum(1 for c in cases if c["status"] == 0),
+        "cases": cases,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-1m", action="store_true")
@@ -383,7 +514,8 @@ def main():
 
     if args.only:
         gen = {"block_edge.json": gen_block_edge, "hash_kat.json": gen_hash_kat, "sig_kat.json": gen_sig_kat,
-               "zip215_corpus.json": gen_zip215_corpus}[args.only]
+               "zip215_corpus.json": gen_zip215_corpus,
+               "block_zip215.json": gen_block_zip215}[args.only]
         with open(os.path.join(GOLDEN, args.only), "w") as f:
             json.dump(gen(), f, indent=1)
         print("wrote", args.only)
@@ -400,6 +532,7 @@ def main():
     dump("blocks_config1.json", gen_blocks_config1())
     dump("blocks_config4_sample.json", gen_blocks_config4_sample())
     dump("block_edge.json", gen_block_edge())
+    dump("block_zip215.json", gen_block_zip215())
     if not args.skip_1m:
         spec, spec_c = gen_batch(1 << 20)
         dump("batch_config2.json", spec)
