@@ -156,11 +156,14 @@ mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes);
 
 /* The resident online service (replaces the per-call device pass for the one-task-per-peer
  * traffic of NetworkSyncer, net_sync.rs:214-221 / synchronizer.rs:146-164): mv_verify_blocks
- * calls of <= 64 short blocks (< 2 KB each on average) are posted to a ring in page-locked
- * memory that a kernel resident on a CU-masked stream polls; the caller's thread spins on its
+ * calls of <= 64 blocks and <= 128 KB of bincode, every block inside the device ingest's 10-KB
+ * window (short and config-4-shape long blocks alike; MV_ONLINE_LONG=0 restricts the service to
+ * calls averaging < MV_COMB_SPLIT_BYTES per block), are posted to a ring in page-locked memory
+ * that a kernel resident on a CU-masked stream polls; the caller's thread spins on its
  * request's done word (no launch, no event, no wake-up per call). The kernel exits after
  * MV_ONLINE_IDLE_US (default 2,000) without work and is relaunched by the next call; calls it
- * does not take (larger, long blocks, MV_FLAG_NO_ONLINE) go through the submission queue.
+ * does not take (more blocks or bytes, a block past the window, MV_FLAG_NO_ONLINE, MV_ONLINE=0)
+ * go through the submission queue, and so does every call after the service has failed.
  * Verdicts and digests are those of the queue path. Counters: requests served by the service
  * and kernel launches it needed, summed over the context's devices. */
 mv_status mv_online_stats(mv_ctx* ctx, uint64_t* requests, uint64_t* launches);
@@ -260,6 +263,15 @@ mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups);
 mv_status mv_set_stage_timing(mv_ctx* ctx, int enable);
 mv_status mv_stage_times(mv_ctx* ctx, double* ms /* MV_NSTAGES or NULL */, uint64_t* calls /* MV_NSTAGES or NULL */,
                          int reset);
+/* Runtime switches (MV_ONLINE, MV_COMB_QUAD, MV_ONLINE_IDLE_US, ...). The library
+ * reads every switch from the environment once, at mv_create -- as the reference reads its env
+ * knobs at start-up (validator.rs:104-119) -- and never per call. mv_set_option changes one
+ * afterwards, between calls (no call on ctx in flight); name is the environment name and value
+ * an integer (0 / 1 for on/off switches). Unknown names, and the switches consumed by
+ * mv_create (MV_PASS_SETS, MV_GUARD_GROUPS, MV_BASE_GROUPS), are MV_E_INVALID_ARG. No switch
+ * changes a verdict, digest or crc. */
+mv_status mv_set_option(mv_ctx* ctx, const char* name, int64_t value);
+mv_status mv_get_option(mv_ctx* ctx, const char* name, int64_t* value);
 /* Runs field/scalar primitive `op` on n lane inputs (16 words each) -> 16 words each (host buffers). */
 mv_status mv_selftest(mv_ctx* ctx, int op, const uint32_t* in, uint32_t n, uint32_t* out);
 

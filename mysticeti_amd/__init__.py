@@ -20,6 +20,7 @@ Reference interfaces mirrored (hrubaanna/mysticeti @ 2025-02-04):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Iterable, List, Optional, Sequence, Tuple
@@ -47,7 +48,7 @@ EXPORTS = [
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
     "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
     "mv_queue_stats", "mv_shard_plan", "mv_crc32", "mv_wal_verify", "mv_wal_layout", "mv_dev_wal_verify",
-    "mv_dev_crc32", "mv_host_alloc", "mv_host_free", "mv_online_stats",
+    "mv_dev_crc32", "mv_host_alloc", "mv_host_free", "mv_online_stats", "mv_set_option", "mv_get_option",
 ]
 WAL_OK, WAL_CRC_MISMATCH, WAL_NONZERO_CRC_LEN0, WAL_BAD_LENGTH = range(4)
 WAL_MAP_BITS, WAL_MAP_BITS_TEST = 24, 16  # wal.rs:95-103
@@ -114,6 +115,8 @@ def load_library(path: str = LIB_PATH):
     lib.mv_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
     lib.mv_host_free.argtypes = [vp, vp]
     lib.mv_host_free.restype = None
+    lib.mv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+    lib.mv_get_option.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
     for name in EXPORTS:
         getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int32
     _lib = lib
@@ -196,6 +199,25 @@ class Engine:
     def _check(self, rc: int, what: str):
         if rc != MV_OK:
             raise MvError(f"{what} failed ({rc}): {self.lib.mv_last_error(self.ctx).decode()}")
+
+    # ---- runtime switches (mv_set_option: the environment is read once, at mv_create) ----
+    def set_option(self, name: str, value: int):
+        self._check(self.lib.mv_set_option(self.ctx, name.encode(), int(value)), f"mv_set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        self._check(self.lib.mv_get_option(self.ctx, name.encode(), ctypes.byref(v)), f"mv_get_option({name})")
+        return v.value
+
+    @contextlib.contextmanager
+    def option(self, name: str, value: int):
+        """Sets a runtime switch for the duration of a with-block (then restores it)."""
+        old = self.get_option(name)
+        self.set_option(name, value)
+        try:
+            yield self
+        finally:
+            self.set_option(name, old)
 
     # ---- committee ----
     def set_committee(self, pks, stakes, epoch: int = 0) -> np.ndarray:

@@ -976,31 +976,15 @@ mv::BvGroups batch_groups(uint32_t n, uint32_t want) {
   return mv::BvGroups{(nchunk + cpg - 1) / cpg, cpg};
 }
 // MV_NO_KEY_AGG=1 (experiments): committee keys keep one A bucket entry per signature
-bool agg_disabled() {
-  static const bool v = [] {
-    const char* e = getenv("MV_NO_KEY_AGG");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
+bool agg_disabled(const Knobs& kn) { return kn.no_key_agg != 0; }
 
 // reduction levels with at most this many elements run four lanes per element
 // (MV_REDUCE_QUAD=<n> for experiments; 0 = never)
-uint32_t reduce_quad_max() {
-  static const int v = [] {
-    const char* e = getenv("MV_REDUCE_QUAD");
-    return e ? atoi(e) : 16384;
-  }();
-  return (uint32_t)v;
-}
+uint32_t reduce_quad_max(const Knobs& kn) { return (uint32_t)kn.reduce_quad; }
 
 // buckets per bucket-kernel lane (a power of two): MV_BV_SEG=<k> for experiments
-uint32_t bucket_segment(uint32_t) {
-  static const int env = [] {
-    const char* e = getenv("MV_BV_SEG");
-    return e ? atoi(e) : -1;
-  }();
-  uint32_t seg = env > 0 ? (uint32_t)env : 1u;  // 1: measured best for 1..16 groups with the quad reduce
+uint32_t bucket_segment(const Knobs& kn) {
+  uint32_t seg = kn.bv_seg > 0 ? (uint32_t)kn.bv_seg : 1u;  // 1: measured best for 1..16 groups with the quad reduce
   if (seg > 64) seg = 64;
   return 1u << (31 - __builtin_clz(seg));
 }
@@ -1012,7 +996,7 @@ uint32_t batch_group_size(uint32_t n, uint32_t groups) {
   return batch_groups(n, groups).cpg * mv::PART_CHUNK;
 }
 
-hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok,
@@ -1052,7 +1036,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   mark(0);
   // committee keys with their comb tables: A from the tables, and its term summed per key
   const bool com = key_idx && key_ok && comb_a;
-  const bool agg = com && n_keys > 0 && n_keys <= (uint32_t)BV_MAXKEYS && !agg_disabled();
+  const bool agg = com && n_keys > 0 && n_keys <= (uint32_t)BV_MAXKEYS && !agg_disabled(kn);
   CommitteeA ca{com ? static_cast<const uint4*>(comb_a) : nullptr, key_ok,
                 (uint32_t)(comb_table_bytes(1) / sizeof(uint4)), agg ? 1u : 0u};
   const uint32_t nw = agg ? BV_NWR : BV_NW;  // windows with bucket entries
@@ -1092,7 +1076,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
   // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
   // through memory and the reduction stays the size of one group's
-  const uint32_t seg = bucket_segment(G.count);
+  const uint32_t seg = bucket_segment(kn);
   hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
                      G.count, seg, nw, segV, segT);
   if (agg) {
@@ -1112,7 +1096,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
     const uint32_t out = (cnt + fan - 1) / fan;
     const uint32_t lanes = out * rows;
-    if (lanes <= reduce_quad_max())  // latency-bound level: four lanes per element
+    if (lanes <= reduce_quad_max(kn))  // latency-bound level: four lanes per element
       hipLaunchKernelGGL(k_bv_reduce_q, dim3((4 * lanes + 255) / 256), dim3(256), 0, s, inV, inT, cnt, fan, shift,
                          rows, nw, inT == segT ? 1u : 0u, rv[pp], rt[pp]);
     else
@@ -1132,7 +1116,7 @@ hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uin
   if (e != hipSuccess) return e;
   // exact fallback: re-verifies the signatures of every group whose equation failed
   // (R and A as k_bv_prep decoded them: no decompression)
-  e = launch_verify(msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag + 1, G.cpg * PART_CHUNK, pts,
+  e = launch_verify(kn, msg, sig, pk, key_idx, n, btab, vscratch, status, s, flag + 1, G.cpg * PART_CHUNK, pts,
                     ca.tab && ca.aggregate ? comb_a : nullptr);
   mark(6);
   return e;

@@ -50,27 +50,15 @@ namespace mvk {
 // strings per quad: 1 (the default: measured on config 4, 2 interleaved strings per quad ran
 // at the same speed -- 5.16 vs 5.11 ms -- with 60% more VGPRs). MV_B2Q_NS=2 selects the
 // interleaved kernel (experiments).
-static int b2q_ns(uint32_t) {
-  static const int env = [] {
-    const char* e = getenv("MV_B2Q_NS");
-    return e ? atoi(e) : 0;
-  }();
-  return env == 2 ? 2 : 1;
-}
+static int b2q_ns(const Knobs& kn) { return kn.b2q_ns == 2 ? 2 : 1; }
 // batch-size calls: the lane-per-string kernel (blake2b_lane.hip) unless MV_B2_LANE=0
-static bool b2_lane(uint32_t n) {
-  static const bool env = [] {
-    const char* e = getenv("MV_B2_LANE");
-    return !(e && e[0] == '0');
-  }();
-  return env && n >= MV_BATCH_MIN;
-}
+static bool b2_lane(const Knobs& kn, uint32_t n) { return kn.b2_lane != 0 && n >= MV_BATCH_MIN; }
 
-hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+hipError_t launch_blake2b_quad(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                                hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (b2_lane(n)) return launch_blake2b_lane(buf, off, len, n, out, s);
-  if (b2q_ns(n) == 2)
+  if (b2_lane(kn, n)) return launch_blake2b_lane(buf, off, len, n, out, s);
+  if (b2q_ns(kn) == 2)
     hipLaunchKernelGGL((mv::b2q::k_b2_quad<false, 2>), dim3((n + 31) / 32), dim3(64), 0, s, buf, off, len, n, out,
                        (uint8_t*)nullptr);
   else
@@ -79,13 +67,13 @@ hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const ui
   return hipGetLastError();
 }
 
-hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+hipError_t launch_block_hash_quad(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                                   uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (b2_lane(n)) return launch_block_hash_lane(buf, off, len, n, msg_out, dig_out, s);
+  if (b2_lane(kn, n)) return launch_block_hash_lane(buf, off, len, n, msg_out, dig_out, s);
   if (n < MV_BATCH_MIN)  // the online path (comb verify): latency form
     hipLaunchKernelGGL(mv::b2q::k_b2_quad_lat, dim3((n + 15) / 16), dim3(64), 0, s, buf, off, len, n, msg_out, dig_out);
-  else if (b2q_ns(n) == 2)
+  else if (b2q_ns(kn) == 2)
     hipLaunchKernelGGL((mv::b2q::k_b2_quad<true, 2>), dim3((n + 31) / 32), dim3(64), 0, s, buf, off, len, n, msg_out,
                        dig_out);
   else

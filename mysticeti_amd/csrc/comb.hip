@@ -1031,17 +1031,15 @@ hipError_t launch_comb_init(const uint8_t* enc, uint32_t nb, int negate, void* t
   return hipGetLastError();
 }
 
-bool comb_short_chain(uint32_t n) {
-  const char* qe = getenv("MV_COMB_QUAD");  // read per call: the tests switch it in-process
-  const int quad_env = qe && *qe ? atoi(qe) : -1;
-  return quad_env >= 0 ? quad_env != 0 : n <= 64u * 256u;
+bool comb_short_chain(const Knobs& kn, uint32_t n) {
+  return kn.comb_quad >= 0 ? kn.comb_quad != 0 : n <= 64u * 256u;
 }
 
-hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+hipError_t launch_verify_comb(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv, const BlockHashIn* hin,
                               const BlockIngestIn* ing) {
-  if ((hin || ing) && !comb_short_chain(n)) return hipErrorInvalidValue;  // the caller parses / hashes first
+  if ((hin || ing) && !comb_short_chain(kn, n)) return hipErrorInvalidValue;  // the caller parses / hashes first
   if (n == 0) return hipSuccess;
   const BlockVerdictOut none{};
   // short chains (k_verify_comb16: a row per R decode, quads for the table sums) up to 64
@@ -1049,7 +1047,7 @@ hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint
   // k_verify_comb / k_verify_comb16 (A/B, tests)
   const BlockHashIn nohash{};
   const BlockIngestIn noingest{};
-  if (comb_short_chain(n))
+  if (comb_short_chain(kn, n))
     hipLaunchKernelGGL(mv::k_verify_comb16, dim3((n + mv::C16_SIGS - 1) / mv::C16_SIGS), dim3(mv::C16_THREADS), 0, s,
                        msg, sig, pk, key_idx, n, (const uint4*)combB, (const uint4*)combA, key_ok, status,
                        bv ? *bv : none, hin ? *hin : nohash, ing ? *ing : noingest);

@@ -35,12 +35,46 @@ constexpr int kBlockStages = 4;
 constexpr int kWalStage0 = kBlockStage0 + kBlockStages;  // walk, crc
 static_assert(kWalStage0 + 2 == MV_NSTAGES, "stage count");
 
+// Buffers that grow retire the old allocation instead of freeing it: hipFree / hipHostFree
+// drain the whole device, which would wait for the resident online kernel (it lives while
+// online traffic flows) and for every other stream's calls. A retired block may still be read
+// by work in flight; it is freed by reap_retired (mv_destroy, mv_set_committee: with the
+// service stopped), when the device drain is harmless. (a buffer grown while the
+// service was live stalled the call for up to the kernel's lifetime.)
+struct Retired {
+  int device;
+  void* p;
+  bool host;
+};
+std::mutex g_retired_mu;
+std::vector<Retired> g_retired;
+
+void retire(void* p, bool host) {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  std::lock_guard<std::mutex> lk(g_retired_mu);
+  g_retired.push_back(Retired{d, p, host});
+}
+
+// Frees the retired blocks of `device` (its current device must be set; drains the device).
+void reap_retired(int device) {
+  std::vector<Retired> mine;
+  {
+    std::lock_guard<std::mutex> lk(g_retired_mu);
+    auto it = std::stable_partition(g_retired.begin(), g_retired.end(),
+                                    [device](const Retired& r) { return r.device != device; });
+    mine.assign(it, g_retired.end());
+    g_retired.erase(it, g_retired.end());
+  }
+  for (const Retired& r : mine) (void)(r.host ? hipHostFree(r.p) : hipFree(r.p));
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
+    if (p) retire(p, false);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 4096);
@@ -64,7 +98,7 @@ struct HostBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
+    if (p) retire(p, true);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 4096);
@@ -223,6 +257,10 @@ struct mv_ctx {
   // exclusively (the resident kernel reads the committee's tables)
   std::shared_mutex com_mu;
   std::atomic<uint64_t> online_rr{0};
+  std::vector<size_t> online_devs;  // devs[] index of the first logical shard of each GPU
+  // the runtime switches, read from the environment at mv_create (knobs_from_env) and changed
+  // only by mv_set_option (diagnostics, between calls)
+  mvk::Knobs kn;
 };
 
 struct mv_ctx::BlockReq {
@@ -390,7 +428,7 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   // committee keys: A comes from the comb tables built at mv_set_committee (no per-signature decode)
   const bool com_a = d_key_idx && dev.committee_loaded && d_pk == dev.committee_pk.as<uint8_t>() &&
                      !(ctx->flags & MV_FLAG_NO_COMB);
-  HIPCHK(ctx, mvk::launch_verify_batch(d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
+  HIPCHK(ctx, mvk::launch_verify_batch(ctx->kn, d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
                                        com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr,
                                        com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p, gate));
@@ -414,11 +452,9 @@ mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const u
   dev.sscr_next = (slot + 1) % Device::kSlots;
   if (!dev.sscr_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.sscr_done[slot], hipEventDisableTiming));
   if (dev.sscr_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.sscr_done[slot], 0));
-  if (dev.sscr[slot].cap < mvk::verify_scratch_bytes(n)) {
-    HIPCHK(ctx, hipDeviceSynchronize());  // the old buffer may still be read by another stream's call
-    HIPCHK(ctx, dev.sscr[slot].ensure(mvk::verify_scratch_bytes(n)));
-  }
-  HIPCHK(ctx, mvk::launch_verify(d_msg, d_sig, d_pk, d_key_idx, n, dev.btab.p, dev.sscr[slot].p, d_status, s));
+  // (growth retires the old buffer, which another stream's call may still read: no drain)
+  HIPCHK(ctx, dev.sscr[slot].ensure(mvk::verify_scratch_bytes(n)));
+  HIPCHK(ctx, mvk::launch_verify(ctx->kn, d_msg, d_sig, d_pk, d_key_idx, n, dev.btab.p, dev.sscr[slot].p, d_status, s));
   HIPCHK(ctx, hipEventRecord(dev.sscr_done[slot], s));
   dev.sscr_used[slot] = true;
   return MV_OK;
@@ -432,7 +468,7 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
                                    const mvk::BlockVerdictOut* bv = nullptr, const mvk::BlockHashIn* hin = nullptr,
                                    const mvk::BlockIngestIn* ing = nullptr) {
   if (!(ctx->flags & MV_FLAG_NO_COMB)) {
-    HIPCHK(ctx, mvk::launch_verify_comb(d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
+    HIPCHK(ctx, mvk::launch_verify_comb(ctx->kn, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
                                         dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv, hin, ing));
   } else {
     return enqueue_verify(ctx, dev, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, d_status, s);
@@ -446,14 +482,6 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
 // (scratch then).
 // own: scratch owned by the caller (a submission-queue pass set, whose reuse is ordered by its
 // own completion event): no ring slot, no slot events (two runtime calls less per pass).
-static bool blk_pipe() {  // MV_BLK_PIPE=0 (A/B): batch-size block calls on one stream
-  static const bool v = [] {
-    const char* e = getenv("MV_BLK_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
                          const uint64_t* d_len, uint32_t n, uint8_t* d_status, uint8_t* d_md, uint8_t* d_bd,
                          hipStream_t s, DevBuf* own = nullptr, Device::BlkAux* own_aux = nullptr) {
@@ -477,8 +505,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   DevBuf& scr = own ? *own : dev.blk[slot];
   // small batches of long blocks: the comb verify's signature-only half beside the hash
   // bytes per block from which the split pays (MV_COMB_SPLIT_BYTES: tests and experiments; 0 = never)
-  const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
-  const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
+  const uint64_t split_bytes = (uint64_t)std::max<int64_t>(0, ctx->kn.comb_split_bytes);
   const bool batch = !(ctx->flags & MV_FLAG_NO_BATCH) && n >= MV_BATCH_MIN;
   const bool split = !batch && !(ctx->flags & MV_FLAG_NO_COMB) && split_bytes && buf_bytes >= split_bytes * (uint64_t)n;
   // scratch: stage | pre_off | pre_len | sig | key_idx | facts | claimed | sig status | md | bd
@@ -490,8 +517,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   // parse and both digests in one kernel with the pre-image streamed through LDS
   // (ingest_hash.hip; 2 waves/SIMD: config 4 measured 81 M blocks/s against 101 M for the
   // two-kernel form). The split comb path always uses the two-kernel form.
-  const char* fe = getenv("MV_BLK_FUSED");  // read per call: the tests switch it in-process
-  const bool fused_ih = fe && fe[0] == '1';
+  const bool fused_ih = ctx->kn.blk_fused != 0;
   const bool need_stage = split || !fused_ih;  // the two-kernel form stages P || sig
   o += need_stage ? al(buf_bytes + 256) : al(256);
   const size_t o_poff = o;
@@ -515,9 +541,8 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   const size_t o_q = o;
   if (split) o += 2 * al(144 * nn) + al(nn);
   if (!own && scr.cap < o) {
-    // grow every ring slot at once (one device drain: another slot may still be read by a call
-    // on another stream), so the ring never allocates again at this size
-    HIPCHK(ctx, hipDeviceSynchronize());
+    // grow every ring slot at once, so the ring never allocates again at this size (the old
+    // buffers are retired, not freed: another stream's call may still read them; no drain)
     for (DevBuf& x : dev.blk) HIPCHK(ctx, x.ensure(o));
   }
   HIPCHK(ctx, scr.ensure(o));
@@ -542,14 +567,13 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   uint8_t* qflags = sbuf + al(144 * nn);
   // short blocks on the online path: the digests are computed inside the committee verify
   // (k_verify_comb16's A wave hashes its blocks before the challenge), one launch less
-  const char* hce = getenv("MV_HASH_IN_COMB");  // A/B: 0 = a separate hash launch
+  // (MV_HASH_IN_COMB=0, A/B: a separate hash launch)
   const bool hash_in_comb = !fused_ih && !split && !batch && !(ctx->flags & MV_FLAG_NO_COMB) &&
-                            mvk::comb_short_chain(n) && !(hce && hce[0] == '0');
+                            mvk::comb_short_chain(ctx->kn, n) && ctx->kn.hash_in_comb;
   const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
   // ... and the parse too: k_verify_comb16 ingests its own blocks (one wave per block), so an
   // online pass is one kernel launch (MV_INGEST_IN_COMB=0: a separate k_block_ingest, A/B)
-  const char* ice = getenv("MV_INGEST_IN_COMB");
-  const bool ingest_in_comb = hash_in_comb && !(ice && ice[0] == '0');
+  const bool ingest_in_comb = hash_in_comb && ctx->kn.ingest_in_comb;
   const mvk::BlockIngestIn ing{d_buf, d_off, d_len, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed};
   if (ingest_in_comb) {
@@ -558,7 +582,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
     HIPCHK(ctx, mark(1));
-  } else if (batch && !split && !ctx->stage_timing && n >= 2 * MV_BATCH_MIN + 64 && blk_pipe() && (!own || own_aux)) {
+  } else if (batch && !split && !ctx->stage_timing && n >= 2 * MV_BATCH_MIN + 64 && ctx->kn.blk_pipe && (!own || own_aux)) {
     // Batch-size calls, two halves: the HBM-bound parse of the second half runs on another
     // stream beside the VALU-bound hash of the first (the two streams of a caller's
     // alternating calls otherwise start in phase, parse beside parse). MV_BLK_PIPE=0: one
@@ -571,7 +595,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
       if (!ax.ev[k]) HIPCHK(ctx, hipEventCreateWithFlags(&ax.ev[k], hipEventDisableTiming));
     hipStream_t aux = ax.stream;
     auto parse = [&](uint32_t lo, uint32_t hi, hipStream_t st) {
-      return mvk::launch_block_parse(d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
+      return mvk::launch_block_parse(ctx->kn, d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
                                      com.epoch, com.quorum_threshold, stage, poff + lo, plen + lo, sig + 64 * (size_t)lo,
                                      kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
     };
@@ -581,17 +605,17 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, parse(h, n, aux));
     HIPCHK(ctx, hipEventRecord(ax.ev[1], aux));
     HIPCHK(ctx, mark(1));
-    HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, h, md, bd, s));
+    HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff, plen, h, md, bd, s));
     HIPCHK(ctx, hipStreamWaitEvent(s, ax.ev[1], 0));
-    HIPCHK(ctx, mvk::launch_block_hash(stage, poff + h, plen + h, n - h, md + 32 * (size_t)h, bd + 32 * (size_t)h, s));
+    HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff + h, plen + h, n - h, md + 32 * (size_t)h, bd + 32 * (size_t)h, s));
   } else {
-    HIPCHK(ctx, mvk::launch_block_parse(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
+    HIPCHK(ctx, mvk::launch_block_parse(ctx->kn, d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                         com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
     HIPCHK(ctx, mark(1));
     if (split)  // the hash, and beside it on workgroups of their own the signature-only terms
       HIPCHK(ctx, mvk::launch_hash_comb_pre(stage, poff, plen, n, md, bd, sig, dev.combB.p, rbuf, sbuf, qflags, s));
     else if (!hash_in_comb)
-      HIPCHK(ctx, mvk::launch_block_hash(stage, poff, plen, n, md, bd, s));
+      HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff, plen, n, md, bd, s));
   }
   // a block whose digest does not match is rejected ahead of its signature (types.rs:327-332):
   // s >= l takes it out of the batch equation, so a tampered block never fails the batch (the
@@ -600,11 +624,8 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   HIPCHK(ctx, mark(2));
   // the comb kernels write the block verdict themselves (one launch less on the online path);
   // the batch path and the MV_FLAG_NO_COMB ladder leave it to k_block_verdict
-  static const bool fuse_env = [] {  // MV_VERDICT_FUSED=0: the separate k_block_verdict (A/B)
-    const char* e = getenv("MV_VERDICT_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  const bool fused = fuse_env && !batch && !(ctx->flags & MV_FLAG_NO_COMB);
+  // (MV_VERDICT_FUSED=0, A/B: the separate k_block_verdict)
+  const bool fused = ctx->kn.verdict_fused && !batch && !(ctx->flags & MV_FLAG_NO_COMB);
   const mvk::BlockVerdictOut bv{facts, claimed, md, bd, d_status};
   if (batch) {
     st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, nullptr);
@@ -685,7 +706,7 @@ mv_status verify_blocks_host_parse(mv_ctx* ctx, const uint8_t* buf, const uint64
       HIPCHK(ctx, hipMemcpyAsync(dev.sig.p, sigs.data(), 64 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(dev.keyidx.p, kidx.data(), 4 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
       // msg digests stay on the device and feed the verify kernel directly
-      HIPCHK(ctx, mvk::launch_block_hash(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
+      HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
                                          dev.msg.as<uint8_t>(), dev.out2.as<uint8_t>(), dev.stream));
       if (!(ctx->flags & MV_FLAG_NO_BATCH) && m >= MV_BATCH_MIN) {
         mv_status st2 = enqueue_batch(ctx, dev, dev.msg.as<uint8_t>(), dev.sig.as<uint8_t>(),
@@ -756,17 +777,12 @@ inline uint64_t packed_len(const BlockItem& b) { return (b.len + 7) & ~7ull; }
 // Chunk limits: <= max_batch blocks and <= MV_BLK_CHUNK_BYTES (default 256 MiB) of bincode.
 // A host-fed call larger than one chunk streams: chunk c + 1 is packed, copied and enqueued
 // on the other pass set while chunk c runs.
-uint64_t chunk_bytes_limit() {
-  static const uint64_t v = [] {
-    const char* e = getenv("MV_BLK_CHUNK_BYTES");
-    const long long x = e ? atoll(e) : 0;
-    return x > 0 ? (uint64_t)x : (uint64_t)(256ull << 20);
-  }();
-  return v;
+uint64_t chunk_bytes_limit(const mv_ctx* ctx) {
+  return ctx->kn.blk_chunk_bytes > 0 ? (uint64_t)ctx->kn.blk_chunk_bytes : (uint64_t)(256ull << 20);
 }
 uint64_t chunk_end(mv_ctx* ctx, const BlockItem* it, uint64_t lo, uint64_t hi) {
   uint64_t j = lo, bytes = 0;
-  const uint64_t lim = chunk_bytes_limit();
+  const uint64_t lim = chunk_bytes_limit(ctx);
   while (j < hi && j - lo < ctx->max_batch && (bytes < lim || j == lo)) bytes += packed_len(it[j++]);
   return j;
 }
@@ -774,7 +790,7 @@ uint64_t chunk_end(mv_ctx* ctx, const BlockItem* it, uint64_t lo, uint64_t hi) {
 // Copies items [lo, hi) into h (their packed offsets in off[], lengths in len[]), on up to
 // `threads` threads for large chunks.
 void pack_items(uint8_t* h, uint64_t* off, uint64_t* len, const BlockItem* it, uint64_t lo, uint64_t hi,
-                size_t buf_bytes) {
+                size_t buf_bytes, int64_t pack_threads) {
   const uint32_t m = (uint32_t)(hi - lo);
   uint64_t pos = 0;
   for (uint32_t k = 0; k < m; k++) {
@@ -789,11 +805,9 @@ void pack_items(uint8_t* h, uint64_t* off, uint64_t* len, const BlockItem* it, u
       memset(h + o + l, 0, ((l + 7) & ~7ull) - l);
     }
   };
-  static const unsigned max_thr = [] {  // MV_PACK_THREADS: host threads packing a large chunk
-    const char* e = getenv("MV_PACK_THREADS");
-    const unsigned hw = std::thread::hardware_concurrency();
-    return e ? (unsigned)std::max(1, atoi(e)) : std::min(8u, hw ? hw : 4u);
-  }();
+  // MV_PACK_THREADS: host threads packing a large chunk (0: min(8, cores))
+  const unsigned hw = std::thread::hardware_concurrency();
+  const unsigned max_thr = pack_threads > 0 ? (unsigned)pack_threads : std::min(8u, hw ? hw : 4u);
   const unsigned threads = pos < (8u << 20) ? 1u : std::min<unsigned>(max_thr, m);
   if (threads <= 1) {
     copy(0, m);
@@ -839,7 +853,7 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   mv_status rc = ensure_pass_set(ctx, dev, s);
   if (rc != MV_OK) return rc;
   Device::PassSet& ps = dev.pset[s];
-  static const bool trace = getenv("MV_BLK_TRACE") != nullptr;  // diagnostics: host-side times
+  const bool trace = ctx->kn.blk_trace != 0;  // diagnostics (MV_BLK_TRACE): host-side times
   auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = trace ? now() : 0;
   const uint32_t m = (uint32_t)(hi - lo);
@@ -847,10 +861,7 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
   for (uint64_t k = lo; k < hi; k++) bytes += packed_len(it[k]);
   // small chunks (the online path): the ingest kernel reads the pinned staging over PCIe
   // itself (zero-copy) instead of waiting for an H2D copy and the launch behind it
-  static const uint64_t zc_max = [] {  // MV_BLK_ZEROCOPY=<bytes> (experiments; 0 = always copy)
-    const char* e = getenv("MV_BLK_ZEROCOPY");
-    return e ? (uint64_t)atoll(e) : (uint64_t)(1u << 20);
-  }();
+  const uint64_t zc_max = (uint64_t)std::max<int64_t>(0, ctx->kn.blk_zerocopy);  // MV_BLK_ZEROCOPY=<bytes> (0: always copy)
   // in-place DMA of pinned caller bytes (see above)
   const uint8_t* base = it[lo].p;
   uint64_t span = 0;
@@ -877,7 +888,7 @@ mv_status enqueue_block_chunk(mv_ctx* ctx, Device& dev, int s, const BlockItem* 
       hlen[k] = it[lo + k].len;
     }
   } else {
-    pack_items(h, (uint64_t*)(h + o_off), (uint64_t*)(h + o_len), it, lo, hi, buf_bytes);
+    pack_items(h, (uint64_t*)(h + o_off), (uint64_t*)(h + o_len), it, lo, hi, buf_bytes, ctx->kn.pack_threads);
   }
   HIPCHK(ctx, ps.bytes.ensure(total));
   HIPCHK(ctx, ps.out2.ensure(65 * (size_t)m + 256));
@@ -941,10 +952,7 @@ mv_status finish_block_chunk(mv_ctx* ctx, Device& dev, int s) {
   ps.inflight = false;
   HIPCHK(ctx, hipSetDevice(dev.id));
   // MV_PASS_SPIN=1 (A/B): the pass owner polls its event instead of blocking in the runtime
-  static const bool spin = [] {
-    const char* e = getenv("MV_PASS_SPIN");
-    return e && e[0] == '1';
-  }();
+  const bool spin = ctx->kn.pass_spin != 0;
   hipError_t e;
   if (spin) {
     while ((e = hipEventQuery(ps.done)) == hipErrorNotReady) std::this_thread::yield();
@@ -1008,7 +1016,10 @@ constexpr size_t kOnOutStride = mvk::ONLINE_OUT_STRIDE;  // md[64] | bd[64] | st
 
 struct OnlineSvc {
   std::mutex mu;
-  bool ready = false, failed = false, launched = false;
+  bool ready = false, launched = false;
+  // set once the service cannot serve (a failed launch, a timed-out request): later requests
+  // take the submission queue; read without o.mu by callers waiting for a slot or a verdict
+  std::atomic<bool> failed{false};
   bool stuck = false;  // a launch that would not end: its stream and memory are never released
   hipStream_t stream = nullptr;
   hipEvent_t exited = nullptr;
@@ -1022,13 +1033,10 @@ struct OnlineSvc {
   uint64_t next_q = 0;
   uint32_t grid = 0, launch_no = 0;
   std::atomic<uint64_t> requests{0}, launches{0};
-  // steady_clock ns of the last request seen done: a kernel that finished a request less than
-  // half its idle limit ago is still live (no runtime query on the request path)
-  std::atomic<int64_t> last_done_ns{0};
   uint64_t idle_us = 2000;
   // MV_ONLINE_TRACE: per-stage sums (us) -- host publish to done seen, and on the kernel's
   // clock seen -> ready -> first claim -> last job done -- printed at release
-  bool trace = false;
+  bool trace = false, debug = false;  // MV_ONLINE_TRACE, MV_ONLINE_DEBUG
   double ticks_per_us = 100.0;
   std::mutex tr_mu;
   double tr_sum[14] = {};
@@ -1038,11 +1046,6 @@ struct OnlineSvc {
 int64_t steady_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
-}
-
-bool online_enabled_env() {
-  const char* e = getenv("MV_ONLINE");  // read per call: the tests switch it in-process
-  return !(e && e[0] == '0');
 }
 
 // Whether a request of n blocks, `bytes` of 8-aligned bincode, takes the online service: the
@@ -1055,22 +1058,15 @@ bool online_enabled_env() {
 // blocks only (< MV_COMB_SPLIT_BYTES on average, as the queue's one-launch case). A block past
 // the wave-parallel ingest's LDS window (ingest_dev.h IG_WIN) goes through the queue.
 bool online_eligible(mv_ctx* ctx, uint32_t n, uint64_t bytes, uint64_t longest) {
-  if ((ctx->flags & (MV_FLAG_NO_ONLINE | MV_FLAG_NO_COMB | MV_FLAG_HOST_PARSE)) || !online_enabled_env()) return false;
+  const mvk::Knobs& kn = ctx->kn;
+  if ((ctx->flags & (MV_FLAG_NO_ONLINE | MV_FLAG_NO_COMB | MV_FLAG_HOST_PARSE)) || !kn.online) return false;
   if (n == 0 || n > kOnMax || bytes > kOnInCap) return false;
   if (longest + 32 > mvk::INGEST_WINDOW_BYTES) return false;
-  static const bool longb = [] {
-    const char* e = getenv("MV_ONLINE_LONG");
-    return !(e && e[0] == '0');
-  }();
-  const char* split_env = getenv("MV_COMB_SPLIT_BYTES");
-  const uint64_t split_bytes = split_env ? (uint64_t)atoll(split_env) : 2048ull;
+  const uint64_t split_bytes = (uint64_t)std::max<int64_t>(0, kn.comb_split_bytes);
   const uint64_t buf_bytes = (bytes + 16 + 15) & ~15ull;
-  if (!longb && split_bytes && buf_bytes >= split_bytes * (uint64_t)n) return false;
-  const char* fe = getenv("MV_BLK_FUSED");
-  const char* hce = getenv("MV_HASH_IN_COMB");
-  const char* ice = getenv("MV_INGEST_IN_COMB");
-  if ((fe && fe[0] == '1') || (hce && hce[0] == '0') || (ice && ice[0] == '0')) return false;
-  return mvk::comb_short_chain(n);
+  if (!kn.online_long && split_bytes && buf_bytes >= split_bytes * (uint64_t)n) return false;
+  if (kn.blk_fused || !kn.hash_in_comb || !kn.ingest_in_comb) return false;
+  return mvk::comb_short_chain(kn, n);
 }
 
 // Allocations and the stream (o.mu held).
@@ -1096,8 +1092,7 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   // CU mask: MV_ONLINE_CUS (default 64) CUs spread evenly over the chip; 0 = an ordinary stream
   int cus = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev.id));
-  const char* ce = getenv("MV_ONLINE_CUS");
-  int want = ce ? atoi(ce) : 64;
+  int want = (int)ctx->kn.online_cus;
   if (want > cus) want = cus;
   if (want > 0 && want < cus) {
     std::vector<uint32_t> mask((cus + 31) / 32, 0u);
@@ -1110,7 +1105,8 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     HIPCHK(ctx, hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking));
   }
   HIPCHK(ctx, hipEventCreateWithFlags(&o.exited, hipEventDisableTiming));
-  o.trace = getenv("MV_ONLINE_TRACE") != nullptr;
+  o.trace = ctx->kn.online_trace != 0;
+  o.debug = ctx->kn.online_debug != 0;
   {
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev.id) == hipSuccess && khz > 0)
@@ -1118,8 +1114,8 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     else
       (void)hipGetLastError();
   }
-  const char* ge = getenv("MV_ONLINE_WGS");  // resident workgroups (4-block jobs in flight)
-  o.grid = (uint32_t)(ge ? std::max(2, atoi(ge)) : (want > 0 ? want : 64));  // >= 2: the poller + workers
+  const int64_t ge = ctx->kn.online_wgs;  // resident workgroups (4-block jobs in flight; 0: one per CU of the mask)
+  o.grid = (uint32_t)(ge > 0 ? std::max<int64_t>(2, ge) : (want > 0 ? want : 64));  // >= 2: the poller + workers
   o.grid = std::min<uint32_t>(o.grid, mvk::ONLINE_MAX_WGS);
   o.ready = true;
   return MV_OK;
@@ -1127,7 +1123,17 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
 
 // Launches the kernel unless one is live (o.mu held).
 mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
-  if (o.launched && steady_ns() - o.last_done_ns.load(std::memory_order_relaxed) < (int64_t)o.idle_us * 500) return MV_OK;
+  if (o.launched) {
+    // the poller's liveness word (comb.hip k_online): the launch number while it runs,
+    // | ONLINE_WG_LEFT once it has left -- no runtime query on the request path. An older
+    // value means the launch has not started yet: it will see the request.
+    const uint32_t w = __atomic_load_n(&o.ctl->wg[0], __ATOMIC_ACQUIRE);
+    if (w != (o.launch_no | mvk::ONLINE_WG_LEFT)) return MV_OK;
+  }
+  if (ctx->kn.online_inject) {  // fault injection (tests): the launch fails
+    (void)hipGetLastError();
+    return set_err(ctx, MV_E_HIP, "online service: injected launch failure (MV_ONLINE_INJECT)");
+  }
   if (o.launched) {
     const hipError_t q = hipEventQuery(o.exited);
     if (q == hipErrorNotReady) {
@@ -1139,8 +1145,7 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
       return set_err(ctx, MV_E_HIP, std::string("online service: ") + hipGetErrorString(q));
     }
   }
-  const char* ie = getenv("MV_ONLINE_IDLE_US");
-  const uint64_t idle_us = ie ? (uint64_t)atoll(ie) : 2000ull;
+  const uint64_t idle_us = (uint64_t)std::max<int64_t>(0, ctx->kn.online_idle_us);
   o.idle_us = idle_us;
   __atomic_store_n(&o.ctl->stop, 0ull, __ATOMIC_RELEASE);
   HIPCHK(ctx, hipSetDevice(dev.id));
@@ -1171,7 +1176,7 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   a.idle_ticks = idle_us * per_us;
   a.max_ticks = 60000000ull * per_us;
   HIPCHK(ctx, mvk::launch_online(a, o.grid, o.stream));
-  if (getenv("MV_ONLINE_DEBUG"))
+  if (o.debug)
     fprintf(stderr, "[online] launch %u: grid %u, idle %llu us, wall clock %d kHz\n", a.launch, o.grid,
             (unsigned long long)idle_us, khz);
   HIPCHK(ctx, hipEventRecord(o.exited, o.stream));
@@ -1281,12 +1286,26 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     q = o.next_q++;
     __atomic_store_n(&o.ctl->tail, o.next_q, __ATOMIC_RELEASE);
     rc = online_ensure_running(ctx, dev, o);
-    if (rc != MV_OK) return rc;  // request q is never served: the service is marked failed
+    if (rc != MV_OK) {
+      // request q is never published, so the poller would stop at it: the service is done
+      // (every later reservation sees `failed`, every waiting caller leaves its loop)
+      o.failed = true;
+      return rc;
+    }
   }
   o.requests++;
   const uint32_t slot = (uint32_t)(q % kOnSlots);
-  if (q >= kOnSlots)  // the slot's previous request must have been read out by its owner
-    while (o.freed[slot].load(std::memory_order_acquire) != q - kOnSlots + 1) std::this_thread::yield();
+  if (q >= kOnSlots) {  // the slot's previous request must have been read out by its owner
+    const auto t0 = std::chrono::steady_clock::now();
+    while (o.freed[slot].load(std::memory_order_acquire) != q - kOnSlots + 1) {
+      // the owner of request q - 64 failed (its service failed with it) or never returns
+      if (o.failed.load(std::memory_order_relaxed) || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
+        o.failed = true;
+        return set_err(ctx, MV_E_HIP, "online service failed: ring slot never released");
+      }
+      std::this_thread::yield();
+    }
+  }
   // the slot's input: off[n] | len[n] | bincode (8-aligned blocks) | 16 zero bytes; the poller
   // copies it to the slot's HBM scratch, which every device pointer below refers to
   uint8_t* in = o.in + kOnInStride * slot;
@@ -1327,8 +1346,7 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     const auto now = std::chrono::steady_clock::now();
     if (now - t_last < std::chrono::microseconds(100)) continue;
     t_last = now;
-    static const bool dbg = getenv("MV_ONLINE_DEBUG") != nullptr;  // diagnostics: a request that waits long
-    if (dbg && now - t_start > std::chrono::milliseconds(500) &&
+    if (o.debug && now - t_start > std::chrono::milliseconds(500) &&
         (now - t_start) % std::chrono::milliseconds(500) < std::chrono::microseconds(150)) {
       const uint64_t* tr = o.ctl->trace[slot];
       fprintf(stderr, "[online] q %llu slot %u waiting %.1f ms: done %llu seq %llu tail %llu trace %llu %llu %llu %llu\n",
@@ -1344,11 +1362,12 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
       break;
     }
     rc = online_ensure_running(ctx, dev, o);
-    if (rc == MV_OK && now - t_start > std::chrono::seconds(20)) {
-      o.failed = true;  // the slot may still be written: never reuse the service
+    if (rc == MV_OK && now - t_start > std::chrono::seconds(20))
       rc = set_err(ctx, MV_E_HIP, "online service: request timed out");
+    if (rc != MV_OK) {
+      o.failed = true;  // the slot may still be written: never reuse the service
+      break;
     }
-    if (rc != MV_OK) break;
   }
   if (rc != MV_OK) return rc;
   if (o.trace) {
@@ -1371,7 +1390,6 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     if (bd) memcpy(bd + 32 * (size_t)k, ho + 32 * ((size_t)kOnMax + k), 32);
   }
   o.freed[slot].store(q + 1, std::memory_order_release);
-  o.last_done_ns.store(steady_ns(), std::memory_order_relaxed);
   return MV_OK;
 }
 
@@ -1508,10 +1526,7 @@ bool pinned_range_holds(const void* p, uint64_t bytes) {
 mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
                                 const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status, bool direct) {
   const uint64_t m = hi - lo;
-  static const int chunk_log2 = [] {  // MV_PIPE_CHUNK_LOG2 (experiments): signatures per chunk
-    const char* e = getenv("MV_PIPE_CHUNK_LOG2");
-    return e ? atoi(e) : 18;
-  }();
+  const int chunk_log2 = (int)std::min<int64_t>(30, std::max<int64_t>(10, ctx->kn.pipe_chunk_log2));  // MV_PIPE_CHUNK_LOG2
   uint64_t chunks = (m + (1ull << chunk_log2) - 1) >> chunk_log2;
   if (chunks < 2) chunks = 2;
   uint64_t cs = ((m + chunks - 1) / chunks + 1023) & ~1023ull;
@@ -1531,13 +1546,10 @@ mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, co
   uint8_t* hst = dev.h_out.as<uint8_t>();
   const uint8_t* dpk_com = dev.committee_pk.as<uint8_t>();
   const unsigned hw = std::thread::hardware_concurrency();
-  static const unsigned max_thr = [] {  // MV_PIPE_THREADS (experiments): host staging threads
-    const char* e = getenv("MV_PIPE_THREADS");
-    return e ? (unsigned)atoi(e) : 8u;
-  }();
+  const unsigned max_thr = (unsigned)std::max<int64_t>(1, ctx->kn.pipe_threads);  // MV_PIPE_THREADS: host staging threads
   const unsigned threads = hw == 0 ? 4u : std::min(max_thr, hw);
   bool staged_used[2] = {false, false};
-  static const bool trace = getenv("MV_PIPE_TRACE") != nullptr;  // diagnostics: host-side stage times
+  const bool trace = ctx->kn.pipe_trace != 0;  // diagnostics (MV_PIPE_TRACE): host-side stage times
   auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = now();
   uint64_t c = 0;
@@ -1604,11 +1616,7 @@ bool verify_host_zerocopy(mv_ctx* ctx, Device& dev, const uint8_t* msg, const ui
   if (!dm || !ds || !dk) return false;
   rc = MV_OK;
   const uint64_t m = hi - lo;
-  static const double first_frac = [] {  // the first batch's share (MV_ZC_FIRST, A/B)
-    const char* e = getenv("MV_ZC_FIRST");
-    const double v = e ? atof(e) : 0.5;
-    return v > 0.0 && v < 1.0 ? v : 0.5;
-  }();
+  const double first_frac = ctx->kn.zc_first;  // the first batch's share (MV_ZC_FIRST, A/B)
   uint64_t b0 = m <= MV_BATCH_MIN * 2 ? m : (((uint64_t)(m * first_frac) + 1023) & ~1023ull);
   if (b0 > ctx->max_batch) b0 = ctx->max_batch;
   if (m - b0 > ctx->max_batch) b0 = m - ctx->max_batch;  // two batches at most per max_batch pair
@@ -1647,30 +1655,12 @@ bool verify_host_zerocopy(mv_ctx* ctx, Device& dev, const uint8_t* msg, const ui
 // beside batch t's sort, buckets and tail (two input buffers, reuse ordered by events).
 mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
                                const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status) {
-  static const int chunk_log2 = [] {  // MV_STREAM_CHUNK_LOG2 (experiments): signatures per copy chunk
-    const char* e = getenv("MV_STREAM_CHUNK_LOG2");
-    const int v = e ? atoi(e) : 17;
-    return v < 8 ? 8 : (v > 24 ? 24 : v);
-  }();
+  const int chunk_log2 = (int)std::min<int64_t>(24, std::max<int64_t>(8, ctx->kn.stream_chunk_log2));  // MV_STREAM_CHUNK_LOG2
   const uint64_t m = hi - lo;
   // Batch sizes: shares of the call (MV_STREAM_FRACS, separated by ',' or '/'; default 0.7,0.3). The
   // last batch's prep, sort, buckets and tail follow the last copy, so the shares decrease;
   // every batch is whole 1,024s, >= MV_BATCH_MIN and <= max_batch (more batches when needed).
-  static const std::vector<double> fracs = [] {
-    std::vector<double> v;
-    const char* e = getenv("MV_STREAM_FRACS");
-    std::string x = e ? e : "0.7,0.3";
-    size_t q = 0;
-    while (q < x.size()) {
-      size_t c = x.find_first_of(",/", q);
-      if (c == std::string::npos) c = x.size();
-      const double f = atof(x.substr(q, c - q).c_str());
-      if (f > 0.0) v.push_back(f);
-      q = c + 1;
-    }
-    if (v.empty()) v.push_back(1.0);
-    return v;
-  }();
+  const std::vector<double> fracs(ctx->kn.stream_fracs, ctx->kn.stream_fracs + ctx->kn.n_stream_fracs);
   std::vector<uint32_t> sizes;
   {
     double tot = 0.0;
@@ -1777,6 +1767,99 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
 
 }  // namespace
 
+// ---- runtime switches (mvk::Knobs) -------------------------------------------
+// Read from the environment once, at mv_create -- as the reference reads its knobs at start-up
+// (validator.rs:104-119, config.rs:39-100) -- never per call: a multi-threaded host may call
+// setenv, and getenv racing it is undefined behaviour. mv_set_option changes one afterwards.
+namespace {
+enum KnobKind { K_ON, K_OFF, K_FLAG, K_INT };  // on unless "0..." | on iff "1..." | on if set | integer
+struct KnobDef {
+  const char* name;
+  int64_t mvk::Knobs::*field;
+  KnobKind kind;
+  bool create_only;  // consumed by mv_create: mv_set_option refuses it
+};
+const KnobDef kKnobs[] = {
+    {"MV_BLK_PIPE", &mvk::Knobs::blk_pipe, K_ON, false},
+    {"MV_COMB_SPLIT_BYTES", &mvk::Knobs::comb_split_bytes, K_INT, false},
+    {"MV_BLK_FUSED", &mvk::Knobs::blk_fused, K_OFF, false},
+    {"MV_HASH_IN_COMB", &mvk::Knobs::hash_in_comb, K_ON, false},
+    {"MV_INGEST_IN_COMB", &mvk::Knobs::ingest_in_comb, K_ON, false},
+    {"MV_VERDICT_FUSED", &mvk::Knobs::verdict_fused, K_ON, false},
+    {"MV_BLK_CHUNK_BYTES", &mvk::Knobs::blk_chunk_bytes, K_INT, false},
+    {"MV_PACK_THREADS", &mvk::Knobs::pack_threads, K_INT, false},
+    {"MV_BLK_TRACE", &mvk::Knobs::blk_trace, K_FLAG, false},
+    {"MV_BLK_ZEROCOPY", &mvk::Knobs::blk_zerocopy, K_INT, false},
+    {"MV_PASS_SPIN", &mvk::Knobs::pass_spin, K_OFF, false},
+    {"MV_PASS_SETS", &mvk::Knobs::pass_sets, K_INT, true},
+    {"MV_Q_LINGER_US", &mvk::Knobs::q_linger_us, K_INT, false},
+    {"MV_Q_SPIN_US", &mvk::Knobs::q_spin_us, K_INT, false},
+    {"MV_ONLINE", &mvk::Knobs::online, K_ON, false},
+    {"MV_ONLINE_LONG", &mvk::Knobs::online_long, K_ON, false},
+    {"MV_ONLINE_CUS", &mvk::Knobs::online_cus, K_INT, false},
+    {"MV_ONLINE_WGS", &mvk::Knobs::online_wgs, K_INT, false},
+    {"MV_ONLINE_IDLE_US", &mvk::Knobs::online_idle_us, K_INT, false},
+    {"MV_ONLINE_TRACE", &mvk::Knobs::online_trace, K_FLAG, false},
+    {"MV_ONLINE_DEBUG", &mvk::Knobs::online_debug, K_FLAG, false},
+    {"MV_ONLINE_INJECT", &mvk::Knobs::online_inject, K_OFF, false},
+    {"MV_PIPELINE", &mvk::Knobs::pipeline, K_INT, false},
+    {"MV_PIPE_CHUNK_LOG2", &mvk::Knobs::pipe_chunk_log2, K_INT, false},
+    {"MV_PIPE_THREADS", &mvk::Knobs::pipe_threads, K_INT, false},
+    {"MV_PIPE_TRACE", &mvk::Knobs::pipe_trace, K_FLAG, false},
+    {"MV_SIG_ZEROCOPY", &mvk::Knobs::sig_zerocopy, K_OFF, false},
+    {"MV_STREAM_CHUNK_LOG2", &mvk::Knobs::stream_chunk_log2, K_INT, false},
+    {"MV_GUARD_GROUPS", &mvk::Knobs::guard_groups, K_INT, true},
+    {"MV_BASE_GROUPS", &mvk::Knobs::base_groups, K_INT, true},
+    {"MV_NO_KEY_AGG", &mvk::Knobs::no_key_agg, K_OFF, false},
+    {"MV_REDUCE_QUAD", &mvk::Knobs::reduce_quad, K_INT, false},
+    {"MV_BV_SEG", &mvk::Knobs::bv_seg, K_INT, false},
+    {"MV_B2Q_NS", &mvk::Knobs::b2q_ns, K_INT, false},
+    {"MV_B2_LANE", &mvk::Knobs::b2_lane, K_ON, false},
+    {"MV_COMB_QUAD", &mvk::Knobs::comb_quad, K_INT, false},
+    {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
+    {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
+};
+
+const KnobDef* find_knob(const char* name) {
+  if (!name) return nullptr;
+  for (const KnobDef& d : kKnobs)
+    if (strcmp(d.name, name) == 0) return &d;
+  return nullptr;
+}
+
+mvk::Knobs knobs_from_env() {
+  mvk::Knobs k;
+  for (const KnobDef& d : kKnobs) {
+    const char* e = getenv(d.name);
+    if (!e || (!*e && d.kind != K_FLAG)) continue;
+    switch (d.kind) {
+      case K_ON: k.*d.field = e[0] != '0'; break;
+      case K_OFF: k.*d.field = e[0] == '1'; break;
+      case K_FLAG: k.*d.field = 1; break;
+      case K_INT: k.*d.field = atoll(e); break;
+    }
+  }
+  if (const char* e = getenv("MV_ZC_FIRST")) {  // the first zero-copy batch's share, in (0, 1)
+    const double v = atof(e);
+    if (v > 0.0 && v < 1.0) k.zc_first = v;
+  }
+  if (const char* e = getenv("MV_STREAM_FRACS")) {  // shares separated by ',' or '/'
+    int n = 0;
+    std::string x = e;
+    for (size_t q = 0; q < x.size() && n < 8;) {
+      size_t c = x.find_first_of(",/", q);
+      if (c == std::string::npos) c = x.size();
+      const double f = atof(x.substr(q, c - q).c_str());
+      if (f > 0.0) k.stream_fracs[n++] = f;
+      q = c + 1;
+    }
+    if (n == 0) k.stream_fracs[n++] = 1.0;
+    k.n_stream_fracs = n;
+  }
+  return k;
+}
+}  // namespace
+
 extern "C" {
 
 const char* mv_version(void) { return "mysti_verify 0.2 gfx950"; }
@@ -1806,6 +1889,25 @@ int64_t mv_block_preimage(const uint8_t* bincode, uint64_t len, uint8_t* out, ui
   return (int64_t)f.preimage_len;
 }
 
+
+mv_status mv_set_option(mv_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx) return MV_E_INVALID_ARG;
+  const KnobDef* d = find_knob(name);
+  if (!d) return set_err(ctx, MV_E_INVALID_ARG, std::string("unknown option ") + (name ? name : "(null)"));
+  if (d->create_only) return set_err(ctx, MV_E_INVALID_ARG, std::string(name) + " is read at mv_create only");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->kn.*d->field = d->kind == K_INT ? value : (value != 0);
+  return MV_OK;
+}
+
+mv_status mv_get_option(mv_ctx* ctx, const char* name, int64_t* value) {
+  if (!ctx || !value) return MV_E_INVALID_ARG;
+  const KnobDef* d = find_knob(name);
+  if (!d) return set_err(ctx, MV_E_INVALID_ARG, std::string("unknown option ") + (name ? name : "(null)"));
+  *value = ctx->kn.*d->field;
+  return MV_OK;
+}
+
 mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   if (!out) return MV_E_INVALID_ARG;
   *out = nullptr;
@@ -1815,21 +1917,15 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
   mv_ctx* ctx = new mv_ctx();
   if (cfg && cfg->max_batch) ctx->max_batch = cfg->max_batch;
   if (cfg) ctx->flags = cfg->flags;
-  if (const char* e = getenv("MV_GUARD_GROUPS")) {  // experiments: sub-batches while guarded
-    const int g = atoi(e);
-    if (g >= 1 && g <= mvk::BATCH_MAX_GROUPS) ctx->guard_groups = (uint32_t)g;
-  }
-  if (const char* e = getenv("MV_BASE_GROUPS")) {  // experiments: sub-batches when not guarded
-    const int g = atoi(e);
-    if (g >= 1 && g <= mvk::BATCH_MAX_GROUPS) ctx->base_groups = (uint32_t)g;
-  }
+  ctx->kn = knobs_from_env();  // the only environment read: every switch, once
+  if (ctx->kn.guard_groups >= 1 && ctx->kn.guard_groups <= mvk::BATCH_MAX_GROUPS)  // sub-batches while guarded
+    ctx->guard_groups = (uint32_t)ctx->kn.guard_groups;
+  if (ctx->kn.base_groups >= 1 && ctx->kn.base_groups <= mvk::BATCH_MAX_GROUPS)  // sub-batches when not guarded
+    ctx->base_groups = (uint32_t)ctx->kn.base_groups;
   // two passes in flight: four measured worse on 16 concurrent 1-block callers (68.0 k vs
   // 72.2 k blocks/s, p99 203 vs 146 us; profiles/r03/c5_pass_sets.txt)
   ctx->q_sets = 2;
-  if (const char* e = getenv("MV_PASS_SETS")) {  // A/B: block passes in flight (2 .. kPassSets)
-    const int k = atoi(e);
-    if (k >= 2 && k <= Device::kPassSets) ctx->q_sets = k;
-  }
+  if (ctx->kn.pass_sets >= 2 && ctx->kn.pass_sets <= Device::kPassSets) ctx->q_sets = (int)ctx->kn.pass_sets;
   {
     FILE* f = fopen("/dev/urandom", "rb");
     size_t got = f ? fread(ctx->secret, 1, sizeof(ctx->secret), f) : 0;
@@ -1878,6 +1974,8 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
       return MV_E_HIP;
     }
   }
+  for (size_t i = 0; i < ctx->devs.size(); i++)
+    if (i == 0 || ctx->devs[i].id != ctx->devs[i - 1].id) ctx->online_devs.push_back(i);
   *out = ctx;
   return MV_OK;
 }
@@ -1940,6 +2038,8 @@ void mv_destroy(mv_ctx* ctx) {
     if (dev.stream) (void)hipStreamSynchronize(dev.stream);
     watch.phase("device drain");
     (void)hipDeviceSynchronize();  // device-API calls may have run on the caller's streams
+    watch.phase("retired buffers");
+    reap_retired(dev.id);
     watch.phase("frees: device buffers");
     for (DevBuf* b : {&dev.btab, &dev.combB, &dev.scratch, &dev.msg, &dev.sig, &dev.pk, &dev.keyidx, &dev.status,
                       &dev.bytes, &dev.off, &dev.len, &dev.out2, &dev.committee_pk, &dev.stakes, &dev.combA,
@@ -2035,6 +2135,7 @@ mv_status mv_set_committee(mv_ctx* ctx, const uint8_t* pks, const uint64_t* stak
   for (auto& dev : ctx->devs) {
     HIPCHK(ctx, hipSetDevice(dev.id));
     HIPCHK(ctx, hipDeviceSynchronize());  // earlier device-API work may still read the old tables
+    reap_retired(dev.id);                 // (the service is stopped: the drain waits for no resident kernel)
     HIPCHK(ctx, dev.committee_pk.ensure(32 * (size_t)n));
     HIPCHK(ctx, dev.stakes.ensure(8 * (size_t)n));
     HIPCHK(ctx, dev.combA.ensure(mvk::comb_table_bytes(n)));
@@ -2087,7 +2188,7 @@ mv_status mv_blake2b256(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, co
       HIPCHK(ctx, hipMemcpyAsync(dev.bytes.p, st, pos, hipMemcpyHostToDevice, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(dev.off.p, soff.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(dev.len.p, slen.data(), 8 * (size_t)m, hipMemcpyHostToDevice, dev.stream));
-      HIPCHK(ctx, mvk::launch_blake2b(dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
+      HIPCHK(ctx, mvk::launch_blake2b(ctx->kn, dev.bytes.as<uint8_t>(), dev.off.as<uint64_t>(), dev.len.as<uint64_t>(), m,
                                       dev.out2.as<uint8_t>(), dev.stream));
       HIPCHK(ctx, hipMemcpyAsync(out + 32 * i, dev.out2.p, 32 * (size_t)m, hipMemcpyDeviceToHost, dev.stream));
       HIPCHK(ctx, hipStreamSynchronize(dev.stream));
@@ -2117,13 +2218,12 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
     // staging runs at ~10 GB/s per thread, and chunks below 2^20 cost the batch path's
     // fixed per-batch work
     // Pinned inputs (mv_host_alloc) stream: chunked DMA copies gate k_bv_prep chunk by chunk.
-    static const int pipeline = getenv("MV_PIPELINE") ? atoi(getenv("MV_PIPELINE")) : 0;
+    const int pipeline = (int)ctx->kn.pipeline;
     if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN) {
       if (pinned) {
         // MV_SIG_ZEROCOPY=1: k_bv_prep reads the pinned arrays over PCIe (no copy phase); measured
         // slower than the chunked copies (175-185 vs 191-195 M/s, profiles/r03/e2e_zerocopy_ab.txt)
-        const char* zce = getenv("MV_SIG_ZEROCOPY");
-        const bool zc = zce && zce[0] == '1';
+        const bool zc = ctx->kn.sig_zerocopy != 0;
         mv_status zrc = MV_OK;
         if (zc && verify_host_zerocopy(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, zrc)) return zrc;
         return verify_host_streamed(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
@@ -2217,7 +2317,9 @@ mv_status mv_verify_blocks(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off,
     if (online_eligible(ctx, n, bytes, longest)) {
       std::shared_lock<std::shared_mutex> cl(ctx->com_mu);
       if (committee_ready(ctx)) {
-        Device& dev = ctx->devs[ctx->online_rr.fetch_add(1) % ctx->devs.size()];
+        // one service per physical GPU: logical shards of one device (shards_per_device) share
+        // the first shard's, so there is one resident kernel per GPU, not one per shard
+        Device& dev = ctx->devs[ctx->online_devs[ctx->online_rr.fetch_add(1) % ctx->online_devs.size()]];
         {
           std::lock_guard<std::mutex> lk(ctx->mu);  // the service object (devs is fixed after mv_create)
           if (!dev.online) dev.online = std::make_shared<OnlineSvc>();
@@ -2243,16 +2345,10 @@ queue_path:
   // (net_sync.rs:214-221, 314-386) thus share GPU round trips, up to q_sets passes in flight.
   mv_ctx::BlockReq req{buf, off, len, n, status, msg_digest, block_digest};
   ctx->q_calls++;
-  static const int linger_us = [] {
-    const char* e = getenv("MV_Q_LINGER_US");  // default 50 (tools/gpu_r03w.sh, gpu_r03x.sh A/B)
-    return e ? atoi(e) : 50;
-  }();
+  const int linger_us = (int)ctx->kn.q_linger_us;  // MV_Q_LINGER_US, default 50 (profiles/r03/ab/queue_linger_*)
   // MV_Q_SPIN_US: a caller whose request is in another caller's pass polls for its verdicts
   // that long before sleeping on the queue's condition variable (no wake-up convoy on q_mu)
-  static const int spin_us = [] {
-    const char* e = getenv("MV_Q_SPIN_US");
-    return e ? atoi(e) : 0;
-  }();
+  const int spin_us = (int)ctx->kn.q_spin_us;
   bool lingered = false, spun = false;
   std::unique_lock<std::mutex> ql(ctx->q_mu);
   ctx->q.push_back(&req);
@@ -2305,7 +2401,7 @@ queue_path:
     }
     // larger than one chunk per device: the pass streams its chunks over both sets
     const uint64_t nd = ctx->devs.size();
-    const bool big = blocks > (uint64_t)ctx->max_batch * nd || bytes > chunk_bytes_limit() * nd;
+    const bool big = blocks > (uint64_t)ctx->max_batch * nd || bytes > chunk_bytes_limit(ctx) * nd;
     ctx->q_packing = true;
     if (big)
       while (any_busy()) ctx->q_cv.wait(ql);

@@ -82,18 +82,14 @@ __global__ void __launch_bounds__(256) k_block_verdict(const uint32_t* __restric
 // ---------------------------------------------------------------- launchers
 namespace mvk {
 
-hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+hipError_t launch_block_parse(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const mv::CommitteeView cv{stakes, n_auth, epoch, quorum_thr};
   const mv::IngestOut io{stage, pre_off, pre_len, sig, key_idx, facts, claimed};
-  static const bool lane_kernel = [] {
-    const char* e = getenv("MV_INGEST_LANE");  // A/B: the lane-per-block kernel
-    return e && e[0] == '1';
-  }();
-  if (lane_kernel)
+  if (kn.ingest_lane)  // A/B (MV_INGEST_LANE=1): the lane-per-block kernel
     hipLaunchKernelGGL(mv::k_block_parse, dim3((n + 255) / 256), dim3(256), 0, s, buf, off, len, n, cv, io);
   else  // (capping its workgroups per CU with padded LDS, to leave room for the other stream's
         // kernels, measured slower: 79 vs 103 M config-4 blocks/s, profiles/r03/ab/)

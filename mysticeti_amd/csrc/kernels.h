@@ -5,10 +5,63 @@
 #include <stdint.h>
 
 namespace mvk {
+// The runtime switches. Read from the environment once, at mv_create
+// (knobs_from_env in engine.cpp, the only getenv in the library), and stored in the context; the
+// diagnostics entry point mv_set_option changes one between calls (the tests select forms that
+// way). None changes a verdict, digest or crc. Launchers that choose between kernel forms take
+// the context's Knobs as their first argument.
+struct Knobs {
+  // block path (engine.cpp)
+  int64_t blk_pipe = 1;                  // MV_BLK_PIPE: batch-size block calls in two halves on two streams
+  int64_t comb_split_bytes = 2048;       // MV_COMB_SPLIT_BYTES: bytes per block from which the split comb path runs
+  int64_t blk_fused = 0;                 // MV_BLK_FUSED: the fused ingest + hash kernel
+  int64_t hash_in_comb = 1;              // MV_HASH_IN_COMB: online passes hash inside k_verify_comb16
+  int64_t ingest_in_comb = 1;            // MV_INGEST_IN_COMB: ... and parse there
+  int64_t verdict_fused = 1;             // MV_VERDICT_FUSED: the block verdict inside the comb kernels
+  int64_t blk_chunk_bytes = 256ll << 20;  // MV_BLK_CHUNK_BYTES: bytes per host-buffer block chunk
+  int64_t pack_threads = 0;              // MV_PACK_THREADS: host threads packing a chunk (0: min(8, cores))
+  int64_t blk_trace = 0;                 // MV_BLK_TRACE: host-side timing lines on stderr
+  int64_t blk_zerocopy = 1ll << 20;      // MV_BLK_ZEROCOPY: passes up to this size read pinned staging
+  int64_t pass_spin = 0;                 // MV_PASS_SPIN: the pass owner polls its event
+  int64_t pass_sets = 2;                 // MV_PASS_SETS: submission-queue pass sets (2 .. 4)
+  int64_t q_linger_us = 50;              // MV_Q_LINGER_US
+  int64_t q_spin_us = 0;                 // MV_Q_SPIN_US
+  // the resident online service
+  int64_t online = 1;                    // MV_ONLINE: small block calls take the service
+  int64_t online_long = 1;               // MV_ONLINE_LONG: long blocks take it too
+  int64_t online_cus = 64;               // MV_ONLINE_CUS: the service stream's CU mask (0: ordinary stream)
+  int64_t online_wgs = 0;                // MV_ONLINE_WGS: resident workgroups (0: = CUs)
+  int64_t online_idle_us = 2000;         // MV_ONLINE_IDLE_US: the launch ends after this long idle
+  int64_t online_trace = 0;              // MV_ONLINE_TRACE: per-stage means on stderr at release
+  int64_t online_debug = 0;              // MV_ONLINE_DEBUG: launch lines, long waits on stderr
+  int64_t online_inject = 0;             // MV_ONLINE_INJECT: fault injection (tests): launches fail
+  // signature path
+  int64_t pipeline = 0;                  // MV_PIPELINE: pageable signature staging experiment
+  int64_t pipe_chunk_log2 = 18;          // MV_PIPE_CHUNK_LOG2
+  int64_t pipe_threads = 8;              // MV_PIPE_THREADS
+  int64_t pipe_trace = 0;                // MV_PIPE_TRACE
+  int64_t sig_zerocopy = 0;              // MV_SIG_ZEROCOPY: k_bv_prep reads pinned inputs over PCIe
+  int64_t stream_chunk_log2 = 17;        // MV_STREAM_CHUNK_LOG2: signatures per copy chunk
+  int64_t guard_groups = 8;              // MV_GUARD_GROUPS: sub-batches while guarded
+  int64_t base_groups = 1;               // MV_BASE_GROUPS: sub-batches when not guarded
+  double zc_first = 0.5;                 // MV_ZC_FIRST: the first zero-copy batch's share
+  double stream_fracs[8] = {0.7, 0.3};   // MV_STREAM_FRACS: the streamed batches' shares
+  int n_stream_fracs = 2;
+  // kernel forms (the launchers)
+  int64_t no_key_agg = 0;                // MV_NO_KEY_AGG: committee A terms as bucket entries
+  int64_t reduce_quad = 16384;           // MV_REDUCE_QUAD: quad-reduce threshold
+  int64_t bv_seg = -1;                   // MV_BV_SEG: bucket segment length (-1: measured best)
+  int64_t b2q_ns = 0;                    // MV_B2Q_NS: strings per quad in k_b2_quad (2: interleaved)
+  int64_t b2_lane = 1;                   // MV_B2_LANE: batch-size BLAKE2b one lane per string
+  int64_t comb_quad = -1;                // MV_COMB_QUAD: force k_verify_comb16 (1) / k_verify_comb (0)
+  int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
+  int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
+};
+
 size_t verify_scratch_bytes(uint32_t n);
 size_t btable_bytes();
 hipError_t launch_btable_init(void* d_btab, hipStream_t s);
-hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+hipError_t launch_verify(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
                          const uint32_t* skip = nullptr, uint32_t skip_group = 0, const void* prep_pts = nullptr,
                          const void* prep_comb = nullptr);
@@ -18,15 +71,15 @@ hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* 
 // tables prep_comb when it was summed per key), and prep's nonzero statuses kept.
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
                        uint8_t* sig, hipStream_t s);
-hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+hipError_t launch_blake2b(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                           hipStream_t s);
-hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+hipError_t launch_block_hash(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                              uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
 // blake2b_quad.hip: the same two hashes with four lanes per string (launch_blake2b /
 // launch_block_hash route to them; at batch size they route on to blake2b_lane.hip)
-hipError_t launch_blake2b_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
+hipError_t launch_blake2b_quad(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
                                hipStream_t s);
-hipError_t launch_block_hash_quad(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+hipError_t launch_block_hash_quad(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                                   uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
 // blake2b_lane.hip: one lane per string (batch-size calls; the quad launchers route to it)
 hipError_t launch_blake2b_lane(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
@@ -52,7 +105,7 @@ constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
 constexpr int BATCH_MAX_GROUPS = 16;
 size_t batch_scratch_bytes(uint32_t n, uint32_t groups);
 uint32_t batch_group_size(uint32_t n, uint32_t groups);
-hipError_t launch_verify_batch(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
@@ -198,12 +251,12 @@ struct OnlineArgs {
   uint64_t idle_ticks, max_ticks;
 };
 hipError_t launch_online(const OnlineArgs& a, uint32_t grid, hipStream_t s);
-hipError_t launch_verify_comb(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+hipError_t launch_verify_comb(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
                               uint8_t* status, hipStream_t s, const BlockVerdictOut* bv = nullptr,
                               const BlockHashIn* hin = nullptr, const BlockIngestIn* ing = nullptr);
 // whether launch_verify_comb takes the short-chain kernel (the one that can fold the hash in)
-bool comb_short_chain(uint32_t n);
+bool comb_short_chain(const Knobs& kn, uint32_t n);
 // the comb verify split in two, for small batches of long blocks: k_hash_comb_pre is
 // launch_block_hash plus, on workgroups of their own, the signature-only terms (R decoded ->
 // rbuf, -[s]B -> sbuf, 144 B per signature each, flags: bit 0 s < l, bit 1 R decodes);
@@ -216,7 +269,7 @@ hipError_t launch_comb_post(const uint8_t* msg, const uint8_t* sig, const uint8_
                             const void* sbuf, const uint8_t* qflags, uint8_t* status, hipStream_t s,
                             const BlockVerdictOut* bv = nullptr);
 // ingest.hip: device-side bincode parse + pre-image staging, and the final block verdict
-hipError_t launch_block_parse(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+hipError_t launch_block_parse(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s);

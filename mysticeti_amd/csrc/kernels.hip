@@ -520,28 +520,23 @@ size_t verify_scratch_bytes(uint32_t n) {
   size_t waves = (size_t)((n + 255) / 256) * 4;  // every wave of the 256-thread grid owns a slot
   return waves * mv::WAVE_QUADS * 64 * sizeof(uint4);
 }
-static int verify_variant() {
-  static int v = [] {
-    const char* e = getenv("MV_VERIFY_OCC");
-    return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
-  }();
-  return v;
-}
+// MV_VERIFY_OCC (A/B): k_verify's waves per SIMD, 1, 2 (default) or 3
+static int verify_variant(const Knobs& kn) { return kn.verify_occ == 1 || kn.verify_occ == 3 ? (int)kn.verify_occ : 2; }
 size_t btable_bytes() { return 2 * mv::BT_TABLE * sizeof(uint4); }
 
 hipError_t launch_btable_init(void* d_btab, hipStream_t s) {
   hipLaunchKernelGGL(mv::k_btable_init, dim3(2), dim3(256), 0, s, (uint4*)d_btab);
   return hipGetLastError();
 }
-hipError_t launch_verify(const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
+hipError_t launch_verify(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                          uint32_t n, const void* btab, void* scratch, uint8_t* status, hipStream_t s,
                          const uint32_t* skip, uint32_t skip_group, const void* prep_pts, const void* prep_comb) {
   if (n == 0) return hipSuccess;
   const mv::PrepView pv{static_cast<const uint4*>(prep_pts), n, static_cast<const uint4*>(prep_comb)};
-  if (verify_variant() == 1)
+  if (verify_variant(kn) == 1)
     hipLaunchKernelGGL(mv::k_verify<1>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)btab, (uint4*)scratch, status, skip, skip_group, pv);
-  else if (verify_variant() == 3)
+  else if (verify_variant(kn) == 3)
     hipLaunchKernelGGL(mv::k_verify<3>, dim3((n + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n,
                        (const uint4*)btab, (uint4*)scratch, status, skip, skip_group, pv);
   else
@@ -557,13 +552,13 @@ hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, cons
 }
 // BLAKE2b launchers: four lanes per string on small calls (blake2b_quad.hip), one lane per
 // string at batch size (blake2b_lane.hip)
-hipError_t launch_blake2b(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
-                          hipStream_t s) {
-  return launch_blake2b_quad(buf, off, len, n, out, s);
+hipError_t launch_blake2b(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                          uint8_t* out, hipStream_t s) {
+  return launch_blake2b_quad(kn, buf, off, len, n, out, s);
 }
-hipError_t launch_block_hash(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
-                             uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
-  return launch_block_hash_quad(buf, off, len, n, msg_out, dig_out, s);
+hipError_t launch_block_hash(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len,
+                             uint32_t n, uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
+  return launch_block_hash_quad(kn, buf, off, len, n, msg_out, dig_out, s);
 }
 hipError_t launch_selftest(int op, const uint32_t* in, uint32_t n, const void* btab, uint32_t* out, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -102,4 +102,6 @@ extern "C" {
     pub fn mv_set_stage_timing(ctx: *mut mv_ctx, enable: i32) -> i32;
     pub fn mv_stage_times(ctx: *mut mv_ctx, ms: *mut f64, calls: *mut u64, reset: i32) -> i32;
     pub fn mv_selftest(ctx: *mut mv_ctx, op: i32, input: *const u32, n: u32, out: *mut u32) -> i32;
+    pub fn mv_set_option(ctx: *mut mv_ctx, name: *const c_char, value: i64) -> i32;
+    pub fn mv_get_option(ctx: *mut mv_ctx, name: *const c_char, value: *mut i64) -> i32;
 }

@@ -41,6 +41,22 @@ def engine():
     eng.close()
 
 
+@pytest.fixture
+def opts(engine):
+    """opts(name, value[, eng]): sets a runtime switch (mv_set_option; the library reads the
+    environment only at mv_create) on the session engine or `eng` for one test, restored after."""
+    saved = []
+
+    def set_opt(name, value, eng=None):
+        eng = eng or engine
+        saved.append((eng, name, eng.get_option(name)))
+        eng.set_option(name, int(value))
+
+    yield set_opt
+    for eng, name, old in reversed(saved):
+        eng.set_option(name, old)
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

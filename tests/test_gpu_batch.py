@@ -280,16 +280,16 @@ def test_pipelined_host_batches(engine, committee, pinned):
 
 @pytest.mark.parametrize("zerocopy", ["1", "0"])
 @pytest.mark.parametrize("committee", [False, True])
-def test_streamed_pinned_inputs_many_batches(committee, zerocopy, monkeypatch):
+def test_streamed_pinned_inputs_many_batches(committee, zerocopy):
     """Pinned inputs with max_batch = 8,192: a call of 5 batches + a ragged tail, on the
     zero-copy path (k_bv_prep reads the page-locked arrays over PCIe; two compute streams) and
     on the chunked-copy streamed path (MV_SIG_ZEROCOPY=0: two input buffers reused across
     batches, copy chunks gating k_bv_prep chunk by chunk), twice in a row, with bad signatures
     in the first, a middle and the last batch: exact verdicts, the same as pageable inputs."""
-    monkeypatch.setenv("MV_SIG_ZEROCOPY", zerocopy)
     rng = np.random.default_rng(77 + committee)
     n = 5 * 8192 + 77
     with M.Engine(devices=(0,), max_batch=8192) as eng:
+        eng.set_option("MV_SIG_ZEROCOPY", int(zerocopy))
         msg = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
         if committee:
             seeds = rng.integers(0, 256, size=(5, 32), dtype=np.uint8)

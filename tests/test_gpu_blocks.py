@@ -181,7 +181,7 @@ def test_config4_shape_4100_blocks_through_the_batch_path(engine):
 
 
 @pytest.mark.parametrize("split", ["1", "0"])
-def test_comb_split_and_fused_paths_agree(engine, golden, monkeypatch, split):
+def test_comb_split_and_fused_paths_agree(engine, golden, opts, split):
     """Batches under MV_BATCH_MIN take the committee comb verify. Long blocks run it split
     (k_comb_pre -- s < l, R decode, R - [s]B -- on a second stream beside the hash, k_comb_post
     after it); MV_COMB_SPLIT_BYTES=1 forces the split for every block, 0 the fused kernel: the
@@ -192,8 +192,8 @@ def test_comb_split_and_fused_paths_agree(engine, golden, monkeypatch, split):
     import mysticeti_amd as M
     import mysticeti_amd.blocks as MB
 
-    monkeypatch.setenv("MV_COMB_SPLIT_BYTES", split)
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_COMB_SPLIT_BYTES", int(split))
+    opts("MV_ONLINE", 0)
     test_block_edge_cases(engine, golden)
     test_mixed_lengths_and_failures(engine)
     bins = list(MB.config4(engine, rounds=1))[:64]

@@ -98,8 +98,6 @@ def test_short_chain_and_one_lane_comb_kernels_agree(engine):
     k_verify_comb (one lane per signature)
     give identical verdicts on a committee batch with corrupted signatures, undecodable R,
     s >= l and an undecodable key, and both match the oracle."""
-    import os
-
     rng = np.random.default_rng(47)
     na, n = 20, 300
     seeds = rng.integers(0, 256, size=(na, 32), dtype=np.uint8)
@@ -119,12 +117,9 @@ def test_short_chain_and_one_lane_comb_kernels_agree(engine):
     sig[3::13, :32] = 0xFF              # R with y >= p (decodes or not, as ZIP-215 says)
     sig[5::17, 0] ^= 1                  # corrupted R
     out = {}
-    try:
-        for mode in ("0", "1"):
-            os.environ["MV_COMB_QUAD"] = mode
+    for mode in ("0", "1"):
+        with engine.option("MV_COMB_QUAD", int(mode)):
             out[mode] = engine.ed25519_verify(msg, sig, key_idx=ki)
-    finally:
-        os.environ.pop("MV_COMB_QUAD", None)
     assert (out["0"] == out["1"]).all(), np.nonzero(out["0"] != out["1"])[0][:10]
     ref = O.verify_batch(pks[ki], sig, msg)
     assert (out["1"] == ref).all()

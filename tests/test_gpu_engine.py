@@ -62,11 +62,11 @@ def test_logical_shards_match_one_device(engine, shards):
         assert int(st1[i]) == ost, i
 
 
-def test_concurrent_callers_are_coalesced(engine, monkeypatch):
+def test_concurrent_callers_are_coalesced(engine, opts):
     """16 threads each submit 1-4 blocks at a time (the per-peer tasks of net_sync.rs); every
     verdict and digest equals the serial call's, and the queue served the calls in fewer
     device passes than calls (the resident online service is off: every call queues)."""
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_ONLINE", 0)
     bins, pks, stakes = ragged_blocks(n_rounds=40, seed=9)
     engine.set_committee(pks, stakes, 0)
     st_ref, md_ref, bd_ref = engine.verify_blocks(bins)
@@ -136,15 +136,15 @@ def _concurrent(engine, bins, threads=16, rounds=3, kmax=5):
     return got_st, got_md, got_bd
 
 
-def test_online_service_concurrent_callers(engine, monkeypatch):
+def test_online_service_concurrent_callers(engine, opts):
     """The resident online service (k_online): 16 threads posting 1-4 blocks at a time get the
     verdicts and digests of the queue path (MV_ONLINE=0) and of the oracle; the service served
     the short-block calls (the long ones, > 2 KB per block, still queue)."""
     bins, pks, stakes = ragged_blocks(n_rounds=40, seed=13)
     engine.set_committee(pks, stakes, 0)
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_ONLINE", 0)
     st_ref, md_ref, bd_ref = engine.verify_blocks(bins)
-    monkeypatch.delenv("MV_ONLINE")
+    opts("MV_ONLINE", 1)
     o0 = engine.online_stats()
     st, md, bd = _concurrent(engine, bins)
     o1 = engine.online_stats()
@@ -155,7 +155,7 @@ def test_online_service_concurrent_callers(engine, monkeypatch):
         assert int(st[i]) == ost and md[i].tobytes() == omd and bd[i].tobytes() == obd, i
 
 
-def test_online_service_edge_blocks_one_and_64_per_call(engine, golden, monkeypatch):
+def test_online_service_edge_blocks_one_and_64_per_call(engine, golden, opts):
     """Every golden edge-case block through the service one per call and in 64-block calls
     (16 jobs of one request), against the fixture's verdicts and the queue path's digests."""
     fx = golden("block_edge.json")
@@ -165,9 +165,9 @@ def test_online_service_edge_blocks_one_and_64_per_call(engine, golden, monkeypa
     engine.set_committee(pks, stakes, fx["committee"]["epoch"])
     bins = [bytes.fromhex(c["bincode"]) for c in fx["cases"]]
     want = np.array([c["status"] for c in fx["cases"]], dtype=np.uint8)
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_ONLINE", 0)
     _, md_ref, bd_ref = engine.verify_blocks(bins)
-    monkeypatch.delenv("MV_ONLINE")
+    opts("MV_ONLINE", 1)
     o0 = engine.online_stats()[0]
     one = [engine.verify_blocks([b]) for b in bins]
     st1 = np.array([r[0][0] for r in one], dtype=np.uint8)
@@ -181,10 +181,10 @@ def test_online_service_edge_blocks_one_and_64_per_call(engine, golden, monkeypa
     assert engine.online_stats()[0] - o0 >= sum(1 for b in bins if len(b) < 1900)
 
 
-def test_online_service_relaunches_after_idle_exit(engine, monkeypatch):
+def test_online_service_relaunches_after_idle_exit(engine, opts):
     """With a 300-us idle limit the kernel exits between calls 20 ms apart; the next call
     relaunches it and gets the right verdicts."""
-    monkeypatch.setenv("MV_ONLINE_IDLE_US", "300")
+    opts("MV_ONLINE_IDLE_US", 300)
     bins, pks, stakes = ragged_blocks(n_rounds=8, seed=3)
     engine.set_committee(pks, stakes, 0)  # stops a resident kernel (its idle limit was read at launch)
     short = [b for b in bins if len(b) < 1500][:6]
@@ -199,13 +199,13 @@ def test_online_service_relaunches_after_idle_exit(engine, monkeypatch):
     assert engine.online_stats()[1] - l0 >= len(short) - 1
 
 
-def test_online_service_does_not_block_other_streams(engine, monkeypatch):
+def test_online_service_does_not_block_other_streams(engine, opts):
     """The resident kernel sits on a CU-masked stream of its own: while it is live (idle limit
     5 s here), a batch-path signature call and a queue-path block call on the engine's other
     streams complete at once, and the service is still the same launch afterwards."""
     import time
 
-    monkeypatch.setenv("MV_ONLINE_IDLE_US", "5000000")
+    opts("MV_ONLINE_IDLE_US", 5000000)
     bins, pks, stakes = ragged_blocks(n_rounds=8, seed=4)
     engine.set_committee(pks, stakes, 0)
     short = [b for b in bins if len(b) < 1500][:4]
@@ -218,9 +218,9 @@ def test_online_service_does_not_block_other_streams(engine, monkeypatch):
     t0 = time.perf_counter()
     pk, sig = engine.ed25519_sign(seed, msg)
     ss = engine.ed25519_verify(msg, sig, pk)
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_ONLINE", 0)
     st_q, _, _ = engine.verify_blocks(short)
-    monkeypatch.delenv("MV_ONLINE")
+    opts("MV_ONLINE", 1)
     dt = time.perf_counter() - t0
     assert (ss == 0).all() and (st_q == st).all()
     assert dt < 2.0, dt  # not serialised behind the resident kernel's 5-s idle limit
@@ -229,7 +229,7 @@ def test_online_service_does_not_block_other_streams(engine, monkeypatch):
     engine.set_committee(pks, stakes, 0)  # stops the service (no 5-s resident kernel left behind)
 
 
-def test_online_service_size_limits_and_garbage(engine, monkeypatch):
+def test_online_service_size_limits_and_garbage(engine, opts):
     """The service takes calls of <= 64 blocks and <= 128 KB (long blocks included); 65 blocks
     go through the queue (as do long blocks under MV_ONLINE_LONG=0). Truncated, garbage and
     empty-length blocks give the queue path's verdicts (PARSE_ERROR, zero digests) either way."""
@@ -240,9 +240,9 @@ def test_online_service_size_limits_and_garbage(engine, monkeypatch):
     calls = [short[:64], short[:65], short[:1], [bins[0][:10]] + short[:3], [bytes(8)] + short[:2],
              [rng.integers(0, 256, size=300, dtype=np.uint8).tobytes()] + short[5:9],
              [b for b in bins if len(b) > 2500][:3] + short[:1]]
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_ONLINE", 0)
     want = [engine.verify_blocks(c) for c in calls]
-    monkeypatch.delenv("MV_ONLINE")
+    opts("MV_ONLINE", 1)
     for c, w in zip(calls, want):
         o0 = engine.online_stats()[0]
         got = engine.verify_blocks(c)
@@ -255,7 +255,7 @@ def test_online_service_size_limits_and_garbage(engine, monkeypatch):
     assert int(want[3][0][0]) == M.BLOCK_PARSE_ERROR and not want[3][1][0].any()
 
 
-def test_online_service_long_blocks(engine, monkeypatch):
+def test_online_service_long_blocks(engine, opts):
     """Config-4-shaped blocks (~9.5 KB, 66 VoteRanges, a 512-B share) take the service: one per
     call, and 12 in one call (< 128 KB), with a bad signature and a tampered digest among them;
     verdicts and both digests equal the queue path's and the oracle's."""
@@ -274,9 +274,9 @@ def test_online_service_long_blocks(engine, monkeypatch):
     b[30] ^= 1
     bins[7] = bytes(b)
     calls = [bins[:1], bins[3:4], bins[7:8], bins]
-    monkeypatch.setenv("MV_ONLINE", "0")
+    opts("MV_ONLINE", 0)
     want = [engine.verify_blocks(c) for c in calls]
-    monkeypatch.delenv("MV_ONLINE")
+    opts("MV_ONLINE", 1)
     for c, w in zip(calls, want):
         o0 = engine.online_stats()[0]
         got = engine.verify_blocks(c)
@@ -326,3 +326,93 @@ def test_online_service_survives_committee_changes(engine):
     assert not any(x.is_alive() for x in th), "a caller hung"
     assert not errors, errors
     assert engine.online_stats()[1] - l0 >= 3  # relaunched after each stop
+
+
+def test_online_service_launch_failure_fails_over_to_the_queue(opts):
+    """A launch that fails after a request number was taken (fault injection, MV_ONLINE_INJECT)
+    marks the service failed: that call returns MV_E_HIP, no caller hangs on the ring, and every
+    later call -- 8 threads at once included -- is served by the submission queue with the
+    oracle's verdicts (a failed request used to leave the ring stuck)."""
+    bins, pks, stakes = ragged_blocks(n_rounds=6, seed=31)
+    short = [b for b in bins if len(b) < 1200][:16]
+    ref = [O.block_verify(b, pks, stakes, 0)[0] for b in short]
+    with M.Engine(devices=(0,)) as eng:
+        eng.set_committee(pks, stakes, 0)
+        opts("MV_ONLINE_INJECT", 1, eng)
+        with pytest.raises(M.MvError, match="injected"):
+            eng.verify_blocks(short[:1])
+        out = [None] * 8
+
+        def worker(t):
+            out[t] = [int(eng.verify_blocks([short[i]])[0][0]) for i in range(t, len(short), 8)]
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=60)
+        assert not any(x.is_alive() for x in th)
+        for t in range(8):
+            assert out[t] == [ref[i] for i in range(t, len(short), 8)]
+        assert eng.queue_stats()[0] >= len(short)
+
+
+def test_buffer_growth_does_not_wait_for_the_live_service(opts):
+    """While the resident kernel is live (5-s idle limit), calls that grow the engine's scratch
+    -- a larger batch-path verify and a larger queue-path block call than the context has seen
+    -- retire the old buffers instead of freeing them (hipFree drains the whole device, the
+    resident kernel with it) and finish at once."""
+    import time
+
+    bins, pks, stakes = ragged_blocks(n_rounds=8, seed=32)
+    short = [b for b in bins if len(b) < 1500][:4]
+    rng = np.random.default_rng(9)
+    n_small, n_big = M.BATCH_MIN + 7, 4 * M.BATCH_MIN + 11
+    seed = rng.integers(0, 256, size=(n_big, 32), dtype=np.uint8)
+    msg = rng.integers(0, 256, size=(n_big, 32), dtype=np.uint8)
+    with M.Engine(devices=(0,)) as eng:
+        pk, sig = eng.ed25519_sign(seed, msg)
+        eng.set_committee(pks, stakes, 0)
+        opts("MV_ONLINE_IDLE_US", 5000000, eng)
+        # the scratch at its first sizes (before the service is live)
+        assert (eng.ed25519_verify(msg[:n_small], sig[:n_small], pk[:n_small]) == 0).all()
+        with eng.option("MV_ONLINE", 0):
+            eng.verify_blocks(bins[:8])
+        eng.verify_blocks(short)  # the service is live now
+        l0 = eng.online_stats()[1]
+        t0 = time.perf_counter()
+        ss = eng.ed25519_verify(msg, sig, pk)  # grows the batch scratch
+        with eng.option("MV_ONLINE", 0):
+            sb, _, _ = eng.verify_blocks(bins * 3)  # grows the block scratch
+        dt = time.perf_counter() - t0
+        assert (ss == 0).all()
+        big = bins * 3
+        for i in range(0, len(big), 29):
+            assert int(sb[i]) == O.block_verify(big[i], pks, stakes, 0)[0]
+        assert dt < 2.0, dt
+        eng.verify_blocks(short)
+        assert eng.online_stats()[1] == l0  # the same launch served it
+
+
+def test_context_with_online_service_is_destroyed_and_the_process_exits():
+    """The driver's smoke shape in a fresh process: mv_create, one call through the resident
+    service, mv_destroy, interpreter exit -- within a time limit, several times over (round 4's
+    driver smoke stalled after its last call)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "import numpy as np, blocks as B, oracle as O, mysticeti_amd as M\n"
+        "blks = B.gen_config1(O.sign, rounds=2)\n"
+        "pks = np.frombuffer(O.public_key(bytes(32)) * 4, dtype=np.uint8).reshape(4, 32)\n"
+        "with M.Engine(devices=(0,)) as eng:\n"
+        "    eng.set_committee(pks, np.ones(4, dtype=np.uint64), 0)\n"
+        "    st, _, _ = eng.verify_blocks([b.bincode() for b in blks])\n"
+        "    assert (st == 0).all() and eng.online_stats()[0] == 1\n"
+        "print('destroyed', flush=True)\n" % (root, os.path.join(root, "oracle")))
+    for rep in range(3):
+        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=90)
+        assert p.returncode == 0 and "destroyed" in p.stdout, (rep, p.returncode, p.stdout[-500:], p.stderr[-2000:])

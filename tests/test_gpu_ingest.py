@@ -16,14 +16,14 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(params=["in_comb", "two_kernel", "fused", "separate_hash"], autouse=True)
-def ingest_form(request, monkeypatch):
+def ingest_form(request, opts):
     """Every test runs on the four device ingest forms: on small calls the parse and the
     digests inside k_verify_comb16 (the default), k_block_ingest + the digests inside
     k_verify_comb16 (MV_INGEST_IN_COMB=0), the fused k_block_ingest_hash (ingest_hash.hip,
     MV_BLK_FUSED=1), and k_block_ingest + a separate k_b2_quad launch (MV_HASH_IN_COMB=0)."""
-    monkeypatch.setenv("MV_BLK_FUSED", "1" if request.param == "fused" else "0")
-    monkeypatch.setenv("MV_HASH_IN_COMB", "0" if request.param == "separate_hash" else "1")
-    monkeypatch.setenv("MV_INGEST_IN_COMB", "0" if request.param == "two_kernel" else "1")
+    opts("MV_BLK_FUSED", request.param == "fused")
+    opts("MV_HASH_IN_COMB", request.param != "separate_hash")
+    opts("MV_INGEST_IN_COMB", request.param != "two_kernel")
     return request.param
 
 

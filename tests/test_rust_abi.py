@@ -39,6 +39,7 @@ C2RUST = {
     "uint32_t": "u32",
     "uint64_t": "u64",
     "int64_t": "i64",
+    "int64_t*": "*mut i64",
     "int": "i32",
     "mv_status": "i32",
 }

@@ -75,7 +75,9 @@ for T in "$@"; do
       run 900 "$OUT/pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${K[@]}"
       tail -1 "$OUT/pytest_gpu.log" ;;
     smoke)
-      MV_ONLINE_DEBUG=1 run 150 "$OUT/smoke.log" python -u -c "import __graft_entry__ as g; g.smoke()"
+      # exactly the driver's command: no -u, no debug environment (a stall then shows as it
+      # would to the driver; tools/smoke_driver.sh adds a stack-dumping watchdog)
+      run 150 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')"
       tail -1 "$OUT/smoke.log" ;;
     bench)
       timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench$SUF.json" 2> "$OUT/bench$SUF.err" || { echo "bench FAILED"; tail -8 "$OUT/bench$SUF.err"; exit 1; }
