@@ -173,6 +173,9 @@ def main():
                     help="default line's config-5 leg: 64-block calls timed per shape")
     ap.add_argument("--config5-seconds", type=float, default=2.0,
                     help="default line's config-5 leg: seconds of concurrent 1-block callers per shape")
+    ap.add_argument("--fanin-callers", type=int, default=99,
+                    help="config 5: the fan-in leg's concurrent 1-block callers (committee - 1 of config 4's "
+                         "100-validator committee; 0 disables)")
     ap.add_argument("--no-wal", dest="wal", action="store_false",
                     help="skip the WAL replay-check rate (row f4) in the default line")
     ap.add_argument("--wal-entries", type=int, default=1 << 20, help="WAL entries (config-4 blocks) per GPU")
@@ -459,7 +462,7 @@ def main():
 
         eng.set_batch_groups(args.groups)
         cfg5 = bench_blocks.config5_measure(eng, batches=args.config5_batches, conc_seconds=args.config5_seconds,
-                                            cpu=args.cpu_sample > 0)
+                                            cpu=args.cpu_sample > 0, fanin_callers=args.fanin_callers)
         ok = ok and cfg5["correct"]
 
     rss_mark("config5")

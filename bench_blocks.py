@@ -175,14 +175,17 @@ def _drive(drv, kind, fn, ctx, packed, per_call, callers, inner_threads=1, secon
     return r, bool(calls) and bad.value == 0 and err.value == 0
 
 
-def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None) -> dict:
+def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None, fanin_callers=99) -> dict:
     """Config 5 on this rank's GPU: for config-1 and config-4 shaped blocks,
       - 64-block calls of mv_verify_blocks one after another (host buffers, PCIe both ways):
         p50/p99 over `batches` calls, beside the oracle's StatementBlock::verify of the same
         64 blocks on one host core (the reference's sequential loop) and on the CPU share;
       - `callers` concurrent 1-block callers for `conc_seconds` (one tokio task per peer,
         net_sync.rs:214-221, 314-386): the GPU queue merges them; the CPU leg verifies each
-        block on the caller's own core (no pool).
+        block on the caller's own core (no pool);
+      - the same with `fanin_callers` callers (default 99 = committee - 1 of config 4's
+        100-validator committee: process_blocks runs one task per peer, net_sync.rs:214-221,
+        committee.rs:56-57); the CPU leg then runs 99 threads on the box's CPU share.
     Every caller is a pthread of bench_native/concurrent.c, so Python caps neither side."""
     import mysticeti_amd.blocks as MB
 
@@ -222,24 +225,29 @@ def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None
             ok &= c1 and c2
             res["cpu_p50_over_gpu_p50"] = {k: round(res[k]["p50_us"] / res["gpu"]["p50_us"], 3)
                                            for k in ("cpu_1t", f"cpu_{threads}t")}
-        # concurrent 1-block callers
-        conc = {"callers": callers, "seconds": conc_seconds}
-        q0, o0 = eng.queue_stats(), eng.online_stats()
-        conc["gpu"], g = _drive(drv, 0, mv_fn, eng.ctx, packed, 1, callers, seconds=conc_seconds)
-        q1, o1 = eng.queue_stats(), eng.online_stats()
-        conc["gpu"]["queue_calls"] = q1[0] - q0[0]
-        if q1[1] > q0[1]:
-            conc["gpu"]["calls_per_device_pass"] = round((q1[0] - q0[0]) / (q1[1] - q0[1]), 2)
-        conc["gpu"]["online_requests"], conc["gpu"]["online_launches"] = o1[0] - o0[0], o1[1] - o0[1]
-        ok &= g
+        # concurrent 1-block callers: the CPU share's thread count, then the reference's fan-in
+        legs = [("concurrent_1_block_callers", callers)]
+        if fanin_callers and fanin_callers != callers:
+            legs.append(("fan_in_callers", fanin_callers))
+        for key, nc in legs:
+            conc = {"callers": nc, "seconds": conc_seconds}
+            q0, o0 = eng.queue_stats(), eng.online_stats()
+            conc["gpu"], g = _drive(drv, 0, mv_fn, eng.ctx, packed, 1, nc, seconds=conc_seconds)
+            q1, o1 = eng.queue_stats(), eng.online_stats()
+            conc["gpu"]["queue_calls"] = q1[0] - q0[0]
+            if q1[1] > q0[1]:
+                conc["gpu"]["calls_per_device_pass"] = round((q1[0] - q0[0]) / (q1[1] - q0[1]), 2)
+            conc["gpu"]["online_requests"], conc["gpu"]["online_launches"] = o1[0] - o0[0], o1[1] - o0[1]
+            ok &= g
+            if comm is not None:
+                conc["cpu_own_core"], c = _drive(drv, 1, comm.fn, comm.ptr, packed, 1, nc, inner_threads=1,
+                                                 seconds=conc_seconds)
+                ok &= c
+                conc["gpu_over_cpu_blocks_per_s"] = round(
+                    conc["gpu"]["blocks_per_s"] / conc["cpu_own_core"]["blocks_per_s"], 3)
+            res[key] = conc
         if comm is not None:
-            conc["cpu_own_core"], c = _drive(drv, 1, comm.fn, comm.ptr, packed, 1, callers, inner_threads=1,
-                                             seconds=conc_seconds)
-            ok &= c
-            conc["gpu_over_cpu_blocks_per_s"] = round(conc["gpu"]["blocks_per_s"] / conc["cpu_own_core"]["blocks_per_s"],
-                                                      3)
             comm.close()
-        res["concurrent_1_block_callers"] = conc
         out["shapes"][shape] = res
     out["correct"] = bool(ok)
     out["note"] = ("GPU: mv_verify_blocks on host buffers (raw bincode in, verdicts out; 64 blocks < MV_BATCH_MIN "
@@ -251,7 +259,8 @@ def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None
 
 
 def config5(args, eng, rank) -> int:
-    res = config5_measure(eng, batches=args.batches, conc_seconds=args.conc_seconds, cpu=args.cpu_sample > 0)
+    res = config5_measure(eng, batches=args.batches, conc_seconds=args.conc_seconds, cpu=args.cpu_sample > 0,
+                          fanin_callers=args.fanin_callers)
     out = {"metric": "config5: 64-block batch verify latency, submit -> verdicts (mv_verify_blocks, host buffers)",
            "higher_is_better": False, "n_gpus": 1, "data": "synthetic (blocks signed on the GPU)"}
     out.update(res)

@@ -333,7 +333,7 @@ def test_online_service_launch_failure_fails_over_to_the_queue(opts):
     marks the service failed: that call returns MV_E_HIP, no caller hangs on the ring, and every
     later call -- 8 threads at once included -- is served by the submission queue with the
     oracle's verdicts (a failed request used to leave the ring stuck)."""
-    bins, pks, stakes = ragged_blocks(n_rounds=6, seed=31)
+    bins, pks, stakes = ragged_blocks(n_rounds=8, seed=31)
     short = [b for b in bins if len(b) < 1200][:16]
     ref = [O.block_verify(b, pks, stakes, 0)[0] for b in short]
     with M.Engine(devices=(0,)) as eng:

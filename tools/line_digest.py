@@ -27,6 +27,10 @@ if c5:
         c = v["concurrent_1_block_callers"]
         out.append(f"c5 {k} p50={v['gpu']['p50_us']} p99={v['gpu']['p99_us']} conc={c['gpu']['blocks_per_s']} "
                    f"p50c={c['gpu']['p50_us']} cpp={c['gpu'].get('calls_per_device_pass')} onl={c['gpu'].get('online_requests')}/{c['gpu'].get('online_launches')} cpu={c.get('cpu_own_core', {}).get('blocks_per_s')}")
+        f = v.get("fan_in_callers")
+        if f:
+            out.append(f"fanin{f['callers']} {k} gpu={f['gpu']['blocks_per_s']} p50={f['gpu']['p50_us']} "
+                       f"p99={f['gpu']['p99_us']} cpu={f.get('cpu_own_core', {}).get('blocks_per_s')}")
 w = d.get("wal") or (d if "WAL" in d.get("metric", "") else None)
 if w:
     out.append(f"wal {w['value']} GB/s stages={w.get('stage_ms')}")
