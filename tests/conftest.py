@@ -54,7 +54,8 @@ def opts(engine):
 
     yield set_opt
     for eng, name, old in reversed(saved):
-        eng.set_option(name, old)
+        if eng.ctx:  # (an engine the test made and closed itself needs no restoring)
+            eng.set_option(name, old)
 
 
 @pytest.fixture(scope="session")
