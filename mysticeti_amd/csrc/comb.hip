@@ -584,17 +584,19 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // The resident online service (kernels.h OnlineArgs). Every branch around a barrier is
 // uniform (the role is the workgroup's, decisions are broadcast through LDS), and every wait
 // loop also tests the launch's end, so all waves leave.
-constexpr uint32_t ON_BATCH = 32;  // requests the poller moves per pass
+constexpr uint32_t ON_BATCH = 64;  // the poller's window (requests it can move per pass): the whole ring
 constexpr uint32_t ON_COPY_UNROLL = 8;  // 16-B input loads per poller thread in flight
 static_assert(IG_WIN == mvk::INGEST_WINDOW_BYTES, "the host's eligibility test uses the ingest window");
+static_assert(ON_BATCH == mvk::ONLINE_SLOTS && ON_BATCH <= 64, "the window's lanes cover distinct slots, one wave");
 
 // Workgroup 0: moves published requests from page-locked memory into HBM, appends their jobs.
 MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   mvk::OnlineCtl* ctl = A.ctl;
   mvk::OnlineDev* dev = A.dev;
-  __shared__ uint32_t sh[4];              // kind (0 idle, 1 move, 2 exit), first request lo / hi, count
+  __shared__ uint32_t sh[5];              // kind (0 idle, 1 move, 2 exit), ready lo / hi, count, advance
   __shared__ uint32_t pre[ON_BATCH + 1];  // 16-B chunk prefix over the batch's inputs
   __shared__ uint32_t nblk[ON_BATCH];
+  __shared__ uint32_t qoff[ON_BATCH];     // request - ready of each moved request
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
   uint64_t t_busy = t_start;
@@ -606,37 +608,47 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
     __hip_atomic_store(&dev->epoch, A.launch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (;;) {
-    if (t < 64) {  // wave 0: how many consecutive requests from `ready` are published
-      uint32_t kind = 0, cnt = 0;
-      // polls are relaxed (an acquire invalidates the caches every time: the working
-      // workgroups' comb tables with them); one acquire fence once requests are seen
-      // the next ON_BATCH slots' seq words are read together (one PCIe round trip): a request is
-      // published once its seq holds its number + 1, which the host writes after its bytes
+    if (t < 64) {
+      // wave 0: every published request of the window [ready, ready + ON_BATCH), in any order:
+      // a caller that publishes late (descheduled between reserving its number and writing
+      // its seq) does not hold back the requests behind it (round 4 moved only the
+      // consecutive prefix, and 99 concurrent callers stalled behind one). `moved[slot]`
+      // (request + 1, poller-only) marks the ones already moved; `ready` advances over the
+      // moved prefix. The window is the whole ring: the slots of its lanes are distinct.
+      // Polls are relaxed (an acquire invalidates the caches every time: the working
+      // workgroups' comb tables with them); one acquire fence once requests are seen. The
+      // window's seq words are read together (one PCIe round trip): a request is published
+      // once its seq holds its number + 1, which the host writes after its bytes.
+      uint32_t kind = 0;
       const uint64_t rdy = __hip_atomic_load(&dev->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t m = ON_BATCH;
-      bool ok = false;
+      bool fresh = false, moved = false;
       uint32_t nb = 0, cb = 0;
-      if (t < m) {
-        const uint64_t q = rdy + t;
-        const mvk::OnlineReq* r = A.reqs + (q % mvk::ONLINE_SLOTS);
-        ok = __hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
-        if (ok) {
+      const uint64_t q = rdy + t;
+      const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
+      if (t < ON_BATCH) {
+        moved = __hip_atomic_load(&dev->moved[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q + 1;
+        const mvk::OnlineReq* r = A.reqs + slot;
+        fresh = !moved && __hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q + 1;
+        if (fresh) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the slot's bytes after seq
           nb = r->n;
           cb = r->copy_bytes;
         }
       }
-      const uint64_t notok = __ballot(!ok);  // lanes >= m count as not ready
-      cnt = notok ? (uint32_t)__builtin_ctzll(notok) : 64u;
-      if (cnt > m) cnt = (uint32_t)m;
+      const uint64_t fm = __ballot(fresh);
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(fm);
+      // the moved prefix after this pass (lanes past the window count as not moved)
+      const uint64_t notdone = __ballot(!(fresh || moved) || t >= ON_BATCH);
+      const uint32_t adv = notdone ? (uint32_t)__builtin_ctzll(notdone) : 64u;
       const uint64_t now = on_now();
-      if (t < cnt) {
-        nblk[t] = nb;
-        pre[t] = (cb + 15) / 16;  // chunk count, prefixed below
-        __hip_atomic_store(&ctl->trace[(rdy + t) % mvk::ONLINE_SLOTS][0], now, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (fresh) {
+        const uint32_t i = (uint32_t)__builtin_popcountll(fm & ((1ull << t) - 1));  // rank among the fresh
+        qoff[i] = t;
+        nblk[i] = nb;
+        pre[i] = (cb + 15) / 16;  // chunk count, prefixed below
+        __hip_atomic_store(&ctl->trace[slot][0], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      if (cnt) {
+      if (cnt || adv) {
         kind = 1;
         t_busy = now;
       } else if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
@@ -654,10 +666,11 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
         sh[1] = (uint32_t)rdy;
         sh[2] = (uint32_t)(rdy >> 32);
         sh[3] = cnt;
+        sh[4] = adv;
       }
     }
     __syncthreads();
-    const uint32_t kind = sh[0], cnt = sh[3];
+    const uint32_t kind = sh[0], cnt = sh[3], adv = sh[4];
     const uint64_t rdy = (uint64_t)sh[1] | ((uint64_t)sh[2] << 32);
     if (kind == 2) {
       if (t == 0) {
@@ -700,7 +713,7 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       if (t < total) {
         uint32_t i = 0;
         while (pre[i + 1] <= t) i++;
-        const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS), c = t - pre[i];
+        const uint32_t slot = (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS), c = t - pre[i];
         reinterpret_cast<uint4*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot)[c] =
             reinterpret_cast<const uint4*>(A.in_host + mvk::ONLINE_IN_STRIDE * slot)[c];
       }
@@ -713,7 +726,7 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
         const uint32_t k = live ? kk : 0u;
         uint32_t i = 0;
         while (pre[i + 1] <= k) i++;
-        const uint32_t slot = (uint32_t)((rdy + i) % mvk::ONLINE_SLOTS), c = k - pre[i];
+        const uint32_t slot = (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS), c = k - pre[i];
         const uint64_t sink = (uint64_t)(dev->sink + 2 * t);
         src[u] = live ? (uint64_t)(A.in_host + mvk::ONLINE_IN_STRIDE * slot + 16 * (size_t)c) : sink;
         dst[u] = live ? (uint64_t)(A.scr + mvk::ONLINE_SCR_STRIDE * slot + 16 * (size_t)c) : sink;
@@ -733,20 +746,21 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
     if (t == 0) {
       unsigned long long jt = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (uint32_t i = 0; i < cnt; i++) {
-        const uint64_t q = rdy + i;
+        const uint64_t q = rdy + qoff[i];
         const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS), nj = (nblk[i] + C16_SIGS - 1) / C16_SIGS;
         dev->n[slot] = nblk[i];
+        __hip_atomic_store(&dev->moved[slot], (unsigned long long)(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (nj == 0)  // a void request: complete it here
           __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         for (uint32_t j = 0; j < nj; j++, jt++) dev->jobs[jt % mvk::ONLINE_JOBS] = ((unsigned long long)q << 8) | j;
       }
-      __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + adv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&dev->jobs_tail, jt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t < cnt)
-      __hip_atomic_store(&ctl->trace[(rdy + t) % mvk::ONLINE_SLOTS][1], on_now(), __ATOMIC_RELAXED,
+      __hip_atomic_store(&ctl->trace[(rdy + qoff[t]) % mvk::ONLINE_SLOTS][1], on_now(), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();  // pre[] / nblk[] / sh[] are rewritten by the next pass
+    __syncthreads();  // pre[] / nblk[] / qoff[] / sh[] are rewritten by the next pass
   }
 }
 

@@ -7,9 +7,14 @@
 // thread (one stream per device, no collective: only per-item verdicts come back), in
 // chunks of at most cfg.max_batch items. Calls on one ctx are serialised by a mutex.
 #include <hip/hip_runtime.h>
+#include <limits.h>
+#include <linux/futex.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1030,6 +1035,19 @@ struct OnlineSvc {
   void *ctl_d = nullptr, *req_d = nullptr, *in_d = nullptr, *out_d = nullptr;  // device views
   DevBuf dctl, scr;
   std::unique_ptr<std::atomic<uint64_t>[]> freed;  // slot released by its owner: request + 1
+  // Waiting callers (round 5). At most max_spinners callers spin on their done word; the others
+  // sleep on a futex word of their slot, which the reaper thread sets and wakes once the done
+  // word holds their request (99 callers spinning on a 16-CPU share descheduled one another
+  // for milliseconds: p99 81 ms). A caller waiting for its slot to be freed sleeps the same way.
+  int max_spinners = 12;
+  std::atomic<int> spinners{0}, sleepers{0};
+  std::unique_ptr<std::atomic<uint32_t>[]> dwake;  // per slot: set by the reaper (futex word)
+  std::unique_ptr<std::atomic<uint64_t>[]> sleep_q;  // per slot: request + 1 its sleeper waits for, 0: none
+  std::unique_ptr<std::atomic<uint32_t>[]> fseq, fwait;  // per slot: frees so far (futex word), sleepers on it
+  std::thread reaper;
+  std::mutex rmu;
+  std::condition_variable rcv;
+  bool rstop = false;
   uint64_t next_q = 0;
   uint32_t grid = 0, launch_no = 0;
   std::atomic<uint64_t> requests{0}, launches{0};
@@ -1069,6 +1087,57 @@ bool online_eligible(mv_ctx* ctx, uint32_t n, uint64_t bytes, uint64_t longest) 
   return mvk::comb_short_chain(kn, n);
 }
 
+void futex_wait_for(std::atomic<uint32_t>& w, uint32_t v, int64_t ns) {
+  static_assert(sizeof(std::atomic<uint32_t>) == 4, "futex word");
+  timespec ts{(time_t)(ns / 1000000000), (long)(ns % 1000000000)};
+  (void)syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAIT_PRIVATE, v, &ts, nullptr, 0);
+}
+void futex_wake_all(std::atomic<uint32_t>& w) {
+  (void)syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+}
+
+// CPUs this process may use: its affinity mask, capped by a cgroup-v2 CPU quota.
+int host_cpu_share() {
+  cpu_set_t set;
+  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long period = 0;
+    if (fscanf(f, "%31s %ld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+      const long q = atol(quota);
+      if (q > 0) n = std::min<int>(n, (int)std::max<long>(1, q / period));
+    }
+    fclose(f);
+  }
+  return std::max(1, n);
+}
+
+// Wakes the sleeping callers whose done word is set (one thread per service, started with it;
+// it polls only while callers sleep and otherwise waits on rcv).
+void online_reaper(OnlineSvc* op) {
+  OnlineSvc& o = *op;
+  std::unique_lock<std::mutex> lk(o.rmu);
+  while (!o.rstop) {
+    if (o.sleepers.load(std::memory_order_acquire) == 0) {
+      o.rcv.wait_for(lk, std::chrono::milliseconds(20));
+      continue;
+    }
+    lk.unlock();
+    for (int it = 0; it < 4096 && o.sleepers.load(std::memory_order_relaxed) > 0; it++) {
+      for (uint32_t k = 0; k < kOnSlots; k++) {
+        uint64_t w = o.sleep_q[k].load(std::memory_order_acquire);
+        if (w && __atomic_load_n(&o.ctl->done[k], __ATOMIC_ACQUIRE) == w &&
+            o.sleep_q[k].compare_exchange_strong(w, 0, std::memory_order_acq_rel)) {
+          o.dwake[k].store(1, std::memory_order_release);
+          futex_wake_all(o.dwake[k]);
+        }
+      }
+      __builtin_ia32_pause();
+    }
+    lk.lock();
+  }
+}
+
 // Allocations and the stream (o.mu held).
 mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   if (o.ready) return MV_OK;
@@ -1088,7 +1157,23 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   HIPCHK(ctx, hipMemset(o.dctl.p, 0, sizeof(mvk::OnlineDev)));
   HIPCHK(ctx, o.scr.ensure(mvk::ONLINE_SCR_STRIDE * kOnSlots));
   o.freed.reset(new std::atomic<uint64_t>[kOnSlots]);
-  for (uint32_t k = 0; k < kOnSlots; k++) o.freed[k].store(0);
+  o.dwake.reset(new std::atomic<uint32_t>[kOnSlots]);
+  o.sleep_q.reset(new std::atomic<uint64_t>[kOnSlots]);
+  o.fseq.reset(new std::atomic<uint32_t>[kOnSlots]);
+  o.fwait.reset(new std::atomic<uint32_t>[kOnSlots]);
+  for (uint32_t k = 0; k < kOnSlots; k++) {
+    o.freed[k].store(0);
+    o.dwake[k].store(0);
+    o.sleep_q[k].store(0);
+    o.fseq[k].store(0);
+    o.fwait[k].store(0);
+  }
+  o.max_spinners = ctx->kn.online_spinners > 0 ? (int)ctx->kn.online_spinners
+                                               : std::max(1, host_cpu_share() * 3 / 4);
+  if (!o.reaper.joinable()) {
+    o.rstop = false;
+    o.reaper = std::thread(online_reaper, &o);
+  }
   // CU mask: MV_ONLINE_CUS (default 64) CUs spread evenly over the chip; 0 = an ordinary stream
   int cus = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev.id));
@@ -1247,6 +1332,14 @@ bool online_stop(OnlineSvc& o) {
 }
 
 void online_release(OnlineSvc& o) {
+  if (o.reaper.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(o.rmu);
+      o.rstop = true;
+    }
+    o.rcv.notify_all();
+    o.reaper.join();
+  }
   if (!online_stop(o)) return;  // stuck: leave its stream and memory alone
   if (o.trace && o.tr_n) {
     const double n = (double)o.tr_n;
@@ -1297,13 +1390,21 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
   const uint32_t slot = (uint32_t)(q % kOnSlots);
   if (q >= kOnSlots) {  // the slot's previous request must have been read out by its owner
     const auto t0 = std::chrono::steady_clock::now();
-    while (o.freed[slot].load(std::memory_order_acquire) != q - kOnSlots + 1) {
+    for (uint32_t spins = 0; o.freed[slot].load(std::memory_order_acquire) != q - kOnSlots + 1; spins++) {
       // the owner of request q - 64 failed (its service failed with it) or never returns
       if (o.failed.load(std::memory_order_relaxed) || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
         o.failed = true;
         return set_err(ctx, MV_E_HIP, "online service failed: ring slot never released");
       }
-      std::this_thread::yield();
+      if (spins < 256) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      // sleep until the owner frees the slot (it wakes fseq's sleepers), 1 ms at most
+      const uint32_t seen = o.fseq[slot].load(std::memory_order_acquire);
+      o.fwait[slot].fetch_add(1, std::memory_order_acq_rel);
+      if (o.freed[slot].load(std::memory_order_acquire) != q - kOnSlots + 1) futex_wait_for(o.fseq[slot], seen, 1000000);
+      o.fwait[slot].fetch_sub(1, std::memory_order_acq_rel);
     }
   }
   // the slot's input: off[n] | len[n] | bincode (8-aligned blocks) | 16 zero bytes; the poller
@@ -1330,24 +1431,16 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
   r.copy_bytes = copy_bytes;
   const int64_t t_pub = o.trace ? steady_ns() : 0;
   __atomic_store_n(&r.seq, q + 1, __ATOMIC_RELEASE);  // the descriptor and the bytes above first
-  // wait for the slot's done word; every ~100 us check that a kernel is still live (one that
-  // exited idle just before this request was published is relaunched)
+  // wait for the slot's done word, spinning (at most max_spinners callers at once) or asleep
+  // until the reaper wakes it; every ~100 us (asleep: 1 ms) check that a kernel is still live
+  // (one that exited idle just before this request was published is relaunched)
   auto t_last = std::chrono::steady_clock::now();
   const auto t_start = t_last;
-  uint32_t spins = 0;
   mv_status rc = MV_OK;
-  while (__atomic_load_n(&o.ctl->done[slot], __ATOMIC_ACQUIRE) != q + 1) {
-    if (++spins < 64) {
-      __builtin_ia32_pause();
-      continue;
-    }
-    spins = 0;
-    std::this_thread::yield();
-    const auto now = std::chrono::steady_clock::now();
-    if (now - t_last < std::chrono::microseconds(100)) continue;
-    t_last = now;
+  auto is_done = [&] { return __atomic_load_n(&o.ctl->done[slot], __ATOMIC_ACQUIRE) == q + 1; };
+  auto check = [&](std::chrono::steady_clock::time_point now) -> bool {  // false: give up (rc set)
     if (o.debug && now - t_start > std::chrono::milliseconds(500) &&
-        (now - t_start) % std::chrono::milliseconds(500) < std::chrono::microseconds(150)) {
+        (now - t_start) % std::chrono::milliseconds(500) < std::chrono::milliseconds(2)) {
       const uint64_t* tr = o.ctl->trace[slot];
       fprintf(stderr, "[online] q %llu slot %u waiting %.1f ms: done %llu seq %llu tail %llu trace %llu %llu %llu %llu\n",
               (unsigned long long)q, slot,
@@ -1359,15 +1452,50 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     std::lock_guard<std::mutex> lk(o.mu);
     if (o.failed) {
       rc = set_err(ctx, MV_E_HIP, "online service failed");
-      break;
+      return false;
     }
     rc = online_ensure_running(ctx, dev, o);
     if (rc == MV_OK && now - t_start > std::chrono::seconds(20))
       rc = set_err(ctx, MV_E_HIP, "online service: request timed out");
     if (rc != MV_OK) {
       o.failed = true;  // the slot may still be written: never reuse the service
-      break;
+      return false;
     }
+    return true;
+  };
+  if (o.spinners.fetch_add(1, std::memory_order_acq_rel) < o.max_spinners) {
+    for (uint32_t spins = 0; !is_done();) {
+      if (++spins < 64) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      spins = 0;
+      std::this_thread::yield();
+      const auto now = std::chrono::steady_clock::now();
+      if (now - t_last < std::chrono::microseconds(100)) continue;
+      t_last = now;
+      if (!check(now)) break;
+    }
+    o.spinners.fetch_sub(1, std::memory_order_acq_rel);
+  } else {
+    o.spinners.fetch_sub(1, std::memory_order_acq_rel);
+    o.dwake[slot].store(0, std::memory_order_relaxed);
+    o.sleep_q[slot].store(q + 1, std::memory_order_release);
+    if (o.sleepers.fetch_add(1, std::memory_order_acq_rel) == 0) {
+      std::lock_guard<std::mutex> lk(o.rmu);
+      o.rcv.notify_one();
+    }
+    while (!is_done()) {
+      futex_wait_for(o.dwake[slot], 0, 1000000);
+      if (is_done()) break;
+      const auto now = std::chrono::steady_clock::now();
+      if (now - t_last < std::chrono::microseconds(900)) continue;
+      t_last = now;
+      if (!check(now)) break;
+    }
+    uint64_t w = q + 1;
+    o.sleep_q[slot].compare_exchange_strong(w, 0, std::memory_order_acq_rel);
+    o.sleepers.fetch_sub(1, std::memory_order_acq_rel);
   }
   if (rc != MV_OK) return rc;
   if (o.trace) {
@@ -1390,6 +1518,8 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
     if (bd) memcpy(bd + 32 * (size_t)k, ho + 32 * ((size_t)kOnMax + k), 32);
   }
   o.freed[slot].store(q + 1, std::memory_order_release);
+  o.fseq[slot].fetch_add(1, std::memory_order_acq_rel);
+  if (o.fwait[slot].load(std::memory_order_acquire)) futex_wake_all(o.fseq[slot]);
   return MV_OK;
 }
 
@@ -1802,6 +1932,7 @@ const KnobDef kKnobs[] = {
     {"MV_ONLINE_TRACE", &mvk::Knobs::online_trace, K_FLAG, false},
     {"MV_ONLINE_DEBUG", &mvk::Knobs::online_debug, K_FLAG, false},
     {"MV_ONLINE_INJECT", &mvk::Knobs::online_inject, K_OFF, false},
+    {"MV_ONLINE_SPINNERS", &mvk::Knobs::online_spinners, K_INT, false},
     {"MV_PIPELINE", &mvk::Knobs::pipeline, K_INT, false},
     {"MV_PIPE_CHUNK_LOG2", &mvk::Knobs::pipe_chunk_log2, K_INT, false},
     {"MV_PIPE_THREADS", &mvk::Knobs::pipe_threads, K_INT, false},

@@ -35,6 +35,7 @@ struct Knobs {
   int64_t online_trace = 0;              // MV_ONLINE_TRACE: per-stage means on stderr at release
   int64_t online_debug = 0;              // MV_ONLINE_DEBUG: launch lines, long waits on stderr
   int64_t online_inject = 0;             // MV_ONLINE_INJECT: fault injection (tests): launches fail
+  int64_t online_spinners = 0;           // MV_ONLINE_SPINNERS: callers spinning on their verdict (0: 3/4 of the CPU share)
   // signature path
   int64_t pipeline = 0;                  // MV_PIPELINE: pageable signature staging experiment
   int64_t pipe_chunk_log2 = 18;          // MV_PIPE_CHUNK_LOG2
@@ -230,6 +231,7 @@ struct OnlineDev {
   uint32_t quit, epoch;          // quit: workers leave; epoch: the launch whose poller is set up
   uint32_t n[ONLINE_SLOTS];
   uint32_t jobs_done[ONLINE_SLOTS];
+  unsigned long long moved[ONLINE_SLOTS];  // request + 1 last moved from each slot (the poller's)
   unsigned long long jobs[ONLINE_JOBS];  // (request << 8) | job
   uint64_t sink[2 * 1024];               // 16 B per poller thread: where its copy lanes past the end go
 };
