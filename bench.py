@@ -173,6 +173,8 @@ def main():
                     help="default line's config-5 leg: 64-block calls timed per shape")
     ap.add_argument("--config5-seconds", type=float, default=2.0,
                     help="default line's config-5 leg: seconds of concurrent 1-block callers per shape")
+    ap.add_argument("--conc-callers", type=int, default=0,
+                    help="config 5: the concurrent-callers leg's callers (0: the CPU share's thread count)")
     ap.add_argument("--fanin-callers", type=int, default=99,
                     help="config 5: the fan-in leg's concurrent 1-block callers (committee - 1 of config 4's "
                          "100-validator committee; 0 disables)")
@@ -462,7 +464,8 @@ def main():
 
         eng.set_batch_groups(args.groups)
         cfg5 = bench_blocks.config5_measure(eng, batches=args.config5_batches, conc_seconds=args.config5_seconds,
-                                            cpu=args.cpu_sample > 0, fanin_callers=args.fanin_callers)
+                                            cpu=args.cpu_sample > 0, fanin_callers=args.fanin_callers,
+                                            callers=args.conc_callers or None)
         ok = ok and cfg5["correct"]
 
     rss_mark("config5")

@@ -260,7 +260,7 @@ def config5_measure(eng, batches=10000, conc_seconds=3.0, cpu=True, callers=None
 
 def config5(args, eng, rank) -> int:
     res = config5_measure(eng, batches=args.batches, conc_seconds=args.conc_seconds, cpu=args.cpu_sample > 0,
-                          fanin_callers=args.fanin_callers)
+                          fanin_callers=args.fanin_callers, callers=args.conc_callers or None)
     out = {"metric": "config5: 64-block batch verify latency, submit -> verdicts (mv_verify_blocks, host buffers)",
            "higher_is_better": False, "n_gpus": 1, "data": "synthetic (blocks signed on the GPU)"}
     out.update(res)
