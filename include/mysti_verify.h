@@ -161,7 +161,7 @@ mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes);
  * calls averaging < MV_COMB_SPLIT_BYTES per block), are posted to a ring in page-locked memory
  * that a kernel resident on a CU-masked stream polls; the caller's thread spins on its
  * request's done word (no launch, no event, no wake-up per call). The kernel exits after
- * MV_ONLINE_IDLE_US (default 2,000) without work and is relaunched by the next call; calls it
+ * MV_ONLINE_IDLE_US (default 10,000) without work and is relaunched by the next call; calls it
  * does not take (more blocks or bytes, a block past the window, MV_FLAG_NO_ONLINE, MV_ONLINE=0)
  * go through the submission queue, and so does every call after the service has failed.
  * Verdicts and digests are those of the queue path. Counters: requests served by the service

@@ -428,10 +428,12 @@ __global__ void __launch_bounds__(256) k_part_top(const uint32_t* __restrict__ p
   }
   if (threadIdx.x == 0) pstart[total] = all;
 }
+// (scal, n: the signatures [base, base + n) of a batch of nall; point refs are batch-wide)
 __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __restrict__ scal, uint32_t n,
                                                              const uint32_t* __restrict__ poff,
                                                              const uint32_t* __restrict__ pstart, BvGroups G,
-                                                             uint32_t skipA, unsigned long long* __restrict__ tmp) {
+                                                             uint32_t skipA, uint32_t nall, uint32_t base,
+                                                             unsigned long long* __restrict__ tmp) {
   __shared__ uint32_t rank[BV_NPG];
   for (int i = threadIdx.x; i < BV_NPG; i += PART_CHUNK) rank[i] = 0;
   __syncthreads();
@@ -450,7 +452,7 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __rest
       const uint32_t key = bv_key(w, d);
       const uint32_t p = key >> BV_FINE_BITS;
       const uint32_t r = atomicAdd(&rank[p], 1u);
-      const uint32_t pt = isA ? n + gid : gid;
+      const uint32_t pt = isA ? nall + base + gid : base + gid;
       tmp[ps[p] + po[p] + r] = ((unsigned long long)(g * BV_NKG + key) << 32) | (pt << 1) | (d < 0 ? 1u : 0u);
     });
   }
@@ -519,9 +521,11 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort(const unsigned long long*
 #ifndef MV_BUCKET_OCC
 #define MV_BUCKET_OCC 3
 #endif
+// acc (streaming MSM, seg = 1): the bucket sums continue from segT (the earlier chunks')
 __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ ents, uint32_t ngroups, uint32_t seg,
-                                                   uint32_t nw, uint4* __restrict__ segV, uint4* __restrict__ segT) {
+                                                   uint32_t nw, uint32_t acc, uint4* __restrict__ segV,
+                                                   uint4* segT) {
   const uint32_t nsw = BV_NB / seg;  // segments per (group, window) row
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
   if (lin >= ngroups * nw * nsw) return;  // windows nw.. carry no entries (per-key A term)
@@ -555,6 +559,7 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* _
   p3 T;
   p3_identity(T);
   if (seg > 1) v_store(T);  // V = identity
+  if (acc) p3_load(T, segT, sidx);
   const uint32_t e_lo = offs[key0];
   uint32_t e = offs[key0 + seg];
   uint4 q[7];
@@ -1042,7 +1047,50 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
   const uint32_t nw = agg ? BV_NWR : BV_NW;  // windows with bucket entries
   e = hipMemsetAsync(bsum, 0, (size_t)BV_MAXG * BSUM_WORDS * 8, s);  // k_bv_prep accumulates per group
   if (e != hipSuccess) return e;
-  if (gate && gate->n) {
+  const uint32_t seg = bucket_segment(kn);
+  const bool msm = gate && gate->n && gate->msm && gate->prep_done && G.count == 1 && seg == 1;
+  if (msm) {
+    // streaming MSM: chunk c's preparation on aux (after its copy), then on s its bucket
+    // entries sorted (the partition sort over the chunk's signatures alone) and added into the
+    // persistent bucket sums segT; the reduction and the final follow the last chunk
+    const uint32_t* end = gate->end;
+    if (end[gate->n - 1] != n) return hipErrorInvalidValue;
+    hipStream_t ps = gate->aux ? gate->aux : s;
+    if (gate->aux) {
+      if ((e = hipEventRecord(gate->fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(gate->aux, gate->fork, 0)) != hipSuccess) return e;
+    }
+    for (uint32_t c = 0, lo = 0; c < gate->n; lo = end[c++]) {
+      const uint32_t hi = end[c], nc = hi - lo;
+      if (hi <= lo || lo % PART_CHUNK) return hipErrorInvalidValue;
+      if ((e = hipStreamWaitEvent(ps, gate->ready[c], 0)) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_bv_prep, dim3((nc + 255) / 256), dim3(256), 0, ps, msg, sig, pk, key_idx, n, k, ca,
+                         pts, scal, bsum, status, lo / 256, G.cpg * PART_CHUNK);
+      if (gate->aux) {
+        if ((e = hipEventRecord(gate->prep_done[c], ps)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, gate->prep_done[c], 0)) != hipSuccess) return e;
+      }
+      const uint32_t c0 = lo / PART_CHUNK, ncc = (nc + PART_CHUNK - 1) / PART_CHUNK;
+      const BvGroups Gc{1, ncc};
+      const uint4* sc = scal + (size_t)lo * SC_QUADS;
+      hipLaunchKernelGGL(k_part_count, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, nc, agg ? 1u : 0u,
+                         pcount + (size_t)c0 * BV_NPG);
+      hipLaunchKernelGGL(k_part_scan, dim3(BV_NPG / 64), dim3(64 * SCAN_SUB), 0, s, pcount + (size_t)c0 * BV_NPG, ncc,
+                         Gc, poff + (size_t)c0 * BV_NPG, ptot);
+      hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, (uint32_t)BV_NPG, pstart);
+      hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, nc, poff + (size_t)c0 * BV_NPG, pstart,
+                         Gc, agg ? 1u : 0u, n, lo, tmp);
+      hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
+      hipLaunchKernelGGL(k_bv_bucket, dim3(nw * BV_NB / 256), dim3(256), 0, s, pts, offs, ents, 1u, 1u, nw,
+                         c ? 1u : 0u, segV, segT);
+    }
+    if (gate->aux) {  // (s has waited for every chunk's preparation)
+      if ((e = hipEventRecord(gate->join, gate->aux)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(s, gate->join, 0)) != hipSuccess) return e;
+    }
+    mark(1);
+    mark(2);
+  } else if (gate && gate->n) {
     const uint32_t* end = gate->end;
     if (end[gate->n - 1] != n) return hipErrorInvalidValue;
     if (gate->aux) {
@@ -1065,20 +1113,22 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,
                        status, 0u, G.cpg * PART_CHUNK);
   }
-  mark(1);
-  hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, agg ? 1u : 0u, pcount);
-  hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(64 * SCAN_SUB), 0, s, pcount, nchunk, G, poff, ptot);
-  hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, nparts, pstart);
-  hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
-                     agg ? 1u : 0u, tmp);
-  hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
-  mark(2);
-  // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
-  // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
-  // through memory and the reduction stays the size of one group's
-  const uint32_t seg = bucket_segment(kn);
-  hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
-                     G.count, seg, nw, segV, segT);
+  if (!msm) {
+    mark(1);
+    hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, agg ? 1u : 0u, pcount);
+    hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(64 * SCAN_SUB), 0, s, pcount, nchunk, G, poff,
+                       ptot);
+    hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, nparts, pstart);
+    hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
+                       agg ? 1u : 0u, n, 0u, tmp);
+    hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
+    mark(2);
+    // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
+    // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
+    // through memory and the reduction stays the size of one group's
+    hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
+                       G.count, seg, nw, 0u, segV, segT);
+  }
   if (agg) {
     hipLaunchKernelGGL(k_bv_keyacc, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, key_idx, n, n_keys, kpart);
     hipLaunchKernelGGL(k_bv_keycol, dim3(G.count * n_keys), dim3(256), 0, s, kpart, nchunk, G.cpg, n_keys,

@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dirent.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -138,6 +139,9 @@ struct Device {
   // pinned inputs: per-chunk "copied" events of the two input buffers (verify_host_streamed)
   static constexpr int kMaxChunks = 64;
   hipEvent_t chunk_ev[kPinBufs][kMaxChunks] = {};
+  // the streaming MSM's per-chunk preparation events (aux -> compute stream) and fork / join
+  hipEvent_t prep_ev[kMaxChunks] = {};
+  hipEvent_t msm_fork = nullptr, msm_join = nullptr;
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
   DevBuf committee_pk, stakes, combA, keyok;
@@ -1013,7 +1017,7 @@ bool committee_ready(mv_ctx* ctx) {
 // reads and writes them over PCIe, as the launched online path does); device memory holds the
 // ticket and each slot's ingest scratch. The kernel runs on its own stream, created with a CU
 // mask (a queue of its own, so kernels on other streams never wait behind it; and a bounded
-// share of the chip), and exits after MV_ONLINE_IDLE_US (default 2,000) without a job.
+// share of the chip), and exits after MV_ONLINE_IDLE_US (default 10,000) without a job.
 constexpr uint32_t kOnSlots = mvk::ONLINE_SLOTS, kOnMax = mvk::ONLINE_MAX_BLOCKS;
 constexpr size_t kOnInCap = mvk::ONLINE_IN_CAP;        // bincode bytes per request
 constexpr size_t kOnInStride = mvk::ONLINE_IN_STRIDE;  // off[n] | len[n] | bincode | 16 zero B
@@ -1039,7 +1043,7 @@ struct OnlineSvc {
   // sleep on a futex word of their slot, which the reaper thread sets and wakes once the done
   // word holds their request (99 callers spinning on a 16-CPU share descheduled one another
   // for milliseconds: p99 81 ms). A caller waiting for its slot to be freed sleeps the same way.
-  int max_spinners = 12;
+  int max_spinners = 4;
   std::atomic<int> spinners{0}, sleepers{0};
   std::unique_ptr<std::atomic<uint32_t>[]> dwake;  // per slot: set by the reaper (futex word)
   std::unique_ptr<std::atomic<uint64_t>[]> sleep_q;  // per slot: request + 1 its sleeper waits for, 0: none
@@ -1051,7 +1055,7 @@ struct OnlineSvc {
   uint64_t next_q = 0;
   uint32_t grid = 0, launch_no = 0;
   std::atomic<uint64_t> requests{0}, launches{0};
-  uint64_t idle_us = 2000;
+  uint64_t idle_us = 10000;
   // MV_ONLINE_TRACE: per-stage sums (us) -- host publish to done seen, and on the kernel's
   // clock seen -> ready -> first claim -> last job done -- printed at release
   bool trace = false, debug = false;  // MV_ONLINE_TRACE, MV_ONLINE_DEBUG
@@ -1169,7 +1173,7 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     o.fwait[k].store(0);
   }
   o.max_spinners = ctx->kn.online_spinners > 0 ? (int)ctx->kn.online_spinners
-                                               : std::max(1, host_cpu_share() * 3 / 4);
+                                               : std::max(1, host_cpu_share() / 4);
   if (!o.reaper.joinable()) {
     o.rstop = false;
     o.reaper = std::thread(online_reaper, &o);
@@ -1790,7 +1794,13 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   // Batch sizes: shares of the call (MV_STREAM_FRACS, separated by ',' or '/'; default 0.7,0.3). The
   // last batch's prep, sort, buckets and tail follow the last copy, so the shares decrease;
   // every batch is whole 1,024s, >= MV_BATCH_MIN and <= max_batch (more batches when needed).
-  const std::vector<double> fracs(ctx->kn.stream_fracs, ctx->kn.stream_fracs + ctx->kn.n_stream_fracs);
+  // Streaming MSM (MV_STREAM_MSM, default on): the call is one batch whose chunks are sorted and
+  // added into persistent buckets during the copy window (launch_verify_batch, ChunkGate::msm),
+  // so only the reduction and the final follow the last copy -- no batch's whole MSM does.
+  const bool msm = ctx->kn.stream_msm && m <= ctx->max_batch && ctx->kn.bv_seg <= 1;
+  const std::vector<double> fracs = msm ? std::vector<double>{1.0}
+                                        : std::vector<double>(ctx->kn.stream_fracs,
+                                                              ctx->kn.stream_fracs + ctx->kn.n_stream_fracs);
   std::vector<uint32_t> sizes;
   {
     double tot = 0.0;
@@ -1871,7 +1881,16 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     }
     // every chunk's prep on cs (a second prep stream per compute stream measured slower:
     // 163-167 vs 175-180 M/s; more streams than the 4 hardware queues share queues)
-    const mvk::ChunkGate gate{dev.chunk_ev[b], (uint32_t)marks.size(), marks.data(), nullptr, nullptr, nullptr};
+    if (msm) {
+      for (size_t c = 0; c < marks.size(); c++)
+        if (!dev.prep_ev[c]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.prep_ev[c], hipEventDisableTiming));
+      for (hipEvent_t* ev : {&dev.msm_fork, &dev.msm_join})
+        if (!*ev) HIPCHK(ctx, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    // msm: the chunks' preparations on the other compute stream, sort + buckets on cs
+    const mvk::ChunkGate gate{dev.chunk_ev[b], (uint32_t)marks.size(), marks.data(),
+                              msm ? dev.pstream[(t & 1) ^ 1] : nullptr, msm ? dev.msm_fork : nullptr,
+                              msm ? dev.msm_join : nullptr, msm, msm ? dev.prep_ev : nullptr};
     mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dev.committee_pk.as<uint8_t>(),
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), cs,
@@ -1949,6 +1968,7 @@ const KnobDef kKnobs[] = {
     {"MV_COMB_QUAD", &mvk::Knobs::comb_quad, K_INT, false},
     {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
+    {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_ON, false},
 };
 
 const KnobDef* find_knob(const char* name) {
@@ -2129,8 +2149,35 @@ class PhaseWatch {
  private:
   void run() {
     std::unique_lock<std::mutex> lk(m_);
-    for (int s = 5; !cv_.wait_for(lk, std::chrono::seconds(5), [this] { return done_; }); s += 5)
+    for (int s = 5; !cv_.wait_for(lk, std::chrono::seconds(5), [this] { return done_; }); s += 5) {
       fprintf(stderr, "[%s] still in '%s' after %d s\n", what_, phase_.load(), s);
+      if (s == 5) dump_threads();
+    }
+  }
+  // every thread's name, kernel wait channel and current system call (/proc/self/task): tells a
+  // runtime wait on a GPU signal (ioctl) from one on a lock (futex)
+  static void dump_threads() {
+    DIR* d = opendir("/proc/self/task");
+    if (!d) return;
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] == '.') continue;
+      char path[128], comm[64] = {0}, wchan[64] = {0}, sc[160] = {0};
+      auto rd = [&](const char* f, char* out, size_t cap) {
+        snprintf(path, sizeof path, "/proc/self/task/%s/%s", e->d_name, f);
+        if (FILE* fp = fopen(path, "r")) {
+          size_t k = fread(out, 1, cap - 1, fp);
+          out[k] = 0;
+          fclose(fp);
+          for (char* c = out; *c; c++)
+            if (*c == '\n') *c = ' ';
+        }
+      };
+      rd("comm", comm, sizeof comm);
+      rd("wchan", wchan, sizeof wchan);
+      rd("syscall", sc, sizeof sc);
+      fprintf(stderr, "  tid %s %s wchan=%s syscall=%s\n", e->d_name, comm, wchan, sc);
+    }
+    closedir(d);
   }
   const char* what_;
   std::atomic<const char*> phase_{"start"};
@@ -2196,6 +2243,11 @@ void mv_destroy(mv_ctx* ctx) {
       if (dev.pin_free[k]) (void)hipEventDestroy(dev.pin_free[k]);
       for (hipEvent_t ev : dev.chunk_ev[k])
         if (ev) (void)hipEventDestroy(ev);
+    }
+    for (hipEvent_t ev : dev.prep_ev)
+      if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : {dev.msm_fork, dev.msm_join}) {
+      if (ev) (void)hipEventDestroy(ev);
     }
     for (int k = 0; k < 2; k++) {
       watch.phase("frees: host staging");

@@ -31,11 +31,11 @@ struct Knobs {
   int64_t online_long = 1;               // MV_ONLINE_LONG: long blocks take it too
   int64_t online_cus = 64;               // MV_ONLINE_CUS: the service stream's CU mask (0: ordinary stream)
   int64_t online_wgs = 0;                // MV_ONLINE_WGS: resident workgroups (0: = CUs)
-  int64_t online_idle_us = 2000;         // MV_ONLINE_IDLE_US: the launch ends after this long idle
+  int64_t online_idle_us = 10000;        // MV_ONLINE_IDLE_US: the launch ends after this long idle
   int64_t online_trace = 0;              // MV_ONLINE_TRACE: per-stage means on stderr at release
   int64_t online_debug = 0;              // MV_ONLINE_DEBUG: launch lines, long waits on stderr
   int64_t online_inject = 0;             // MV_ONLINE_INJECT: fault injection (tests): launches fail
-  int64_t online_spinners = 0;           // MV_ONLINE_SPINNERS: callers spinning on their verdict (0: 3/4 of the CPU share)
+  int64_t online_spinners = 0;           // MV_ONLINE_SPINNERS: callers spinning on their verdict (0: 1/4 of the CPU share)
   // signature path
   int64_t pipeline = 0;                  // MV_PIPELINE: pageable signature staging experiment
   int64_t pipe_chunk_log2 = 18;          // MV_PIPE_CHUNK_LOG2
@@ -57,6 +57,7 @@ struct Knobs {
   int64_t comb_quad = -1;                // MV_COMB_QUAD: force k_verify_comb16 (1) / k_verify_comb (0)
   int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
   int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
+  int64_t stream_msm = 1;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM
 };
 
 size_t verify_scratch_bytes(uint32_t n);
@@ -101,6 +102,12 @@ struct ChunkGate {
   const uint32_t* end;
   hipStream_t aux;  // may be null: every chunk on s
   hipEvent_t fork, join;
+  // streaming MSM (msm = true, one group, chunk starts multiples of 1,024): each chunk's bucket
+  // entries are sorted and added into persistent bucket sums as soon as its preparation is
+  // done, so only the reduction and the final follow the last chunk. prep_done (n events):
+  // chunk c's preparation on aux -> s.
+  bool msm;
+  const hipEvent_t* prep_done;
 };
 constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
 constexpr int BATCH_MAX_GROUPS = 16;
