@@ -1794,9 +1794,12 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   // Batch sizes: shares of the call (MV_STREAM_FRACS, separated by ',' or '/'; default 0.7,0.3). The
   // last batch's prep, sort, buckets and tail follow the last copy, so the shares decrease;
   // every batch is whole 1,024s, >= MV_BATCH_MIN and <= max_batch (more batches when needed).
-  // Streaming MSM (MV_STREAM_MSM, default on): the call is one batch whose chunks are sorted and
-  // added into persistent buckets during the copy window (launch_verify_batch, ChunkGate::msm),
-  // so only the reduction and the final follow the last copy -- no batch's whole MSM does.
+  // Streaming MSM (MV_STREAM_MSM=1, off by default): the call is one batch whose chunks are sorted
+  // and added into persistent buckets during the copy window (launch_verify_batch,
+  // ChunkGate::msm), so only the reduction and the final follow the last copy. Measured slower
+  // (2^20 pinned signatures: 181-196 M/s against 198 M/s for two batches on two streams,
+  // profiles/r05/e2e_msm.txt): the call is bound by its compute (~4.3 ms of kernels on one
+  // stream against 2.9 ms of copies), and every chunk pays a sort and a walk over all buckets.
   const bool msm = ctx->kn.stream_msm && m <= ctx->max_batch && ctx->kn.bv_seg <= 1;
   const std::vector<double> fracs = msm ? std::vector<double>{1.0}
                                         : std::vector<double>(ctx->kn.stream_fracs,
@@ -1968,7 +1971,7 @@ const KnobDef kKnobs[] = {
     {"MV_COMB_QUAD", &mvk::Knobs::comb_quad, K_INT, false},
     {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
-    {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_ON, false},
+    {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_OFF, false},
 };
 
 const KnobDef* find_knob(const char* name) {

@@ -57,7 +57,7 @@ struct Knobs {
   int64_t comb_quad = -1;                // MV_COMB_QUAD: force k_verify_comb16 (1) / k_verify_comb (0)
   int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
   int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
-  int64_t stream_msm = 1;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM
+  int64_t stream_msm = 0;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM (measured slower)
 };
 
 size_t verify_scratch_bytes(uint32_t n);
