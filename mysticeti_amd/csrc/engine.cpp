@@ -1181,6 +1181,14 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   // CU mask: MV_ONLINE_CUS (default 64) CUs spread evenly over the chip; 0 = an ordinary stream
   int cus = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev.id));
+  // The service's stream needs a hardware queue of its own: a kernel queued behind the resident
+  // one on a shared queue would wait for it. Default (round 5): a stream of the highest priority
+  // (the runtime keeps a queue per priority level, and the engine's other streams are all of
+  // the default priority). Round 4 used a CU-masked stream (MV_ONLINE_CUS > 0, still
+  // selectable): tearing one down left a later hipStreamDestroy of an unrelated stream waiting
+  // forever on a runtime lock, in about 1 of 10 processes (the driver's round-4
+  // smoke; 0 stalls in 78 processes without it). MV_ONLINE_CUS = 0 and MV_ONLINE_PRIO = 0: an
+  // ordinary stream (shares a queue; A/B only).
   int want = (int)ctx->kn.online_cus;
   if (want > cus) want = cus;
   if (want > 0 && want < cus) {
@@ -1190,6 +1198,10 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
       mask[cu / 32] |= 1u << (cu % 32);
     }
     HIPCHK(ctx, hipExtStreamCreateWithCUMask(&o.stream, (uint32_t)mask.size(), mask.data()));
+  } else if (ctx->kn.online_prio) {
+    int least = 0, greatest = 0;
+    HIPCHK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(ctx, hipStreamCreateWithPriority(&o.stream, hipStreamNonBlocking, greatest));
   } else {
     HIPCHK(ctx, hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking));
   }
@@ -1203,7 +1215,7 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     else
       (void)hipGetLastError();
   }
-  const int64_t ge = ctx->kn.online_wgs;  // resident workgroups (4-block jobs in flight; 0: one per CU of the mask)
+  const int64_t ge = ctx->kn.online_wgs;  // resident workgroups (4-block jobs in flight; 0: 64, or one per CU of the mask)
   o.grid = (uint32_t)(ge > 0 ? std::max<int64_t>(2, ge) : (want > 0 ? want : 64));  // >= 2: the poller + workers
   o.grid = std::min<uint32_t>(o.grid, mvk::ONLINE_MAX_WGS);
   o.ready = true;
@@ -1949,6 +1961,7 @@ const KnobDef kKnobs[] = {
     {"MV_ONLINE", &mvk::Knobs::online, K_ON, false},
     {"MV_ONLINE_LONG", &mvk::Knobs::online_long, K_ON, false},
     {"MV_ONLINE_CUS", &mvk::Knobs::online_cus, K_INT, false},
+    {"MV_ONLINE_PRIO", &mvk::Knobs::online_prio, K_ON, false},
     {"MV_ONLINE_WGS", &mvk::Knobs::online_wgs, K_INT, false},
     {"MV_ONLINE_IDLE_US", &mvk::Knobs::online_idle_us, K_INT, false},
     {"MV_ONLINE_TRACE", &mvk::Knobs::online_trace, K_FLAG, false},

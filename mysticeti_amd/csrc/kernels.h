@@ -29,7 +29,8 @@ struct Knobs {
   // the resident online service
   int64_t online = 1;                    // MV_ONLINE: small block calls take the service
   int64_t online_long = 1;               // MV_ONLINE_LONG: long blocks take it too
-  int64_t online_cus = 64;               // MV_ONLINE_CUS: the service stream's CU mask (0: ordinary stream)
+  int64_t online_cus = 0;                // MV_ONLINE_CUS: > 0: a CU-masked service stream of that many CUs (round 4)
+  int64_t online_prio = 1;               // MV_ONLINE_PRIO: the service stream at the highest priority (its own queue)
   int64_t online_wgs = 0;                // MV_ONLINE_WGS: resident workgroups (0: = CUs)
   int64_t online_idle_us = 10000;        // MV_ONLINE_IDLE_US: the launch ends after this long idle
   int64_t online_trace = 0;              // MV_ONLINE_TRACE: per-stage means on stderr at release
