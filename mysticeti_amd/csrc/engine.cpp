@@ -148,7 +148,10 @@ struct Device {
   // scratch rings: consecutive calls rotate over kSlots slots, so a call on one stream can
   // run while the previous ones (on other streams) finish their latency-bound tails; an
   // event per slot orders reuse across streams. Batch path: bscr/vscr; blocks: blk.
-  static constexpr int kSlots = 2;
+#ifndef MV_SLOTS
+#define MV_SLOTS 2
+#endif
+  static constexpr int kSlots = MV_SLOTS;
   static constexpr int kFlagWords = 1 + mvk::BATCH_MAX_GROUPS;
   DevBuf bscr[kSlots], vscr[kSlots];
   hipEvent_t slot_done[kSlots] = {};
