@@ -144,7 +144,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20, help="0 disables the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="batch path: streams the steps alternate over")
+    ap.add_argument("--streams", type=int, default=3, help="batch path: streams the steps rotate over (3: profiles/r05/c2_streams_slots.txt)")
     ap.add_argument("--path", choices=["batch", "single"], default="batch",
                     help="batch: one combined equation per step (batch.hip) with exact fallback; "
                          "single: every signature verified alone (k_verify)")
@@ -232,8 +232,10 @@ def main():
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     # dedicated non-default streams: the library launches on them and the HIP events
     # below are recorded on them, so kernel_ms times exactly the verify launches. The
-    # batch path alternates two streams so that one batch's latency-bound tail (window
-    # reduction, final check: a few waves) runs beside the next batch's full-chip kernels.
+    # batch path rotates over three streams so that one batch's latency-bound tail (window
+    # reduction, final check: a few waves) runs beside the next batches' full-chip kernels
+    # (three streams and three engine scratch slots: 316-319 M/s against 295-299 M/s on two,
+    # profiles/r05/c2_streams_slots.txt).
     nstreams = args.streams if args.path == "batch" else 1
     streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
     assert all(st.cuda_stream != 0 for st in streams)

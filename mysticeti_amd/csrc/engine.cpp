@@ -149,7 +149,7 @@ struct Device {
   // run while the previous ones (on other streams) finish their latency-bound tails; an
   // event per slot orders reuse across streams. Batch path: bscr/vscr; blocks: blk.
 #ifndef MV_SLOTS
-#define MV_SLOTS 2
+#define MV_SLOTS 3
 #endif
   static constexpr int kSlots = MV_SLOTS;
   static constexpr int kFlagWords = 1 + mvk::BATCH_MAX_GROUPS;
