@@ -174,7 +174,10 @@ struct Device {
   // keeps one call running beside the next), all grown together on first use so no slot is
   // allocated inside a caller's steady state (a 2^21-block slot is ~21 GB; round 3's four
   // lazily grown slots put one ~0.8 s allocation into the driver's timed steps)
-  static constexpr int kBlkSlots = 2;
+#ifndef MV_BLK_SLOTS
+#define MV_BLK_SLOTS 2
+#endif
+  static constexpr int kBlkSlots = MV_BLK_SLOTS;
   DevBuf blk[kBlkSlots];
   hipEvent_t blk_done[kBlkSlots] = {};
   bool blk_used[kBlkSlots] = {};
