@@ -584,10 +584,11 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // The resident online service (kernels.h OnlineArgs). Every branch around a barrier is
 // uniform (the role is the workgroup's, decisions are broadcast through LDS), and every wait
 // loop also tests the launch's end, so all waves leave.
-constexpr uint32_t ON_BATCH = 64;  // the poller's window (requests it can move per pass): the whole ring
+constexpr uint32_t ON_BATCH = 64;  // the poller's window (requests it can move per pass): one wave's lanes
 constexpr uint32_t ON_COPY_UNROLL = 8;  // 16-B input loads per poller thread in flight
 static_assert(IG_WIN == mvk::INGEST_WINDOW_BYTES, "the host's eligibility test uses the ingest window");
-static_assert(ON_BATCH == mvk::ONLINE_SLOTS && ON_BATCH <= 64, "the window's lanes cover distinct slots, one wave");
+static_assert(ON_BATCH <= mvk::ONLINE_SLOTS && ON_BATCH <= 64 && mvk::ONLINE_SLOTS % 64 == 0,
+              "the window's lanes cover distinct slots, one wave");
 
 // Workgroup 0: moves published requests from page-locked memory into HBM, appends their jobs.
 MV_DEV void online_poller(const mvk::OnlineArgs& A) {
@@ -614,7 +615,7 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       // its seq) does not hold back the requests behind it (round 4 moved only the
       // consecutive prefix, and 99 concurrent callers stalled behind one). `moved[slot]`
       // (request + 1, poller-only) marks the ones already moved; `ready` advances over the
-      // moved prefix. The window is the whole ring: the slots of its lanes are distinct.
+      // moved prefix. The window is at most the ring: the slots of its lanes are distinct.
       // Polls are relaxed (an acquire invalidates the caches every time: the working
       // workgroups' comb tables with them); one acquire fence once requests are seen. The
       // window's seq words are read together (one PCIe round trip): a request is published

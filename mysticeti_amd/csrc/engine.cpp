@@ -175,7 +175,7 @@ struct Device {
   // allocated inside a caller's steady state (a 2^21-block slot is ~21 GB; round 3's four
   // lazily grown slots put one ~0.8 s allocation into the driver's timed steps)
 #ifndef MV_BLK_SLOTS
-#define MV_BLK_SLOTS 2
+#define MV_BLK_SLOTS 3
 #endif
   static constexpr int kBlkSlots = MV_BLK_SLOTS;
   DevBuf blk[kBlkSlots];

@@ -188,9 +188,12 @@ struct BlockIngestIn {
 // max_ticks; workers leave when they see quit. A launch starts by discarding tickets of the
 // previous launch's workers (head = tail) before any worker takes one (epoch handshake).
 // The slot's HBM scratch layout is fixed (below), so a descriptor is 16 bytes.
-constexpr uint32_t ONLINE_SLOTS = 64;
+#ifndef MV_ONLINE_SLOTS
+#define MV_ONLINE_SLOTS 64
+#endif
+constexpr uint32_t ONLINE_SLOTS = MV_ONLINE_SLOTS;  // request ring (a multiple of 64)
 constexpr uint32_t ONLINE_MAX_BLOCKS = 64;  // 16 jobs per request
-constexpr uint32_t ONLINE_JOBS = 2048;      // job ring (>= SLOTS x 16)
+constexpr uint32_t ONLINE_JOBS = 16 * ONLINE_SLOTS;  // job ring (>= SLOTS x 16)
 constexpr uint32_t ONLINE_MAX_WGS = 256;    // resident workgroups at most (the poller + workers)
 constexpr uint32_t ONLINE_WG_LEFT = 0x80000000u;
 constexpr uint64_t ONLINE_EXIT_STOP = 1, ONLINE_EXIT_IDLE = 2, ONLINE_EXIT_MAX = 3;
