@@ -189,7 +189,7 @@ struct BlockIngestIn {
 // previous launch's workers (head = tail) before any worker takes one (epoch handshake).
 // The slot's HBM scratch layout is fixed (below), so a descriptor is 16 bytes.
 #ifndef MV_ONLINE_SLOTS
-#define MV_ONLINE_SLOTS 64
+#define MV_ONLINE_SLOTS 128
 #endif
 constexpr uint32_t ONLINE_SLOTS = MV_ONLINE_SLOTS;  // request ring (a multiple of 64)
 constexpr uint32_t ONLINE_MAX_BLOCKS = 64;  // 16 jobs per request
