@@ -267,6 +267,15 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
         if (live) pt_store(pts, (size_t)n + gid, pc);
       }
     } else {
+#ifdef MV_PREP_X2
+    // (A/B) both chains interleaved: twice the ILP per lane
+    p3 P, Q;
+    decompress2_lean(Q, okA, aw, P, okR, rw);
+    precomp_from_affine(pc, P);
+    if (live) pt_store(pts, gid, pc);
+    precomp_from_affine(pc, Q);
+    if (live) pt_store(pts, (size_t)n + gid, pc);
+#else
     // one decode at a time at 3 waves/SIMD beat the two decodes in lock-step (decompress_x2)
     // at 2 waves/SIMD: 241 vs 220 M verifies/s for the whole batch path
     p3 P;
@@ -279,6 +288,7 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
     decompress1_lean(P, okA, aw);
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, (size_t)n + gid, pc);
+#endif
     }
   }
   const bool ok = live && okA && okR && s_ok;

@@ -266,4 +266,52 @@ MV_DEV void decompress1_lean(p3& A, bool& okA, const uint32_t ea[8]) {
   A.X = xa; A.Y = ya; fe_set(A.Z, 1); fe_mul(A.T, xa, ya);
 }
 
+// Two decompress1_lean's with their exponentiation chains interleaved (fe_pow_p58_x2: two
+// independent squarings per step, twice the ILP of one chain); only the two chain states are
+// live across them, the rest is recomputed from the encodings afterwards.
+MV_DEV void decompress2_lean(p3& A, bool& okA, const uint32_t ea[8], p3& R, bool& okR, const uint32_t er[8]) {
+  fe pa, pr;
+  {
+    fe xa, xr;
+    {
+      fe d, one, y, u, v, t;
+      fe_const(d, K_D);
+      fe_set(one, 1);
+      fe_from_words(y, ea);
+      fe_sq(t, y);
+      fe_sub(u, t, one);
+      fe_mul(v, t, d);
+      fe_add(v, v, one);
+      fe_sq(t, v); fe_mul(xa, t, v);
+      fe_sq(t, xa); fe_mul(xa, t, v); fe_mul(xa, xa, u);  // u v^7 of A
+      fe_from_words(y, er);
+      fe_sq(t, y);
+      fe_sub(u, t, one);
+      fe_mul(v, t, d);
+      fe_add(v, v, one);
+      fe_sq(t, v); fe_mul(xr, t, v);
+      fe_sq(t, xr); fe_mul(xr, t, v); fe_mul(xr, xr, u);  // u v^7 of R
+    }
+    fe_pow_p58_x2(pa, pr, xa, xr);
+  }
+  auto finish = [](p3& P, bool& ok, const uint32_t e[8], fe& p) {
+    fe d, one, y, u, v, t, v3, x, n;
+    fe_const(d, K_D);
+    fe_set(one, 1);
+    fe_from_words(y, e);
+    fe_sq(t, y);
+    fe_sub(u, t, one);
+    fe_mul(v, t, d);
+    fe_add(v, v, one);
+    fe_sq(t, v); fe_mul(v3, t, v);
+    fe_mul(p, p, v3); fe_mul(p, p, u);
+    ok = sqrt_ratio_finish(x, u, v, p);
+    fe_neg(n, x);
+    fe_cmov(x, n, (e[7] >> 31) != 0);
+    P.X = x; P.Y = y; fe_set(P.Z, 1); fe_mul(P.T, x, y);
+  };
+  finish(A, okA, ea, pa);
+  finish(R, okR, er, pr);
+}
+
 }  // namespace mv
