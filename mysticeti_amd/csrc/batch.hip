@@ -182,6 +182,9 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
   // thread's own stores (which would keep the values live in registers after all); volatile
   // would not do: it turns the accesses into 64-bit-addressed flat ones
   __shared__ uint32_t va[8][256], vs[8][256], vz[4][256];
+#ifdef MV_PREP_X2
+  __shared__ uint32_t vr[8][256];  // R's encoding, parked like A's across the two chains
+#endif
   const uint32_t t = threadIdx.x;
   if (threadIdx.x < BSUM_WORDS) sbsum[threadIdx.x] = 0;
   __syncthreads();
@@ -270,7 +273,13 @@ __global__ void __launch_bounds__(256, MV_PREP_OCC)
 #ifdef MV_PREP_X2
     // (A/B) both chains interleaved: twice the ILP per lane
     p3 P, Q;
-    decompress2_lean(Q, okA, aw, P, okR, rw);
+#pragma unroll
+    for (int i = 0; i < 8; i++) vr[i][t] = rw[i];
+    decompress2_lean(Q, okA, P, okR, [&](int which, uint32_t (&e)[8]) {
+      asm volatile("" ::: "memory");  // re-read from LDS (not forwarded from registers)
+#pragma unroll
+      for (int i = 0; i < 8; i++) e[i] = which ? vr[i][t] : va[i][t];
+    });
     precomp_from_affine(pc, P);
     if (live) pt_store(pts, gid, pc);
     precomp_from_affine(pc, Q);

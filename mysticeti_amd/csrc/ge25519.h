@@ -269,12 +269,18 @@ MV_DEV void decompress1_lean(p3& A, bool& okA, const uint32_t ea[8]) {
 // Two decompress1_lean's with their exponentiation chains interleaved (fe_pow_p58_x2: two
 // independent squarings per step, twice the ILP of one chain); only the two chain states are
 // live across them, the rest is recomputed from the encodings afterwards.
-MV_DEV void decompress2_lean(p3& A, bool& okA, const uint32_t ea[8], p3& R, bool& okR, const uint32_t er[8]) {
+// The encodings come from get(which, words) (0: A, 1: R), called before and again after the
+// chains, so a kernel can park them in LDS instead of holding 16 registers across the chains.
+template <class Get>
+MV_DEV void decompress2_lean(p3& A, bool& okA, p3& R, bool& okR, Get get) {
   fe pa, pr;
   {
     fe xa, xr;
     {
       fe d, one, y, u, v, t;
+      uint32_t ea[8], er[8];
+      get(0, ea);
+      get(1, er);
       fe_const(d, K_D);
       fe_set(one, 1);
       fe_from_words(y, ea);
@@ -292,7 +298,7 @@ MV_DEV void decompress2_lean(p3& A, bool& okA, const uint32_t ea[8], p3& R, bool
       fe_sq(t, v); fe_mul(xr, t, v);
       fe_sq(t, xr); fe_mul(xr, t, v); fe_mul(xr, xr, u);  // u v^7 of R
     }
-    fe_pow_p58_x2(pa, pr, xa, xr);
+    fe_pow_p58_x2_nox(pa, pr, xa, xr);  // (u v^7)^(2^252 - 4): the last factor u v^7 below
   }
   auto finish = [](p3& P, bool& ok, const uint32_t e[8], fe& p) {
     fe d, one, y, u, v, t, v3, x, n;
@@ -304,14 +310,19 @@ MV_DEV void decompress2_lean(p3& A, bool& okA, const uint32_t ea[8], p3& R, bool
     fe_mul(v, t, d);
     fe_add(v, v, one);
     fe_sq(t, v); fe_mul(v3, t, v);
+    fe_sq(t, v3); fe_mul(t, t, v); fe_mul(t, t, u);  // u v^7
+    fe_mul(p, p, t);                                 // (u v^7)^((p - 5) / 8)
     fe_mul(p, p, v3); fe_mul(p, p, u);
     ok = sqrt_ratio_finish(x, u, v, p);
     fe_neg(n, x);
     fe_cmov(x, n, (e[7] >> 31) != 0);
     P.X = x; P.Y = y; fe_set(P.Z, 1); fe_mul(P.T, x, y);
   };
-  finish(A, okA, ea, pa);
-  finish(R, okR, er, pr);
+  uint32_t e[8];
+  get(0, e);
+  finish(A, okA, e, pa);
+  get(1, e);
+  finish(R, okR, e, pr);
 }
 
 }  // namespace mv
