@@ -614,27 +614,6 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
                                      com.epoch, com.quorum_threshold, stage, poff + lo, plen + lo, sig + 64 * (size_t)lo,
                                      kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
     };
-    const uint64_t phc = ctx->kn.blk_ph_chunk > 0 ? std::max<uint64_t>(MV_BATCH_MIN, (uint64_t)ctx->kn.blk_ph_chunk) : 0;
-    if (phc && n >= 2 * phc) {
-      // (A/B, MV_BLK_PH_CHUNK) chunks of phc blocks, parse then hash on one stream, even chunks
-      // on s and odd ones on aux: each hash re-reads a pre-image written a moment before
-      // (a chunk's pre-images can stay in the 256-MB Infinity Cache), and one stream's parse
-      // runs beside the other's hash
-      HIPCHK(ctx, hipEventRecord(ax.ev[0], s));
-      HIPCHK(ctx, hipStreamWaitEvent(aux, ax.ev[0], 0));
-      const uint64_t c = (phc + 63) & ~63ull;
-      uint32_t k = 0;
-      for (uint64_t lo = 0; lo < n; lo += c, k++) {
-        const uint32_t hi = (uint32_t)std::min<uint64_t>(n, lo + c);
-        hipStream_t st = (k & 1) ? aux : s;
-        HIPCHK(ctx, parse((uint32_t)lo, hi, st));
-        HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff + lo, plen + lo, hi - (uint32_t)lo, md + 32 * lo,
-                                           bd + 32 * lo, st));
-      }
-      HIPCHK(ctx, hipEventRecord(ax.ev[1], aux));
-      HIPCHK(ctx, hipStreamWaitEvent(s, ax.ev[1], 0));
-      HIPCHK(ctx, mark(1));
-    } else {
     HIPCHK(ctx, parse(0, h, s));
     HIPCHK(ctx, hipEventRecord(ax.ev[0], s));
     HIPCHK(ctx, hipStreamWaitEvent(aux, ax.ev[0], 0));
@@ -644,7 +623,6 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff, plen, h, md, bd, s));
     HIPCHK(ctx, hipStreamWaitEvent(s, ax.ev[1], 0));
     HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff + h, plen + h, n - h, md + 32 * (size_t)h, bd + 32 * (size_t)h, s));
-    }
   } else {
     HIPCHK(ctx, mvk::launch_block_parse(ctx->kn, d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                         com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
@@ -2013,7 +1991,6 @@ const KnobDef kKnobs[] = {
     {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
     {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_OFF, false},
-    {"MV_BLK_PH_CHUNK", &mvk::Knobs::blk_ph_chunk, K_INT, false},
 };
 
 const KnobDef* find_knob(const char* name) {

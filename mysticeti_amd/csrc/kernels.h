@@ -13,7 +13,6 @@ namespace mvk {
 struct Knobs {
   // block path (engine.cpp)
   int64_t blk_pipe = 1;                  // MV_BLK_PIPE: batch-size block calls in two halves on two streams
-  int64_t blk_ph_chunk = 0;              // MV_BLK_PH_CHUNK: > 0: parse + hash in chunks of this many blocks
   int64_t comb_split_bytes = 2048;       // MV_COMB_SPLIT_BYTES: bytes per block from which the split comb path runs
   int64_t blk_fused = 0;                 // MV_BLK_FUSED: the fused ingest + hash kernel
   int64_t hash_in_comb = 1;              // MV_HASH_IN_COMB: online passes hash inside k_verify_comb16
