@@ -483,9 +483,15 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     traffic, traffic_src = pmc_traffic(kname, "c4")
     if hash_ms:
         ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
+        # kernel_ms is one launch over the call's n blocks (stage timing runs the hash as one
+        # launch); the PMC pass (tools/gpu.sh pmc:c4s1) launches it over 2^20 blocks, so its
+        # bytes are scaled to n: both numbers are per the same n blocks
+        traffic_n = round(traffic * n / (1 << 20)) if traffic else None
         roof = {"bound": "valu", "kernel": kname, "kernel_ms": hash_ms,
                 "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
-                "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": traffic_n,
+                "per": f"one launch over {n} blocks (kernel_ms, traffic, achieved)",
+                "traffic_per_2^20_blocks": traffic, "traffic_source": traffic_src,
                 "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
                                   f"algorithmic) x {W_BLAKE2B_OPS} ops"}
     host_fed = None
