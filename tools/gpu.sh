@@ -140,6 +140,9 @@ for T in "$@"; do
       cmd=${W[$wl]}
       [ -n "$cmd" ] || { echo "unknown workload $wl"; exit 1; }
       mkdir -p "$OUT/pmc_$wl"
+      # config 4: one parse and one hash launch per call (no two halves), so every launch of a
+      # kernel covers the same 2^20 blocks and the per-launch averages are per 2^20 blocks
+      [ "$wl" = c4s1 ] && export MV_BLK_PIPE=0
       run 400 "$OUT/pmc_$wl/trace.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmc_$wl/trace1" -o run -- $cmd
       i=0
       for group in "${PMC_GROUPS[@]}"; do
