@@ -746,15 +746,40 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
     __syncthreads();
     if (t == 0) {
       unsigned long long jt = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // merge (A.merge): the pass's one-block requests go four to a job in a merge area; the
+      // area's off / len point at each block's bincode in its own slot's scratch (offsets from
+      // A.scr), so nothing is copied
+      uint32_t gcnt = 0, garea = 0;
+      auto close_group = [&]() {
+        dev->mcount[garea] = gcnt;
+        dev->jobs[jt % mvk::ONLINE_JOBS] = mvk::ONLINE_JOB_MERGED | garea;
+        jt++;
+        gcnt = 0;
+      };
       for (uint32_t i = 0; i < cnt; i++) {
         const uint64_t q = rdy + qoff[i];
         const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS), nj = (nblk[i] + C16_SIGS - 1) / C16_SIGS;
         dev->n[slot] = nblk[i];
         __hip_atomic_store(&dev->moved[slot], (unsigned long long)(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (nj == 0)  // a void request: complete it here
+        if (nj == 0) {  // a void request: complete it here
           __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        for (uint32_t j = 0; j < nj; j++, jt++) dev->jobs[jt % mvk::ONLINE_JOBS] = ((unsigned long long)q << 8) | j;
+        } else if (A.merge && nblk[i] == 1) {
+          if (gcnt == 0) garea = (uint32_t)(dev->mgroups++ % mvk::ONLINE_SLOTS);
+          // (the slot's off[0] / len[0], just copied by the other threads: read past this CU's L1,
+          // which may hold the slot's previous request)
+          uint64_t* so = reinterpret_cast<uint64_t*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot);
+          const uint64_t o0 = __hip_atomic_load(so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t l0 = __hip_atomic_load(so + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint64_t* ao = reinterpret_cast<uint64_t*>(A.mscr + mvk::ONLINE_SCR_STRIDE * garea);
+          ao[gcnt] = mvk::ONLINE_SCR_STRIDE * slot + 16 + o0;  // the block's bincode, from A.scr
+          ao[4 + gcnt] = l0;                                    // its length
+          dev->mq[garea][gcnt] = q;
+          if (++gcnt == C16_SIGS) close_group();
+        } else {
+          for (uint32_t j = 0; j < nj; j++, jt++) dev->jobs[jt % mvk::ONLINE_JOBS] = ((unsigned long long)q << 8) | j;
+        }
       }
+      if (gcnt) close_group();
       __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + adv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&dev->jobs_tail, jt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -765,12 +790,65 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   }
 }
 
+// A merged job (OnlineArgs::merge): up to four one-block requests in merge area `area`, whose
+// off / len point at each block's bincode in its own slot's scratch (offsets from A.scr); the
+// pre-images, digests and verdicts go to the area; then each block's outputs to its request's
+// page-locked slot (index 0) and, after one system-scope fence, each request's done word.
+MV_DEV void online_merged_job(const mvk::OnlineArgs& A, uint32_t area) {
+  mvk::OnlineCtl* ctl = A.ctl;
+  mvk::OnlineDev* dev = A.dev;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(dev->mcount[area]);
+  uint8_t* sc = A.mscr + mvk::ONLINE_SCR_STRIDE * area;
+  const uint64_t* off = reinterpret_cast<const uint64_t*>(sc);
+  uint8_t* out = sc + mvk::ONLINE_O_OUT;
+  uint8_t* md = out;
+  uint8_t* bd = out + 32 * mvk::ONLINE_MAX_BLOCKS;
+  uint8_t* st = out + 64 * mvk::ONLINE_MAX_BLOCKS;
+  uint8_t* stage = sc + mvk::ONLINE_O_STAGE;
+  uint64_t* poff = reinterpret_cast<uint64_t*>(sc + mvk::ONLINE_O_POFF);
+  uint64_t* plen = reinterpret_cast<uint64_t*>(sc + mvk::ONLINE_O_PLEN);
+  uint8_t* sig = sc + mvk::ONLINE_O_SIG;
+  uint32_t* kidx = reinterpret_cast<uint32_t*>(sc + mvk::ONLINE_O_KIDX);
+  uint32_t* facts = reinterpret_cast<uint32_t*>(sc + mvk::ONLINE_O_FACTS);
+  uint8_t* claimed = sc + mvk::ONLINE_O_CLAIMED;
+  const mvk::BlockVerdictOut bv{facts, claimed, md, bd, st};
+  const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
+  const mvk::BlockIngestIn ing{A.scr, off, off + 4, A.stakes, A.n_auth, A.epoch, A.quorum_thr,
+                               stage, poff, plen, sig, kidx, facts, claimed};
+  comb16_wg(0, md, sig, A.pk, kidx, n, (const uint4*)A.combB, (const uint4*)A.combA, A.key_ok,
+            sc + mvk::ONLINE_O_SST, bv, hin, ing, nullptr);
+  __syncthreads();  // the job's digests and verdicts are in HBM (workgroup scope)
+  if (t < 16 * n) {  // block b's md (words 0..7) and bd (8..15) -> its request's slot, index 0
+    const uint32_t b = t / 16, w = t % 16;
+    const uint32_t slot = (uint32_t)(dev->mq[area][b] % mvk::ONLINE_SLOTS);
+    uint8_t* oh = A.out_host + mvk::ONLINE_OUT_STRIDE * slot;
+    const size_t src = w < 8 ? 32 * (size_t)b + 4 * w : 32 * ((size_t)mvk::ONLINE_MAX_BLOCKS + b) + 4 * (w - 8);
+    const size_t dst = w < 8 ? 4 * (size_t)w : 32 * (size_t)mvk::ONLINE_MAX_BLOCKS + 4 * (w - 8);
+    *reinterpret_cast<uint32_t*>(oh + dst) = *reinterpret_cast<const uint32_t*>(out + src);
+  } else if (t >= 64 && t < 64 + n) {
+    const uint32_t b = t - 64;
+    const uint32_t slot = (uint32_t)(dev->mq[area][b] % mvk::ONLINE_SLOTS);
+    A.out_host[mvk::ONLINE_OUT_STRIDE * slot + 64 * (size_t)mvk::ONLINE_MAX_BLOCKS] =
+        out[64 * (size_t)mvk::ONLINE_MAX_BLOCKS + b];
+  }
+  if (t < 128) __threadfence_system();  // the writers' outputs (waves 0, 1) before the done words
+  __syncthreads();
+  if (t < n) {
+    const uint64_t q = dev->mq[area][t];
+    const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
+    __hip_atomic_store(&ctl->trace[slot][3], on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();  // mcount / mq of this area are read before the next claim reuses LDS
+}
+
 // Workgroups 1..: take a ticket, wait until the ring's tail passes it, run that job from HBM,
 // hand its outputs to the host.
 MV_DEV void online_worker(const mvk::OnlineArgs& A) {
   mvk::OnlineCtl* ctl = A.ctl;
   mvk::OnlineDev* dev = A.dev;
-  __shared__ uint32_t job[4];  // kind (1 work, 2 exit), request lo / hi, job
+  __shared__ uint32_t job[4];  // kind (1 work, 2 exit, 3 merged job), request (merged: area) lo / hi, job
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
   bool setup = false;
@@ -795,9 +873,15 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
           if (tk < __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const unsigned long long e = dev->jobs[tk % mvk::ONLINE_JOBS];
-            q = e >> 8;
-            j = (uint32_t)(e & 0xffu);
-            kind = 1;
+            if (e & mvk::ONLINE_JOB_MERGED) {  // a merge area: q holds the area
+              q = e & 0xffffffffull;
+              j = 0;
+              kind = 3;
+            } else {
+              q = e >> 8;
+              j = (uint32_t)(e & 0xffu);
+              kind = 1;
+            }
             break;
           }
           if (__hip_atomic_load(&dev->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
@@ -808,6 +892,10 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
         if (kind == 1 && j == 0)
           __hip_atomic_store(&ctl->trace[q % mvk::ONLINE_SLOTS][2], on_now(), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if (kind == 3)
+          for (uint32_t b = 0; b < dev->mcount[q]; b++)
+            __hip_atomic_store(&ctl->trace[dev->mq[q][b] % mvk::ONLINE_SLOTS][2], on_now(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
       }
       job[0] = kind;
       job[1] = (uint32_t)q;
@@ -820,6 +908,10 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
     const uint32_t j = __builtin_amdgcn_readfirstlane(job[3]);
     __syncthreads();  // job[] is rewritten by the next claim only after every wave read it
     if (kind == 2) return;
+    if (kind == 3) {
+      online_merged_job(A, (uint32_t)q);
+      continue;
+    }
     const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(q % mvk::ONLINE_SLOTS));
     const uint32_t n = __builtin_amdgcn_readfirstlane(dev->n[slot]);
     // the slot's HBM scratch (kernels.h layout): everything below is uniform address arithmetic

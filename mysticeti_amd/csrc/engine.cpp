@@ -1043,7 +1043,7 @@ struct OnlineSvc {
   uint8_t* in = nullptr;
   uint8_t* out = nullptr;
   void *ctl_d = nullptr, *req_d = nullptr, *in_d = nullptr, *out_d = nullptr;  // device views
-  DevBuf dctl, scr;
+  DevBuf dctl, scr, mscr;
   std::unique_ptr<std::atomic<uint64_t>[]> freed;  // slot released by its owner: request + 1
   // Waiting callers (round 5). At most max_spinners callers spin on their done word; the others
   // sleep on a futex word of their slot, which the reaper thread sets and wakes once the done
@@ -1166,6 +1166,7 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   HIPCHK(ctx, o.dctl.ensure(sizeof(mvk::OnlineDev)));
   HIPCHK(ctx, hipMemset(o.dctl.p, 0, sizeof(mvk::OnlineDev)));
   HIPCHK(ctx, o.scr.ensure(mvk::ONLINE_SCR_STRIDE * kOnSlots));
+  HIPCHK(ctx, o.mscr.ensure(mvk::ONLINE_SCR_STRIDE * kOnSlots));  // merge areas (MV_ONLINE_MERGE)
   o.freed.reset(new std::atomic<uint64_t>[kOnSlots]);
   o.dwake.reset(new std::atomic<uint32_t>[kOnSlots]);
   o.sleep_q.reset(new std::atomic<uint64_t>[kOnSlots]);
@@ -1270,6 +1271,8 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   a.in_host = static_cast<const uint8_t*>(o.in_d);
   a.out_host = static_cast<uint8_t*>(o.out_d);
   a.scr = o.scr.as<uint8_t>();
+  a.mscr = o.mscr.as<uint8_t>();
+  a.merge = ctx->kn.online_merge ? 1u : 0u;
   a.combB = dev.combB.p;
   a.combA = dev.combA.p;
   a.key_ok = dev.keyok.as<uint8_t>();
@@ -1380,6 +1383,7 @@ void online_release(OnlineSvc& o) {
     if (h) (void)hipHostFree(h);
   o.dctl.release();
   o.scr.release();
+  o.mscr.release();
   o.ready = false;
 }
 
@@ -1974,6 +1978,7 @@ const KnobDef kKnobs[] = {
     {"MV_ONLINE_DEBUG", &mvk::Knobs::online_debug, K_FLAG, false},
     {"MV_ONLINE_INJECT", &mvk::Knobs::online_inject, K_OFF, false},
     {"MV_ONLINE_SPINNERS", &mvk::Knobs::online_spinners, K_INT, false},
+    {"MV_ONLINE_MERGE", &mvk::Knobs::online_merge, K_OFF, false},
     {"MV_PIPELINE", &mvk::Knobs::pipeline, K_INT, false},
     {"MV_PIPE_CHUNK_LOG2", &mvk::Knobs::pipe_chunk_log2, K_INT, false},
     {"MV_PIPE_THREADS", &mvk::Knobs::pipe_threads, K_INT, false},

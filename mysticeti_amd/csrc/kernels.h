@@ -36,6 +36,7 @@ struct Knobs {
   int64_t online_trace = 0;              // MV_ONLINE_TRACE: per-stage means on stderr at release
   int64_t online_debug = 0;              // MV_ONLINE_DEBUG: launch lines, long waits on stderr
   int64_t online_inject = 0;             // MV_ONLINE_INJECT: fault injection (tests): launches fail
+  int64_t online_merge = 0;              // MV_ONLINE_MERGE: one-block requests share 4-signature jobs
   int64_t online_spinners = 0;           // MV_ONLINE_SPINNERS: callers spinning on their verdict (0: 1/4 of the CPU share)
   // signature path
   int64_t pipeline = 0;                  // MV_PIPELINE: pageable signature staging experiment
@@ -243,6 +244,11 @@ struct OnlineDev {
   uint32_t n[ONLINE_SLOTS];
   uint32_t jobs_done[ONLINE_SLOTS];
   unsigned long long moved[ONLINE_SLOTS];  // request + 1 last moved from each slot (the poller's)
+  // merged jobs (OnlineArgs::merge): up to four one-block requests verified by one job in merge
+  // area a (ONLINE_SCR_STRIDE of HBM each, mscr): their request numbers and count
+  unsigned long long mgroups;              // merge groups formed (the poller's)
+  unsigned long long mq[ONLINE_SLOTS][4];
+  uint32_t mcount[ONLINE_SLOTS];
   unsigned long long jobs[ONLINE_JOBS];  // (request << 8) | job
   uint64_t sink[2 * 1024];               // 16 B per poller thread: where its copy lanes past the end go
 };
@@ -262,7 +268,10 @@ struct OnlineArgs {
   uint32_t n_auth;
   uint32_t launch;                // launch number (the epoch handshake)
   uint64_t idle_ticks, max_ticks;
+  uint8_t* mscr;                  // HBM merge areas, ONLINE_SCR_STRIDE each (ONLINE_SLOTS of them)
+  uint32_t merge;                 // 1: one-block requests of a pass share 4-signature jobs
 };
+constexpr unsigned long long ONLINE_JOB_MERGED = 1ull << 62;  // job entry: merged, area in the low bits
 hipError_t launch_online(const OnlineArgs& a, uint32_t grid, hipStream_t s);
 hipError_t launch_verify_comb(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,

@@ -416,3 +416,29 @@ def test_context_with_online_service_is_destroyed_and_the_process_exits():
     for rep in range(3):
         p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=90)
         assert p.returncode == 0 and "destroyed" in p.stdout, (rep, p.returncode, p.stdout[-500:], p.stderr[-2000:])
+
+
+@pytest.mark.parametrize("kmax", [2, 5])
+def test_online_service_merged_jobs(engine, golden, opts, kmax):
+    """MV_ONLINE_MERGE: the poller packs the one-block requests of a pass four to a job (each
+    block read from its own request's slot, its verdict and digests routed back to that
+    request). 16 threads posting one block (kmax 2) or 1-4 blocks (kmax 5) at a time, and every
+    golden edge case one per call from 8 threads at once: the queue path's verdicts and digests."""
+    bins, pks, stakes = ragged_blocks(n_rounds=40, seed=17)
+    engine.set_committee(pks, stakes, 0)
+    opts("MV_ONLINE", 0)
+    st_ref, md_ref, bd_ref = engine.verify_blocks(bins)
+    opts("MV_ONLINE", 1)
+    opts("MV_ONLINE_MERGE", 1)
+    engine.set_committee(pks, stakes, 0)  # the next launch reads the switch
+    st, md, bd = _concurrent(engine, bins, kmax=kmax)
+    assert (st == st_ref).all() and (md == md_ref).all() and (bd == bd_ref).all()
+    fx = golden("block_edge.json")
+    epks = np.frombuffer(b"".join(bytes.fromhex(k) for k in fx["committee"]["pks"]), dtype=np.uint8).reshape(-1, 32)
+    engine.set_committee(epks, np.array(fx["committee"]["stakes"], dtype=np.uint64), fx["committee"]["epoch"])
+    ebins = [bytes.fromhex(c["bincode"]) for c in fx["cases"]] * 4
+    want = np.array([c["status"] for c in fx["cases"]] * 4, dtype=np.uint8)
+    est, _, _ = _concurrent(engine, ebins, threads=8, rounds=1, kmax=2)
+    assert (est == want).all(), np.nonzero(est != want)[0][:8]
+    opts("MV_ONLINE_MERGE", 0)
+    engine.set_committee(pks, stakes, 0)  # stops the merging launch
