@@ -586,6 +586,9 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // loop also tests the launch's end, so all waves leave.
 constexpr uint32_t ON_BATCH = 64;  // the poller's window (requests it can move per pass): one wave's lanes
 constexpr uint32_t ON_COPY_UNROLL = 8;  // 16-B input loads per poller thread in flight
+constexpr uint32_t ON_MHDR = 64;        // a merge area's off[4] | len[4] before its input region
+static_assert(ON_MHDR + 4 * (16 + mvk::INGEST_WINDOW_BYTES + 32) <= mvk::ONLINE_IN_STRIDE,
+              "four one-block inputs fit a merge area's input region");
 static_assert(IG_WIN == mvk::INGEST_WINDOW_BYTES, "the host's eligibility test uses the ingest window");
 static_assert(ON_BATCH <= mvk::ONLINE_SLOTS && ON_BATCH <= 64 && mvk::ONLINE_SLOTS % 64 == 0,
               "the window's lanes cover distinct slots, one wave");
@@ -598,10 +601,18 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   __shared__ uint32_t pre[ON_BATCH + 1];  // 16-B chunk prefix over the batch's inputs
   __shared__ uint32_t nblk[ON_BATCH];
   __shared__ uint32_t qoff[ON_BATCH];     // request - ready of each moved request
+  __shared__ uint64_t dstp[ON_BATCH];     // where its input goes: its slot's scratch or a merge area
+  __shared__ uint32_t marea[ON_BATCH];    // merged: its area (else ~0u) and its input's byte offset
+  __shared__ uint32_t mbyte[ON_BATCH];    // in the area's input region
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
   uint64_t t_busy = t_start;
   uint64_t why = 0;  // wave 0: why the launch ends (mvk::ONLINE_EXIT_*)
+  // thread 0: merge groups formed by this launch (the area of the next one); a register, not
+  // memory: a store does not refresh this CU's L1 copy of the line, so a counter kept in HBM and
+  // read back through L1 repeated areas still in use (and lost their requests). Per launch is
+  // enough: every area of an earlier launch is finished when a launch starts.
+  uint64_t groups = 0;
   if (t == 0) {  // this launch's setup: tickets of earlier launches are void
     const unsigned long long tl = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&dev->jobs_head, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -694,11 +705,29 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       continue;
     }
     if (t == 0) {
-      uint32_t c = 0;
+      // chunk prefix; and the merge groups (A.merge): the pass's one-block requests four to an
+      // area, each request's input copied into the area's input region (a merged job's ingest
+      // then reads and stages its blocks inside the area, as a request's does inside its slot)
+      uint32_t c = 0, gcnt = 0, garea = 0, gbytes = 0;
       for (uint32_t i = 0; i < cnt; i++) {
         const uint32_t k = pre[i];
         pre[i] = c;
         c += k;
+        const uint32_t slot = (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS);
+        if (A.merge && nblk[i] == 1) {
+          if (gcnt == 0) {
+            garea = (uint32_t)(groups++ % mvk::ONLINE_SLOTS);
+            gbytes = 0;
+          }
+          marea[i] = garea;
+          mbyte[i] = gbytes;
+          dstp[i] = (uint64_t)(A.mscr + mvk::ONLINE_SCR_STRIDE * garea + ON_MHDR + gbytes);
+          gbytes += 16 * k;
+          if (++gcnt == C16_SIGS) gcnt = 0;
+        } else {
+          marea[i] = ~0u;
+          dstp[i] = (uint64_t)(A.scr + mvk::ONLINE_SCR_STRIDE * slot);
+        }
       }
       pre[cnt] = c;
     }
@@ -715,8 +744,7 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
         uint32_t i = 0;
         while (pre[i + 1] <= t) i++;
         const uint32_t slot = (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS), c = t - pre[i];
-        reinterpret_cast<uint4*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot)[c] =
-            reinterpret_cast<const uint4*>(A.in_host + mvk::ONLINE_IN_STRIDE * slot)[c];
+        reinterpret_cast<uint4*>(dstp[i])[c] = reinterpret_cast<const uint4*>(A.in_host + mvk::ONLINE_IN_STRIDE * slot)[c];
       }
     } else for (uint32_t k0 = 0; k0 < total; k0 += blockDim.x * ON_COPY_UNROLL) {
       uint64_t src[ON_COPY_UNROLL], dst[ON_COPY_UNROLL];
@@ -730,7 +758,7 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
         const uint32_t slot = (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS), c = k - pre[i];
         const uint64_t sink = (uint64_t)(dev->sink + 2 * t);
         src[u] = live ? (uint64_t)(A.in_host + mvk::ONLINE_IN_STRIDE * slot + 16 * (size_t)c) : sink;
-        dst[u] = live ? (uint64_t)(A.scr + mvk::ONLINE_SCR_STRIDE * slot + 16 * (size_t)c) : sink;
+        dst[u] = live ? dstp[i] + 16 * (uint64_t)c : sink;
       }
       uint64_t lo[ON_COPY_UNROLL], hi[ON_COPY_UNROLL];
 #pragma unroll
@@ -746,9 +774,8 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
     __syncthreads();
     if (t == 0) {
       unsigned long long jt = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // merge (A.merge): the pass's one-block requests go four to a job in a merge area; the
-      // area's off / len point at each block's bincode in its own slot's scratch (offsets from
-      // A.scr), so nothing is copied
+      // merge groups (formed above, in the same order): each area's off / len (the header) and
+      // its requests, then one job per area
       uint32_t gcnt = 0, garea = 0;
       auto close_group = [&]() {
         dev->mcount[garea] = gcnt;
@@ -763,16 +790,17 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
         __hip_atomic_store(&dev->moved[slot], (unsigned long long)(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (nj == 0) {  // a void request: complete it here
           __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else if (A.merge && nblk[i] == 1) {
-          if (gcnt == 0) garea = (uint32_t)(dev->mgroups++ % mvk::ONLINE_SLOTS);
-          // (the slot's off[0] / len[0], just copied by the other threads: read past this CU's L1,
-          // which may hold the slot's previous request)
-          uint64_t* so = reinterpret_cast<uint64_t*>(A.scr + mvk::ONLINE_SCR_STRIDE * slot);
-          const uint64_t o0 = __hip_atomic_load(so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t l0 = __hip_atomic_load(so + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          uint64_t* ao = reinterpret_cast<uint64_t*>(A.mscr + mvk::ONLINE_SCR_STRIDE * garea);
-          ao[gcnt] = mvk::ONLINE_SCR_STRIDE * slot + 16 + o0;  // the block's bincode, from A.scr
-          ao[4 + gcnt] = l0;                                    // its length
+        } else if (marea[i] != ~0u) {
+          garea = marea[i];
+          // the request's off[0] / len[0], just copied into the area by the other threads (read
+          // past this CU's L1, which may hold the area's previous contents)
+          uint8_t* area = A.mscr + mvk::ONLINE_SCR_STRIDE * garea;
+          uint64_t* hdr = reinterpret_cast<uint64_t*>(area + ON_MHDR + mbyte[i]);
+          const uint64_t o0 = __hip_atomic_load(hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t l0 = __hip_atomic_load(hdr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint64_t* ao = reinterpret_cast<uint64_t*>(area);
+          ao[gcnt] = mbyte[i] + 16 + o0;  // the block's bincode, from the input region (area + ON_MHDR)
+          ao[4 + gcnt] = l0;              // its length
           dev->mq[garea][gcnt] = q;
           if (++gcnt == C16_SIGS) close_group();
         } else {
@@ -790,10 +818,11 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   }
 }
 
-// A merged job (OnlineArgs::merge): up to four one-block requests in merge area `area`, whose
-// off / len point at each block's bincode in its own slot's scratch (offsets from A.scr); the
-// pre-images, digests and verdicts go to the area; then each block's outputs to its request's
-// page-locked slot (index 0) and, after one system-scope fence, each request's done word.
+// A merged job (OnlineArgs::merge): up to four one-block requests in merge area `area`: the
+// poller copied their inputs into the area's input region (area + ON_MHDR) and wrote the blocks'
+// off / len there (its header); the pre-images, digests and verdicts go to the area; then each
+// block's outputs to its request's page-locked slot (index 0) and, after one system-scope
+// fence, each request's done word.
 MV_DEV void online_merged_job(const mvk::OnlineArgs& A, uint32_t area) {
   mvk::OnlineCtl* ctl = A.ctl;
   mvk::OnlineDev* dev = A.dev;
@@ -814,7 +843,9 @@ MV_DEV void online_merged_job(const mvk::OnlineArgs& A, uint32_t area) {
   uint8_t* claimed = sc + mvk::ONLINE_O_CLAIMED;
   const mvk::BlockVerdictOut bv{facts, claimed, md, bd, st};
   const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
-  const mvk::BlockIngestIn ing{A.scr, off, off + 4, A.stakes, A.n_auth, A.epoch, A.quorum_thr,
+  // the blocks' bincode sits in the area's input region (area + ON_MHDR), so their staged
+  // pre-images (at the same offsets in `stage`) stay inside the area
+  const mvk::BlockIngestIn ing{sc + ON_MHDR, off, off + 4, A.stakes, A.n_auth, A.epoch, A.quorum_thr,
                                stage, poff, plen, sig, kidx, facts, claimed};
   comb16_wg(0, md, sig, A.pk, kidx, n, (const uint4*)A.combB, (const uint4*)A.combA, A.key_ok,
             sc + mvk::ONLINE_O_SST, bv, hin, ing, nullptr);

@@ -246,7 +246,6 @@ struct OnlineDev {
   unsigned long long moved[ONLINE_SLOTS];  // request + 1 last moved from each slot (the poller's)
   // merged jobs (OnlineArgs::merge): up to four one-block requests verified by one job in merge
   // area a (ONLINE_SCR_STRIDE of HBM each, mscr): their request numbers and count
-  unsigned long long mgroups;              // merge groups formed (the poller's)
   unsigned long long mq[ONLINE_SLOTS][4];
   uint32_t mcount[ONLINE_SLOTS];
   unsigned long long jobs[ONLINE_JOBS];  // (request << 8) | job
