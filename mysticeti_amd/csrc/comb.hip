@@ -638,19 +638,18 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       const uint64_t q = rdy + t;
       const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
       if (t < ON_BATCH) {
-        // the descriptor (seq | n | copy_bytes: 16 bytes of one line) in ONE read, issued beside the
-        // HBM read of moved[]: the host writes n and copy_bytes before seq, and x86 stores become
-        // visible in order, so a read of the line that sees seq sees them (round 4 read n and
-        // copy_bytes after seq: a second PCIe round trip per pass)
+        // moved[] (HBM) and seq (PCIe) read side by side; n and copy_bytes after seq. (Reading the
+        // 16-byte descriptor in one nontemporal load instead served requests only after the
+        // launch's idle exit, ~10 ms: that load is not system-coherent; profiles/r05/c5_desc_ab.txt)
         const unsigned long long mvq = __hip_atomic_load(&dev->moved[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(A.reqs + slot));
+        const mvk::OnlineReq* r = A.reqs + slot;
+        const uint64_t sq = __hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         moved = mvq == q + 1;
-        fresh = !moved && ((uint64_t)d[0] | ((uint64_t)d[1] << 32)) == q + 1;
+        fresh = !moved && sq == q + 1;
         if (fresh) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the slot's input bytes after seq
-          nb = d[2];
-          cb = d[3];
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the slot's bytes after seq
+          nb = r->n;
+          cb = r->copy_bytes;
         }
       }
       const uint64_t fm = __ballot(fresh);
