@@ -34,6 +34,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "fe25519.h"
 #include "ge25519.h"
 #include "hash_dev.h"
@@ -625,6 +627,108 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* _
   p3_store(segT, sidx, T);
 }
 
+// Balanced buckets (seg = 1, MV_BUCKET_BAL): one lane per bucket leaves a wave as slow as its
+// fullest bucket — bucket sizes are Poisson (mean 32-128 by window), and the wave's max of 64
+// kept lanes busy ~75% of the time (SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU),
+// profiles/r05/pmc/pmc_c2_k_bv_bucket.txt). Here every lane adds the same number L of entries:
+// lane j takes entries [j L, (j + 1) L) of the whole key-sorted list (all groups and windows:
+// ents is sorted by key = g * BV_NKG + w * BV_NB + |d| - 1). A bucket that starts in the lane's
+// range is written to segT by it (complete, or its first piece); the piece of a bucket that
+// began before the range goes to carry[j], which k_bv_bucket_fix adds to segT. Empty buckets
+// are written (identity) by k_bv_bucket_fix too.
+// offs_key(x): the largest key k in [k0, nk) with offs[k] <= x (offs nondecreasing, offs[k0] <= x)
+MV_DEV uint32_t bv_key_of(const uint32_t* __restrict__ offs, uint32_t k0, uint32_t nk, uint32_t x) {
+  uint32_t lo = k0, hi = nk;  // offs[lo] <= x, answer in [lo, hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint4* __restrict__ pts,
+                                                                     const uint32_t* __restrict__ offs,
+                                                                     const uint32_t* __restrict__ ents, uint32_t nk,
+                                                                     uint32_t nlanes, uint4* __restrict__ carry,
+                                                                     uint4* __restrict__ segT) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nlanes) return;
+  const uint32_t e0 = offs[0], e1 = offs[nk];
+  const uint32_t L = (e1 - e0 + nlanes - 1) / nlanes;
+  const uint32_t lo = min(e0 + j * L, e1), hi = min(lo + L, e1);
+  if (lo >= hi) return;
+  uint32_t b = bv_key_of(offs, 0, nk, lo);  // the bucket holding entry lo (non-empty)
+  uint32_t nb = offs[b + 1];                // its end
+  bool head = offs[b] < lo;                 // began before this lane: the piece is a carry
+  p3 T;
+  p3_identity(T);
+  uint4 q[7];
+  uint32_t ent = ents[lo];
+  {
+    const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+#pragma unroll
+    for (int i = 0; i < 7; i++) q[i] = p[i];
+  }
+  for (uint32_t x = lo; x < hi; x++) {
+    precomp pc;
+    quads_to_precomp(pc, q);
+    const bool neg = ent & 1u;
+    if (x + 1 < hi) {  // next point in flight during this add
+      ent = ents[x + 1];
+      const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+#pragma unroll
+      for (int i = 0; i < 7; i++) q[i] = p[i];
+    }
+    precomp_cneg(pc, neg);
+    p1p1 t;
+    p3_add_precomp(t, T, pc);
+    p1p1_to_p3(T, t);
+    if (x + 1 == nb) {  // bucket b complete (in this lane)
+      if (head) p3_store(carry, j, T); else p3_store(segT, b, T);
+      head = false;
+      p3_identity(T);
+      if (x + 1 < hi) {  // the next non-empty bucket: usually b + 1, else search (empty runs)
+        const uint32_t n2 = offs[b + 2];
+        if (n2 > nb) { b++; nb = n2; }
+        else { b = bv_key_of(offs, b + 1, nk, x + 1); nb = offs[b + 1]; }
+      }
+    }
+  }
+  if (hi != nb) {  // the range ends inside bucket b
+    if (head) p3_store(carry, j, T); else p3_store(segT, b, T);
+  }
+}
+
+// One lane per bucket key (g, w < nw, |d| - 1): empty -> identity; a bucket whose entries run
+// past the lane that began it gets the carries of the lanes it continues into.
+__global__ void __launch_bounds__(256) k_bv_bucket_fix(const uint32_t* __restrict__ offs, uint32_t nk,
+                                                       uint32_t ngroups, uint32_t nw, uint32_t nlanes,
+                                                       const uint4* __restrict__ carry, uint4* __restrict__ segT) {
+  const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lin >= ngroups * nw * BV_NB) return;
+  const uint32_t g = lin / (nw * BV_NB), r = lin % (nw * BV_NB);
+  const uint32_t key = g * BV_NKG + r;  // (w, |d| - 1) = (r / NB, r % NB), w < nw
+  const uint32_t e0 = offs[0], e1 = offs[nk];
+  const uint32_t L = (e1 - e0 + nlanes - 1) / nlanes;
+  const uint32_t lo = offs[key], hi = offs[key + 1];
+  if (lo == hi) {
+    p3 I;
+    p3_identity(I);
+    p3_store(segT, key, I);
+    return;
+  }
+  const uint32_t j0 = (lo - e0) / L, j1 = (hi - 1 - e0) / L;
+  if (j1 == j0) return;
+  p3 T;
+  p3_load(T, segT, key);
+  for (uint32_t j = j0 + 1; j <= j1; j++) {
+    p3 C;
+    p3_load(C, carry, j);
+    p3_acc(T, C);
+  }
+  p3_store(segT, key, T);
+}
+
 // ---------------------------------------------------------------- reduction
 // Rows = (group, window); row r holds cnt_in elements. Elements (V, T) with indices
 // m = 0..cnt-1 stand for V + (m * scale) T. Groups of FAN consecutive elements m = FAN*q + t
@@ -979,7 +1083,8 @@ struct BatchLayout {
     tmp = take((size_t)(BV_NWR + BV_NW) * n * 8);
     offs = take(((size_t)groups * BV_NKG + 1) * 4);
     ents = take((size_t)(BV_NWR + BV_NW) * n * 4);
-    segV = take((size_t)groups * BV_NKG / 2 * P3_QUADS * 16);  // segments of >= 2 buckets only
+    // segments of >= 2 buckets, or the balanced bucket kernel's carries (one per lane)
+    segV = take((size_t)groups * BV_NKG / 2 * P3_QUADS * 16);
     segT = take((size_t)groups * BV_NKG * P3_QUADS * 16);
     const size_t lv = (size_t)groups * (BV_NKG / BV_FAN) * P3_QUADS * 16;
     rV0 = take(lv); rT0 = take(lv); rV1 = take(lv); rT1 = take(lv);
@@ -1024,7 +1129,7 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
                                uint32_t n, uint32_t groups, const uint32_t key[10], const void* btab,
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev, const void* comb_a, const uint8_t* key_ok,
-                               uint32_t n_keys, const void* comb_b, const ChunkGate* gate) {
+                               uint32_t n_keys, const void* comb_b, const ChunkGate* gate, const hipEvent_t* chain) {
   using namespace mv;
   // optional stage events (engine stage timing): ev[0] before prep, ev[i + 1] after stage i
   auto mark = [&](int i) { if (ev) (void)hipEventRecord(ev[i], s); };
@@ -1129,8 +1234,10 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
       if ((e = hipStreamWaitEvent(s, gate->join, 0)) != hipSuccess) return e;
     }
   } else {
+    if (chain && chain[0] && (e = hipStreamWaitEvent(s, chain[0], 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_bv_prep, dim3(nblk), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca, pts, scal, bsum,
                        status, 0u, G.cpg * PART_CHUNK);
+    if (chain && (e = hipEventRecord(chain[1], s)) != hipSuccess) return e;
   }
   if (!msm) {
     mark(1);
@@ -1145,8 +1252,20 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
     // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
     // through memory and the reduction stays the size of one group's
-    hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
-                       G.count, seg, nw, 0u, segV, segT);
+    const uint32_t nk = G.count * BV_NKG;
+    if (seg == 1 && kn.bucket_bal > 0) {
+      // equal entries per lane (the carries in segV: at most one per lane)
+      const uint64_t per = kn.bucket_bal > 1 ? (uint64_t)kn.bucket_bal : 64u;
+      const uint64_t est = (uint64_t)n * (nw + BV_NWR);  // entries: at most one per window of z and of z k
+      const uint32_t cap = nk / 2;
+      uint32_t nl = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(256, (est / per + 255) / 256 * 256));
+      hipLaunchKernelGGL(k_bv_bucket_bal, dim3(nl / 256), dim3(256), 0, s, pts, offs, ents, nk, nl, segV, segT);
+      hipLaunchKernelGGL(k_bv_bucket_fix, dim3(G.count * nw * BV_NB / 256), dim3(256), 0, s, offs, nk, G.count, nw, nl,
+                         segV, segT);
+    } else {
+      hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
+                         G.count, seg, nw, 0u, segV, segT);
+    }
   }
   if (agg) {
     hipLaunchKernelGGL(k_bv_keyacc, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, key_idx, n, n_keys, kpart);

@@ -142,6 +142,10 @@ struct Device {
   // the streaming MSM's per-chunk preparation events (aux -> compute stream) and fork / join
   hipEvent_t prep_ev[kMaxChunks] = {};
   hipEvent_t msm_fork = nullptr, msm_join = nullptr;
+  // the batch path's preparation chain (MV_PREP_CHAIN): recorded after each batch's k_bv_prep;
+  // the next batch's k_bv_prep waits for it (prep_chained: recorded at least once)
+  hipEvent_t prep_chain = nullptr;
+  bool prep_chained = false;
   DevBuf btab, combB, scratch, msg, sig, pk, keyidx, status, bytes, off, len, out2;
   // committee: key encodings, stakes, per-key comb tables C_A, per-key decode flags
   DevBuf committee_pk, stakes, combA, keyok;
@@ -443,10 +447,19 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   // committee keys: A comes from the comb tables built at mv_set_committee (no per-signature decode)
   const bool com_a = d_key_idx && dev.committee_loaded && d_pk == dev.committee_pk.as<uint8_t>() &&
                      !(ctx->flags & MV_FLAG_NO_COMB);
+  hipEvent_t chain[2] = {};
+  const bool chained = ctx->kn.prep_chain && !(gate && gate->n);
+  if (chained) {
+    if (!dev.prep_chain) HIPCHK(ctx, hipEventCreateWithFlags(&dev.prep_chain, hipEventDisableTiming));
+    chain[0] = dev.prep_chained ? dev.prep_chain : nullptr;
+    chain[1] = dev.prep_chain;
+  }
   HIPCHK(ctx, mvk::launch_verify_batch(ctx->kn, d_msg, d_sig, d_pk, d_key_idx, n, groups, key, dev.btab.p, dev.bscr[slot].p,
                                        dev.vscr[slot].p, d_status, s, &flag, evs.empty() ? nullptr : evs.data(),
                                        com_a ? dev.combA.p : nullptr, com_a ? dev.keyok.as<uint8_t>() : nullptr,
-                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p, gate));
+                                       com_a ? (uint32_t)ctx->committee.size() : 0u, dev.combB.p, gate,
+                                       chained ? chain : nullptr));
+  if (chained) dev.prep_chained = true;
   keep_events(ctx, dev.id, 0, evs);
   if (flag_dst) HIPCHK(ctx, hipMemcpyAsync(flag_dst, flag, 4, hipMemcpyDeviceToDevice, s));
   const uint32_t ng = (n + mvk::batch_group_size(n, groups) - 1) / mvk::batch_group_size(n, groups);
@@ -1996,6 +2009,8 @@ const KnobDef kKnobs[] = {
     {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
     {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_OFF, false},
+    {"MV_PREP_CHAIN", &mvk::Knobs::prep_chain, K_ON, false},
+    {"MV_BUCKET_BAL", &mvk::Knobs::bucket_bal, K_INT, false},
 };
 
 const KnobDef* find_knob(const char* name) {
@@ -2273,7 +2288,7 @@ void mv_destroy(mv_ctx* ctx) {
     }
     for (hipEvent_t ev : dev.prep_ev)
       if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : {dev.msm_fork, dev.msm_join}) {
+    for (hipEvent_t ev : {dev.msm_fork, dev.msm_join, dev.prep_chain}) {
       if (ev) (void)hipEventDestroy(ev);
     }
     for (int k = 0; k < 2; k++) {

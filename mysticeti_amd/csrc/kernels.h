@@ -60,6 +60,8 @@ struct Knobs {
   int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
   int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
   int64_t stream_msm = 0;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM (measured slower)
+  int64_t bucket_bal = 1;                // MV_BUCKET_BAL: equal entries per bucket-kernel lane (>1: entries per lane)
+  int64_t prep_chain = 1;                // MV_PREP_CHAIN: a batch's k_bv_prep starts after the previous batch's
 };
 
 size_t verify_scratch_bytes(uint32_t n);
@@ -120,7 +122,11 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
                                void* bscratch, void* vscratch, uint8_t* status, hipStream_t s,
                                uint32_t** flag_out, hipEvent_t* ev = nullptr, const void* comb_a = nullptr,
                                const uint8_t* key_ok = nullptr, uint32_t n_keys = 0, const void* comb_b = nullptr,
-                               const struct ChunkGate* gate = nullptr);
+                               const struct ChunkGate* gate = nullptr, const hipEvent_t* chain = nullptr);
+// chain (optional, unchunked calls): k_bv_prep waits for chain[0] (may be null) and chain[1]
+// is recorded after it, so consecutive batches on different streams run their preparations
+// one after another and each overlaps the previous batches' narrow tails (sort, reduce, final)
+// instead of all starting together and leaving the tails to run side by side.
 // gate (optional): the inputs arrive in chunks (H2D copies on another stream). Chunk c =
 // signatures [end[c - 1], end[c]) (ends multiples of 256 except the last = n); k_bv_prep runs
 // chunk by chunk, each launch after hipStreamWaitEvent on ready[c], alternating between s and
