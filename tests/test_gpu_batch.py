@@ -314,3 +314,25 @@ def test_streamed_pinned_inputs_many_batches(committee, zerocopy):
             assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
         st2 = eng.ed25519_verify(msg, sig, key_idx=ki) if committee else eng.ed25519_verify(msg, sig, pk)
         assert (st2 == st).all()
+
+
+@pytest.mark.parametrize("bal", [0, 1, 7, 200])
+@pytest.mark.parametrize("groups", [0, 5])
+def test_bucket_forms_agree(engine, opts, bal, groups):
+    """Both bucket kernels (one lane per bucket: MV_BUCKET_BAL=0; equal entries per lane: 1 =
+    64 per lane, or 7 / 200 entries so that lanes split buckets many ways or hold many
+    buckets) give equations that hold on valid batches and fail exactly where a signature is
+    bad, with and without sub-batch equations."""
+    opts("MV_BUCKET_BAL", bal)
+    n = 9000
+    msg, sig, pk = signed(engine, n, 77)
+    engine.set_batch_groups(groups)
+    try:
+        st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+        assert (st == 0).all() and nb == 1 and nf == 0
+        s2 = sig.copy()
+        s2[[3, 4444, n - 1], 40] ^= 0x10
+        st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, s2, pk))
+        assert (st == O.verify_batch(pk, s2, msg)).all() and nb == 1 and nf == 1
+    finally:
+        engine.set_batch_groups(0)
