@@ -649,8 +649,8 @@ MV_DEV uint32_t bv_key_of(const uint32_t* __restrict__ offs, uint32_t k0, uint32
 __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint4* __restrict__ pts,
                                                                      const uint32_t* __restrict__ offs,
                                                                      const uint32_t* __restrict__ ents, uint32_t nk,
-                                                                     uint32_t nlanes, uint4* __restrict__ carry,
-                                                                     uint4* __restrict__ segT) {
+                                                                     uint32_t nlanes, uint32_t acc,
+                                                                     uint4* __restrict__ carry, uint4* segT) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nlanes) return;
   const uint32_t e0 = offs[0], e1 = offs[nk];
@@ -660,6 +660,19 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
   uint32_t b = bv_key_of(offs, 0, nk, lo);  // the bucket holding entry lo (non-empty)
   uint32_t nb = offs[b + 1];                // its end
   bool head = offs[b] < lo;                 // began before this lane: the piece is a carry
+  // a piece: the carry, or the bucket's sum (acc: added to the sum of the earlier segments)
+  auto emit = [&](uint32_t key, p3& P) {
+    if (head) {
+      p3_store(carry, j, P);
+    } else {
+      if (acc) {
+        p3 O;
+        p3_load(O, segT, key);
+        p3_acc(P, O);
+      }
+      p3_store(segT, key, P);
+    }
+  };
   p3 T;
   p3_identity(T);
   uint4 q[7];
@@ -684,7 +697,7 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
     p3_add_precomp(t, T, pc);
     p1p1_to_p3(T, t);
     if (x + 1 == nb) {  // bucket b complete (in this lane)
-      if (head) p3_store(carry, j, T); else p3_store(segT, b, T);
+      emit(b, T);
       head = false;
       p3_identity(T);
       if (x + 1 < hi) {  // the next non-empty bucket: usually b + 1, else search (empty runs)
@@ -694,15 +707,15 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
       }
     }
   }
-  if (hi != nb) {  // the range ends inside bucket b
-    if (head) p3_store(carry, j, T); else p3_store(segT, b, T);
-  }
+  if (hi != nb) emit(b, T);  // the range ends inside bucket b
 }
 
 // One lane per bucket key (g, w < nw, |d| - 1): empty -> identity; a bucket whose entries run
-// past the lane that began it gets the carries of the lanes it continues into.
+// past the lane that began it gets the carries of the lanes it continues into. acc (streaming
+// MSM segments after the first): the buckets hold the earlier segments' sums, and an empty one
+// keeps its sum.
 __global__ void __launch_bounds__(256) k_bv_bucket_fix(const uint32_t* __restrict__ offs, uint32_t nk,
-                                                       uint32_t ngroups, uint32_t nw, uint32_t nlanes,
+                                                       uint32_t ngroups, uint32_t nw, uint32_t nlanes, uint32_t acc,
                                                        const uint4* __restrict__ carry, uint4* __restrict__ segT) {
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
   if (lin >= ngroups * nw * BV_NB) return;
@@ -711,10 +724,12 @@ __global__ void __launch_bounds__(256) k_bv_bucket_fix(const uint32_t* __restric
   const uint32_t e0 = offs[0], e1 = offs[nk];
   const uint32_t L = (e1 - e0 + nlanes - 1) / nlanes;
   const uint32_t lo = offs[key], hi = offs[key + 1];
-  if (lo == hi) {
-    p3 I;
-    p3_identity(I);
-    p3_store(segT, key, I);
+  if (lo == hi) {  // (acc: the earlier segments' sum stays)
+    if (!acc) {
+      p3 I;
+      p3_identity(I);
+      p3_store(segT, key, I);
+    }
     return;
   }
   const uint32_t j0 = (lo - e0) / L, j1 = (hi - 1 - e0) / L;
@@ -1173,10 +1188,31 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
   if (e != hipSuccess) return e;
   const uint32_t seg = bucket_segment(kn);
   const bool msm = gate && gate->n && gate->msm && gate->prep_done && G.count == 1 && seg == 1;
+  const uint32_t nk = G.count * BV_NKG;
+  // bucket sums of the sorted entries of m signatures (acc: added to the sums in segT)
+  auto buckets = [&](uint64_t m, uint32_t acc) {
+    if (seg == 1 && kn.bucket_bal > 0) {
+      // equal entries per lane (the carries in segV: at most one per lane): 64 per lane, but at
+      // least 3 waves per SIMD (196,608 lanes) while lanes keep >= 8 entries, so a small batch or
+      // segment still fills the chip instead of running a few long lanes
+      const uint64_t est = m * (nw + BV_NWR);  // entries: at most one per window of z and of z k
+      uint64_t want = kn.bucket_bal > 1 ? est / (uint64_t)kn.bucket_bal
+                                        : std::max<uint64_t>(est / 64, std::min<uint64_t>(est / 8, 196608));
+      const uint32_t cap = nk / 2;
+      uint32_t nl = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(256, (want + 255) / 256 * 256));
+      hipLaunchKernelGGL(k_bv_bucket_bal, dim3(nl / 256), dim3(256), 0, s, pts, offs, ents, nk, nl, acc, segV, segT);
+      hipLaunchKernelGGL(k_bv_bucket_fix, dim3(G.count * nw * BV_NB / 256), dim3(256), 0, s, offs, nk, G.count, nw, nl,
+                         acc, segV, segT);
+    } else {
+      hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
+                         G.count, seg, nw, acc, segV, segT);
+    }
+  };
   if (msm) {
-    // streaming MSM: chunk c's preparation on aux (after its copy), then on s its bucket
-    // entries sorted (the partition sort over the chunk's signatures alone) and added into the
-    // persistent bucket sums segT; the reduction and the final follow the last chunk
+    // streaming MSM: chunk c's preparation on aux (after its copy); once a segment's chunks are
+    // prepared, on s its bucket entries are sorted (the partition sort over the segment's
+    // signatures alone) and added into the persistent bucket sums segT; the reduction and the
+    // final follow the last segment
     const uint32_t* end = gate->end;
     if (end[gate->n - 1] != n) return hipErrorInvalidValue;
     hipStream_t ps = gate->aux ? gate->aux : s;
@@ -1184,29 +1220,36 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
       if ((e = hipEventRecord(gate->fork, s)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(gate->aux, gate->fork, 0)) != hipSuccess) return e;
     }
+    // segments (gate->seg_end, ascending, the last = n; none: every chunk is one): the entries of
+    // a segment's signatures are sorted and added into the buckets once its last chunk is prepared
+    uint32_t sg = 0, seg_lo = 0;
     for (uint32_t c = 0, lo = 0; c < gate->n; lo = end[c++]) {
       const uint32_t hi = end[c], nc = hi - lo;
       if (hi <= lo || lo % PART_CHUNK) return hipErrorInvalidValue;
       if ((e = hipStreamWaitEvent(ps, gate->ready[c], 0)) != hipSuccess) return e;
       hipLaunchKernelGGL(k_bv_prep, dim3((nc + 255) / 256), dim3(256), 0, ps, msg, sig, pk, key_idx, n, k, ca,
                          pts, scal, bsum, status, lo / 256, G.cpg * PART_CHUNK);
+      while (gate->n_seg && sg + 1 < gate->n_seg && gate->seg_end[sg] <= lo) sg++;
+      const bool seg_done = !gate->n_seg || hi == n || hi >= gate->seg_end[sg];
+      if (!seg_done) continue;
       if (gate->aux) {
         if ((e = hipEventRecord(gate->prep_done[c], ps)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(s, gate->prep_done[c], 0)) != hipSuccess) return e;
       }
-      const uint32_t c0 = lo / PART_CHUNK, ncc = (nc + PART_CHUNK - 1) / PART_CHUNK;
+      const uint32_t m = hi - seg_lo;
+      const uint32_t c0 = seg_lo / PART_CHUNK, ncc = (m + PART_CHUNK - 1) / PART_CHUNK;
       const BvGroups Gc{1, ncc};
-      const uint4* sc = scal + (size_t)lo * SC_QUADS;
-      hipLaunchKernelGGL(k_part_count, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, nc, agg ? 1u : 0u,
+      const uint4* sc = scal + (size_t)seg_lo * SC_QUADS;
+      hipLaunchKernelGGL(k_part_count, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, agg ? 1u : 0u,
                          pcount + (size_t)c0 * BV_NPG);
       hipLaunchKernelGGL(k_part_scan, dim3(BV_NPG / 64), dim3(64 * SCAN_SUB), 0, s, pcount + (size_t)c0 * BV_NPG, ncc,
                          Gc, poff + (size_t)c0 * BV_NPG, ptot);
       hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, (uint32_t)BV_NPG, pstart);
-      hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, nc, poff + (size_t)c0 * BV_NPG, pstart,
-                         Gc, agg ? 1u : 0u, n, lo, tmp);
+      hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, poff + (size_t)c0 * BV_NPG, pstart,
+                         Gc, agg ? 1u : 0u, n, seg_lo, tmp);
       hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
-      hipLaunchKernelGGL(k_bv_bucket, dim3(nw * BV_NB / 256), dim3(256), 0, s, pts, offs, ents, 1u, 1u, nw,
-                         c ? 1u : 0u, segV, segT);
+      buckets(m, seg_lo ? 1u : 0u);
+      seg_lo = hi;
     }
     if (gate->aux) {  // (s has waited for every chunk's preparation)
       if ((e = hipEventRecord(gate->join, gate->aux)) != hipSuccess) return e;
@@ -1252,20 +1295,7 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
     // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
     // through memory and the reduction stays the size of one group's
-    const uint32_t nk = G.count * BV_NKG;
-    if (seg == 1 && kn.bucket_bal > 0) {
-      // equal entries per lane (the carries in segV: at most one per lane)
-      const uint64_t per = kn.bucket_bal > 1 ? (uint64_t)kn.bucket_bal : 64u;
-      const uint64_t est = (uint64_t)n * (nw + BV_NWR);  // entries: at most one per window of z and of z k
-      const uint32_t cap = nk / 2;
-      uint32_t nl = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(256, (est / per + 255) / 256 * 256));
-      hipLaunchKernelGGL(k_bv_bucket_bal, dim3(nl / 256), dim3(256), 0, s, pts, offs, ents, nk, nl, segV, segT);
-      hipLaunchKernelGGL(k_bv_bucket_fix, dim3(G.count * nw * BV_NB / 256), dim3(256), 0, s, offs, nk, G.count, nw, nl,
-                         segV, segT);
-    } else {
-      hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
-                         G.count, seg, nw, 0u, segV, segT);
-    }
+    buckets(n, 0u);
   }
   if (agg) {
     hipLaunchKernelGGL(k_bv_keyacc, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, key_idx, n, n_keys, kpart);

@@ -1863,18 +1863,29 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   for (uint32_t z : sizes) cap = std::max(cap, z);
   uint32_t chunk = 1u << chunk_log2;
   while ((cap + chunk - 1) / chunk > (uint32_t)Device::kMaxChunks / 2) chunk <<= 1;
-  // chunk schedule: the first batch starts with small chunks (2^14, 2^15, ... signatures), so
-  // the chip starts preparing after ~40 us of copying instead of a whole chunk's
-  std::vector<uint32_t> sched[2];
-  for (int b = 0; b < 2; b++) {
-    uint32_t o = 0, c = b == 0 ? std::min<uint32_t>(chunk, 1u << 14) : chunk;
-    while (o < cap) {
-      sched[b].push_back(o);
+  // chunk schedule of a batch of k: the first batch starts with small chunks (2^14, 2^15, ...
+  // signatures), so the chip starts preparing after ~40 us of copying instead of a whole chunk's.
+  // MV_STREAM_TAIL: the last chunk halved down to 2^14 signatures (2^16, 2^15, 2^14, 2^14 of a
+  // 2^17 chunk), so the preparation that follows the last copy is a short one
+  auto schedule = [&](int first, uint32_t k) {
+    std::vector<uint32_t> cut;
+    uint32_t o = 0, c = first ? std::min<uint32_t>(chunk, 1u << 14) : chunk;
+    while (o < k) {
+      cut.push_back(o);
       o += c;
       if (c < chunk) c *= 2;
     }
-    sched[b].push_back(cap);
-  }
+    if (ctx->kn.stream_tail && cut.size() >= 1) {
+      uint32_t a = cut.back(), left = k - a;
+      while (left > (1u << 14) && (left / 2) % 1024 == 0 && cut.size() + 2 < (size_t)Device::kMaxChunks) {
+        a += left / 2;
+        left -= left / 2;
+        cut.push_back(a);
+      }
+    }
+    cut.push_back(k);
+    return cut;
+  };
   const size_t kb = pk ? 32 : 4;  // pk rows or committee key indices
   for (int b = 0; b < 2; b++)
     if (!dev.pstream[b]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[b], hipStreamNonBlocking));
@@ -1903,7 +1914,7 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     // buffer b is free once batch t - kPinBufs (or the previous call's batch on it) is done
     HIPCHK(ctx, hipStreamWaitEvent(xs, dev.pin_free[b], 0));
     const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);
-    const std::vector<uint32_t>& cut = sched[t == 0 ? 0 : 1];
+    const std::vector<uint32_t> cut = schedule(t == 0, k);
     std::vector<uint32_t> marks;  // chunk ends, signatures
     for (uint32_t c = 0; c + 1 < cut.size() && cut[c] < k; c++) {
       const uint32_t o = cut[c];
@@ -1925,10 +1936,22 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
       for (hipEvent_t* ev : {&dev.msm_fork, &dev.msm_join})
         if (!*ev) HIPCHK(ctx, hipEventCreateWithFlags(ev, hipEventDisableTiming));
     }
-    // msm: the chunks' preparations on the other compute stream, sort + buckets on cs
+    // msm: the chunks' preparations on the other compute stream, sort + buckets on cs, in two
+    // segments: the chunks up to MV_MSM_SEG_PCT % of the batch (sorted and bucketed while the
+    // rest is copied), then the rest (MV_MSM_SEG_PCT = 0: every chunk a segment)
+    std::vector<uint32_t> seg_end;
+    if (msm && ctx->kn.msm_seg_pct > 0) {
+      for (uint32_t e : marks)
+        if ((uint64_t)e * 100 >= (uint64_t)k * (uint64_t)ctx->kn.msm_seg_pct) {
+          if (e < k) seg_end.push_back(e);
+          break;
+        }
+      seg_end.push_back(k);
+    }
     const mvk::ChunkGate gate{dev.chunk_ev[b], (uint32_t)marks.size(), marks.data(),
                               msm ? dev.pstream[(t & 1) ^ 1] : nullptr, msm ? dev.msm_fork : nullptr,
-                              msm ? dev.msm_join : nullptr, msm, msm ? dev.prep_ev : nullptr};
+                              msm ? dev.msm_join : nullptr, msm, msm ? dev.prep_ev : nullptr,
+                              seg_end.empty() ? nullptr : seg_end.data(), (uint32_t)seg_end.size()};
     mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dev.committee_pk.as<uint8_t>(),
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), cs,
@@ -2011,6 +2034,8 @@ const KnobDef kKnobs[] = {
     {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_OFF, false},
     {"MV_PREP_CHAIN", &mvk::Knobs::prep_chain, K_ON, false},
     {"MV_BUCKET_BAL", &mvk::Knobs::bucket_bal, K_INT, false},
+    {"MV_MSM_SEG_PCT", &mvk::Knobs::msm_seg_pct, K_INT, false},
+    {"MV_STREAM_TAIL", &mvk::Knobs::stream_tail, K_OFF, false},
 };
 
 const KnobDef* find_knob(const char* name) {

@@ -60,6 +60,8 @@ struct Knobs {
   int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
   int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
   int64_t stream_msm = 0;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM (measured slower)
+  int64_t stream_tail = 0;               // MV_STREAM_TAIL: pinned calls' last copy chunk halved down to 2^14
+  int64_t msm_seg_pct = 70;              // MV_MSM_SEG_PCT: streaming MSM's first segment (% of the batch; 0: per chunk)
   int64_t bucket_bal = 1;                // MV_BUCKET_BAL: equal entries per bucket-kernel lane (>1: entries per lane)
   int64_t prep_chain = 1;                // MV_PREP_CHAIN: a batch's k_bv_prep starts after the previous batch's
 };
@@ -112,6 +114,10 @@ struct ChunkGate {
   // chunk c's preparation on aux -> s.
   bool msm;
   const hipEvent_t* prep_done;
+  // msm: the chunks are sorted and bucketed in segments ending at seg_end[0..n_seg) (chunk ends,
+  // ascending, the last = n); n_seg = 0: every chunk is a segment
+  const uint32_t* seg_end;
+  uint32_t n_seg;
 };
 constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
 constexpr int BATCH_MAX_GROUPS = 16;

@@ -336,3 +336,34 @@ def test_bucket_forms_agree(engine, opts, bal, groups):
         assert (st == O.verify_batch(pk, s2, msg)).all() and nb == 1 and nf == 1
     finally:
         engine.set_batch_groups(0)
+
+
+@pytest.mark.parametrize("seg_pct,bal", [(70, 1), (0, 1), (70, 0), (40, 7)])
+def test_streaming_msm_segments(engine, opts, seg_pct, bal):
+    """The streaming MSM (MV_STREAM_MSM=1) on pinned inputs: 4,096-signature copy chunks
+    prepared as they land, their bucket entries sorted and added into persistent buckets in
+    segments (the first MV_MSM_SEG_PCT % of the batch, then the rest; 0: every chunk a segment),
+    with both bucket kernels: the equation holds on a valid batch without a fallback, and bad
+    signatures anywhere come back exact."""
+    for name, v in (("MV_STREAM_MSM", 1), ("MV_STREAM_CHUNK_LOG2", 12), ("MV_MSM_SEG_PCT", seg_pct),
+                    ("MV_BUCKET_BAL", bal)):
+        opts(name, v)
+    n = 9 * M.BATCH_MIN + 333
+    msg, sig, pk = signed(engine, n, 91 + seg_pct)
+
+    def pin(a):
+        h = engine.host_empty(a.shape, a.dtype)
+        h[...] = a
+        return h
+
+    engine.set_batch_groups(1)  # one equation: the streaming form (no adaptive guard from earlier tests)
+    try:
+        pm, ps, pp = pin(msg), pin(sig), pin(pk)
+        st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(pm, ps, pp))
+        assert (st == 0).all() and nb == 1 and nf == 0
+        bad = [0, 4095, 4096, n // 2, n - 1]
+        ps[bad, 40] ^= 0x10
+        st = engine.ed25519_verify(pm, ps, pp)
+        assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
+    finally:
+        engine.set_batch_groups(0)
