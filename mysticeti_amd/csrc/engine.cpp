@@ -1830,11 +1830,13 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   // last batch's prep, sort, buckets and tail follow the last copy, so the shares decrease;
   // every batch is whole 1,024s, >= MV_BATCH_MIN and <= max_batch (more batches when needed).
   // Streaming MSM (MV_STREAM_MSM=1, off by default): the call is one batch whose chunks are sorted
-  // and added into persistent buckets during the copy window (launch_verify_batch,
-  // ChunkGate::msm), so only the reduction and the final follow the last copy. Measured slower
-  // (2^20 pinned signatures: 181-196 M/s against 198 M/s for two batches on two streams,
-  // profiles/r05/e2e_msm.txt): the call is bound by its compute (~4.3 ms of kernels on one
-  // stream against 2.9 ms of copies), and every chunk pays a sort and a walk over all buckets.
+  // and added into persistent buckets during the copy window in segments (launch_verify_batch,
+  // ChunkGate::msm; MV_MSM_SEG_PCT), so only the last segment's sort and buckets, the reduction
+  // and the final follow the last copy. Measured slower: per chunk 181-196 M/s, in two segments
+  // 197-198 M/s against 208 M/s for two batches on two streams (2^20 pinned signatures,
+  // profiles/r05/e2e_msm.txt, e2e_msm_segments.txt): the call is bound by its compute (the
+  // preparations take the chip through the copy window, so the first segment's buckets run
+  // after it either way; profiles/r05/e2e/timeline_*.txt).
   const bool msm = ctx->kn.stream_msm && m <= ctx->max_batch && ctx->kn.bv_seg <= 1;
   const std::vector<double> fracs = msm ? std::vector<double>{1.0}
                                         : std::vector<double>(ctx->kn.stream_fracs,
