@@ -26,7 +26,7 @@ SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hi
 # batch.hip under LLVM's max-ilp machine scheduler, config 2 +1.4% (294.4/294.7 -> 299.2/298.4 M
 # sigs/s, interleaved A/B, profiles/r04/ab_ilp.txt)
 SOURCE_FLAGS = {"batch.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
-HEADERS = ["asm_ops.h", "fe25519.h", "ge25519.h", "hash_dev.h", "scalar25519.h", "kernels.h", "block_codec.h", "tables.h", "carry32.h", "comb.h", "quad25519.h", "fe_q4.h", "fe_r16.h", "blake2b_quad.h", "block_verdict.h", "ingest_dev.h"]
+HEADERS = ["asm_ops.h", "fe25519.h", "ge25519.h", "hash_dev.h", "scalar25519.h", "kernels.h", "block_codec.h", "tables.h", "carry32.h", "comb.h", "quad25519.h", "fe_q4.h", "fe_r16.h", "blake2b_quad.h", "block_verdict.h", "ingest_dev.h", "pt_r16.h"]
 
 
 def _newer(target: str, deps) -> bool:

@@ -44,6 +44,7 @@
 #include "tables.h"
 #include "comb.h"
 #include "quad25519.h"
+#include "pt_r16.h"
 
 namespace mv {
 
@@ -994,11 +995,15 @@ __global__ void __launch_bounds__(256) k_bv_reduce_q(const uint4* __restrict__ i
 // reduction level, one per window), four lanes per point. Lane g of wave 1, meanwhile:
 // -[sum z s mod l]B of group g from its column sums (k_bv_prep) on the comb table of B.
 // flags[1 + g] = group g's equation held; flags[0] = all.
+// rows (one group): the Horner on all of wave 0, one DPP row per coordinate (pt_r16.h), then
+// quad 0 continues from its result
 __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV, uint32_t nw,
                                                   const uint4* __restrict__ asum,
                                                   const unsigned long long* __restrict__ bsum, uint32_t ngroups,
-                                                  const uint4* __restrict__ combB, uint32_t* __restrict__ flags) {
+                                                  const uint4* __restrict__ combB, uint32_t* __restrict__ flags,
+                                                  uint32_t rows) {
   __shared__ uint4 sbp[BV_MAXG][P3_QUADS];
+  __shared__ uint4 shp[P3_QUADS];
   __shared__ uint32_t sflag[BV_MAXG];
   const uint32_t lane = threadIdx.x & 63;
   if (threadIdx.x >= 64) {
@@ -1034,7 +1039,27 @@ __global__ void __launch_bounds__(128) k_bv_final(const uint4* __restrict__ winV
   // squaring and one multiplication deep), then the per-key A term
   const uint32_t g = lane >> 2;
   fe v;
-  if (threadIdx.x < 64 && g < ngroups) {
+  if (threadIdx.x < 64 && rows && ngroups == 1) {
+    const r16::Consts K = r16::consts();
+    fe d2;
+    fe_const(d2, K_D2);
+    fer d2r;
+    fer_from_fe(d2r, d2);
+    fer pv = r4::load(winV, nw - 1);
+#pragma unroll 1
+    for (int w = (int)nw - 2; w >= 0; w--) {
+      const fer wv = r4::load(winV, w);
+#pragma unroll 1
+      for (int i = 0; i < BV_C; i++) r4::dbl(pv, K);
+      r4::addp(pv, wv, d2r, K);
+    }
+    if (asum) r4::addp(pv, r4::load(asum, 0), d2r, K);
+    r4::store(reinterpret_cast<uint32_t*>(shp), pv);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the rows' stores before quad 0 reads
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (g == 0) qp_load(v, shp, 0);
+  } else if (threadIdx.x < 64 && g < ngroups) {
     const size_t row0 = (size_t)g * nw;
     qp_load(v, winV, row0 + nw - 1);
     for (int w = (int)nw - 2; w >= 0; w--) {
@@ -1328,7 +1353,7 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
   }
   mark(4);
   hipLaunchKernelGGL(k_bv_final, dim3(1), dim3(128), 0, s, inV, nw, agg ? (const uint4*)asum : nullptr, bsum,
-                     G.count, static_cast<const uint4*>(comb_b), flag);
+                     G.count, static_cast<const uint4*>(comb_b), flag, kn.final_rows ? 1u : 0u);
   mark(5);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
