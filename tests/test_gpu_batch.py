@@ -367,3 +367,25 @@ def test_streaming_msm_segments(engine, opts, seg_pct, bal):
         assert (st[bad] == 1).all() and (np.delete(st, bad) == 0).all()
     finally:
         engine.set_batch_groups(0)
+
+
+@pytest.mark.parametrize("rows", [1, 0])
+@pytest.mark.parametrize("groups", [0, 3])
+def test_final_forms_agree(engine, opts, rows, groups):
+    """k_bv_final's Horner with one DPP row per coordinate (MV_FINAL_ROWS=1, one equation) and
+    with four lanes per point (0, or several sub-batch equations): valid batches hold without a
+    fallback (a wrong window sum, doubling or addition would fail the equation), and a bad
+    signature fails exactly its group."""
+    opts("MV_FINAL_ROWS", rows)
+    n = 6000
+    msg, sig, pk = signed(engine, n, 303)
+    engine.set_batch_groups(groups)
+    try:
+        st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, sig, pk))
+        assert (st == 0).all() and nb == 1 and nf == 0
+        s2 = sig.copy()
+        s2[[17, n - 5], 40] ^= 0x10
+        st, nb, nf = stats_delta(engine, lambda: engine.ed25519_verify(msg, s2, pk))
+        assert (st == O.verify_batch(pk, s2, msg)).all() and nb == 1 and nf == 1
+    finally:
+        engine.set_batch_groups(0)
