@@ -479,6 +479,86 @@ __global__ void __launch_bounds__(PART_CHUNK) k_part_scatter(const uint4* __rest
     });
   }
 }
+// The same scatter with coalesced stores (MV_SCATTER_LDS): window by window, the block's entries
+// are first placed in LDS in partition order (the chunk's per-partition counts from
+// k_part_count, scanned), then thread i stores LDS entry i, so consecutive threads write
+// consecutive words of a partition's run instead of one scattered 8-byte word per entry (the
+// direct form wrote 2.7x the entry bytes, profiles/r05/pmc/pmc_c2_k_part_scatter.txt). Entry
+// order inside a run changes, which no later stage depends on (the fine sort orders by key,
+// and a bucket's sum does not depend on the order of its points).
+constexpr uint32_t BV_PPW_ = BV_NB >> BV_FINE_BITS;  // partitions per window (128)
+__global__ void __launch_bounds__(PART_CHUNK) k_part_scatter_lds(const uint4* __restrict__ scal, uint32_t n,
+                                                                 const uint32_t* __restrict__ pcount,
+                                                                 const uint32_t* __restrict__ poff,
+                                                                 const uint32_t* __restrict__ pstart, BvGroups G,
+                                                                 uint32_t skipA, uint32_t nall, uint32_t base,
+                                                                 unsigned long long* __restrict__ tmp) {
+  __shared__ unsigned long long buf[2 * PART_CHUNK];  // one window's entries (<= 2 per signature)
+  __shared__ uint32_t lofs[BV_PPW_ + 1], gpos[BV_PPW_], rank[BV_PPW_];
+  const uint32_t gid = blockIdx.x * PART_CHUNK + threadIdx.x;
+  const bool live = gid < n;
+  const uint32_t g = blockIdx.x / G.cpg;
+  // the signature's digits, all windows (bv_for_digits' carries), kept in registers
+  int dR[8], dA[16];
+#pragma unroll
+  for (int w = 0; w < 8; w++) dR[w] = 0;
+#pragma unroll
+  for (int w = 0; w < 16; w++) dA[w] = 0;
+  if (live) {
+    uint32_t z[4], zk[8];
+    load_scalars(z, zk, scal, gid);
+    if (skipA) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) zk[i] = 0;
+    }
+    bv_for_digits(z, zk, [&](int w, int d, int isA) {
+      if (isA) dA[w] = d; else dR[w < 8 ? w : 0] = d;
+    });
+  }
+  const uint32_t* pc = pcount + (size_t)blockIdx.x * BV_NPG;
+  const uint32_t* po = poff + (size_t)blockIdx.x * BV_NPG;
+  const uint32_t* ps = pstart + (size_t)g * BV_NPG;
+  const uint32_t ptR = base + gid, ptA = nall + base + gid;
+#pragma unroll 1
+  for (int w = 0; w < BV_NW; w++) {
+    // this window's partitions: chunk-local offsets (wave 0 scans 128 counts), global run starts
+    if (threadIdx.x < 64) {
+      const uint32_t l = threadIdx.x, p0 = (uint32_t)w * BV_PPW_ + 2 * l;
+      const uint32_t c0 = pc[p0], c1 = pc[p0 + 1];
+      uint32_t incl = c0 + c1;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = (uint32_t)__shfl_up((int)incl, o);
+        if (l >= (uint32_t)o) incl += x;
+      }
+      const uint32_t ex = incl - c0 - c1;
+      lofs[2 * l] = ex;
+      lofs[2 * l + 1] = ex + c0;
+      if (l == 63) lofs[BV_PPW_] = incl;
+      gpos[2 * l] = ps[p0] + po[p0];
+      gpos[2 * l + 1] = ps[p0 + 1] + po[p0 + 1];
+      rank[2 * l] = 0;
+      rank[2 * l + 1] = 0;
+    }
+    __syncthreads();
+    auto place = [&](int d, uint32_t pt) {
+      const uint32_t key = bv_key(w, d), pl = (key >> BV_FINE_BITS) & (BV_PPW_ - 1);
+      const uint32_t r = atomicAdd(&rank[pl], 1u);
+      buf[lofs[pl] + r] = ((unsigned long long)(g * BV_NKG + key) << 32) | (pt << 1) | (d < 0 ? 1u : 0u);
+    };
+    if (w < 8 && dR[w]) place(dR[w], ptR);
+    if (dA[w]) place(dA[w], ptA);
+    __syncthreads();
+    const uint32_t tot = lofs[BV_PPW_];
+    for (uint32_t i = threadIdx.x; i < tot; i += PART_CHUNK) {
+      const unsigned long long e = buf[i];
+      const uint32_t pl = ((uint32_t)(e >> 32) >> BV_FINE_BITS) & (BV_PPW_ - 1);
+      tmp[gpos[pl] + (i - lofs[pl])] = e;
+    }
+    __syncthreads();
+  }
+}
+
 // block -> partition P: the partition's entries sorted by bucket into ents; offs[key] for
 // its 256 keys. FINE_NT threads over 256 bins (a partition holds ~8K entries, window 15's
 // ~32K: digits stop at 2^13), so the ranked stores of the blocks in flight merge in L2. The
@@ -1270,8 +1350,12 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
       hipLaunchKernelGGL(k_part_scan, dim3(BV_NPG / 64), dim3(64 * SCAN_SUB), 0, s, pcount + (size_t)c0 * BV_NPG, ncc,
                          Gc, poff + (size_t)c0 * BV_NPG, ptot);
       hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, (uint32_t)BV_NPG, pstart);
-      hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, poff + (size_t)c0 * BV_NPG, pstart,
-                         Gc, agg ? 1u : 0u, n, seg_lo, tmp);
+      if (kn.scatter_lds)
+        hipLaunchKernelGGL(k_part_scatter_lds, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, pcount + (size_t)c0 * BV_NPG,
+                           poff + (size_t)c0 * BV_NPG, pstart, Gc, agg ? 1u : 0u, n, seg_lo, tmp);
+      else
+        hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, poff + (size_t)c0 * BV_NPG, pstart,
+                           Gc, agg ? 1u : 0u, n, seg_lo, tmp);
       hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
       buckets(m, seg_lo ? 1u : 0u);
       seg_lo = hi;
@@ -1313,8 +1397,12 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(64 * SCAN_SUB), 0, s, pcount, nchunk, G, poff,
                        ptot);
     hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, nparts, pstart);
-    hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
-                       agg ? 1u : 0u, n, 0u, tmp);
+    if (kn.scatter_lds)
+      hipLaunchKernelGGL(k_part_scatter_lds, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, pcount, poff, pstart, G,
+                         agg ? 1u : 0u, n, 0u, tmp);
+    else
+      hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
+                         agg ? 1u : 0u, n, 0u, tmp);
     hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
     mark(2);
     // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,

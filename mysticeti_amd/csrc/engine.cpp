@@ -2039,6 +2039,7 @@ const KnobDef kKnobs[] = {
     {"MV_MSM_SEG_PCT", &mvk::Knobs::msm_seg_pct, K_INT, false},
     {"MV_STREAM_TAIL", &mvk::Knobs::stream_tail, K_OFF, false},
     {"MV_FINAL_ROWS", &mvk::Knobs::final_rows, K_ON, false},
+    {"MV_SCATTER_LDS", &mvk::Knobs::scatter_lds, K_ON, false},
 };
 
 const KnobDef* find_knob(const char* name) {
