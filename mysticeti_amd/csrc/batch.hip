@@ -611,6 +611,84 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort(const unsigned long long*
   }
 }
 
+// The same sort with its output staged in LDS (MV_FINE_LDS): a partition of <= FINE_LDS entries
+// is read once into registers (16 per thread), counted, scanned, placed in LDS in bucket order
+// and stored coalesced; the direct form read each entry twice and stored one scattered word per
+// entry. Larger partitions (window 15's at 2^20 signatures: ~32K) take the direct form.
+constexpr uint32_t FINE_LDS = 16384;
+constexpr int FINE_FPT = FINE_LDS / FINE_NT;
+__global__ void __launch_bounds__(FINE_NT) k_fine_sort_lds(const unsigned long long* __restrict__ tmp,
+                                                           const uint32_t* __restrict__ pstart, uint32_t ngroups,
+                                                           uint32_t* __restrict__ ents, uint32_t* __restrict__ offs) {
+  constexpr int NF = 1 << BV_FINE_BITS;
+  __shared__ uint32_t cnt[NF];
+  __shared__ uint32_t obuf[FINE_LDS];
+  const uint32_t span = ngroups * BV_PPW;
+  const uint32_t w = BV_NW - 1 - blockIdx.x / span;
+  const uint32_t g = (blockIdx.x % span) / BV_PPW;
+  const uint32_t p = g * BV_NPG + w * BV_PPW + blockIdx.x % BV_PPW;
+  const uint32_t s = pstart[p], e = pstart[p + 1], m = e - s;
+  const bool staged = m <= FINE_LDS;  // (uniform in the block)
+  if (threadIdx.x < NF) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long v[FINE_FPT];
+  if (staged) {
+#pragma unroll
+    for (int k = 0; k < FINE_FPT; k++) {
+      const uint32_t i = threadIdx.x + (uint32_t)k * FINE_NT;
+      v[k] = i < m ? tmp[s + i] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < FINE_FPT; k++)
+      if (threadIdx.x + (uint32_t)k * FINE_NT < m) atomicAdd(&cnt[(uint32_t)(v[k] >> 32) & (NF - 1)], 1u);
+  } else {
+    for (uint32_t i = s + threadIdx.x; i < e; i += FINE_NT) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
+  }
+  __syncthreads();
+  static_assert(NF == 256, "wave 0 scans four bins per lane");
+  if (threadIdx.x < 64) {  // wave 0 alone (no barrier inside): exclusive scan of the bins
+    const uint32_t l = threadIdx.x;
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = cnt[4 * l + k];
+      sum += c[k];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)incl, o);
+      if (l >= (uint32_t)o) incl += x;
+    }
+    uint32_t ex = incl - sum;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      offs[(size_t)p * NF + 4 * l + k] = s + ex;
+      cnt[4 * l + k] = ex;
+      ex += c[k];
+    }
+    if (p == ngroups * BV_NPG - 1 && l == 0) offs[(size_t)ngroups * BV_NKG] = e;
+  }
+  __syncthreads();
+  if (staged) {
+#pragma unroll
+    for (int k = 0; k < FINE_FPT; k++) {
+      if (threadIdx.x + (uint32_t)k * FINE_NT < m) {
+        const uint32_t r = atomicAdd(&cnt[(uint32_t)(v[k] >> 32) & (NF - 1)], 1u);
+        obuf[r] = (uint32_t)v[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += FINE_NT) ents[s + i] = obuf[i];
+  } else {
+    for (uint32_t i = s + threadIdx.x; i < e; i += FINE_NT) {
+      const unsigned long long x = tmp[i];
+      const uint32_t r = atomicAdd(&cnt[(uint32_t)(x >> 32) & (NF - 1)], 1u);
+      ents[s + r] = (uint32_t)x;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- buckets
 // Lane = segment of `seg` consecutive buckets (g, w, j*seg .. j*seg + seg - 1), consumed from
 // the top bucket down: T = running sum of the segment's buckets, V = sum of T after every
@@ -1356,7 +1434,10 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
       else
         hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, poff + (size_t)c0 * BV_NPG, pstart,
                            Gc, agg ? 1u : 0u, n, seg_lo, tmp);
-      hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
+      if (kn.fine_lds)
+        hipLaunchKernelGGL(k_fine_sort_lds, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
+      else
+        hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
       buckets(m, seg_lo ? 1u : 0u);
       seg_lo = hi;
     }
@@ -1403,7 +1484,10 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     else
       hipLaunchKernelGGL(k_part_scatter, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, poff, pstart, G,
                          agg ? 1u : 0u, n, 0u, tmp);
-    hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
+    if (kn.fine_lds)
+      hipLaunchKernelGGL(k_fine_sort_lds, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
+    else
+      hipLaunchKernelGGL(k_fine_sort, dim3(nparts), dim3(FINE_NT), 0, s, tmp, pstart, G.count, ents, offs);
     mark(2);
     // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
     // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go

@@ -2040,6 +2040,7 @@ const KnobDef kKnobs[] = {
     {"MV_STREAM_TAIL", &mvk::Knobs::stream_tail, K_OFF, false},
     {"MV_FINAL_ROWS", &mvk::Knobs::final_rows, K_ON, false},
     {"MV_SCATTER_LDS", &mvk::Knobs::scatter_lds, K_ON, false},
+    {"MV_FINE_LDS", &mvk::Knobs::fine_lds, K_ON, false},
 };
 
 const KnobDef* find_knob(const char* name) {
