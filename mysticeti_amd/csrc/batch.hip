@@ -904,6 +904,9 @@ __global__ void __launch_bounds__(256) k_bv_bucket_fix(const uint32_t* __restric
 }
 
 // ---------------------------------------------------------------- reduction
+#ifndef MV_REDUCE_PF
+#define MV_REDUCE_PF 1  // inputs loaded one step ahead (0: the old load-then-use order, A/B)
+#endif
 // Rows = (group, window); row r holds cnt_in elements. Elements (V, T) with indices
 // m = 0..cnt-1 stand for V + (m * scale) T. Groups of FAN consecutive elements m = FAN*q + t
 // become one element with index q:
@@ -927,7 +930,9 @@ __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV,
   p3 U, Sx, X;
   p3_identity(U);
   p3_identity(Sx);
+  // each step's point(s) loaded one step ahead (the lane is a lone latency chain)
   if (!inV) {
+#if MV_REDUCE_PF == 0
     for (int t = m - 1; t >= 0; t--) {
       p3_load(X, inT, base + t);
       p3_acc(U, X);
@@ -936,15 +941,45 @@ __global__ void __launch_bounds__(64) k_bv_reduce(const uint4* __restrict__ inV,
     p3_store(outV, gid, Sx);
     p3_store(outT, gid, U);
     return;
+#endif
+    p3_load(X, inT, base + m - 1);
+    for (int t = m - 1; t >= 0; t--) {
+      const p3 Xc = X;
+      if (t > 0) p3_load(X, inT, base + t - 1);
+      p3_acc(U, Xc);
+      p3_acc(Sx, U);
+    }
+    p3_store(outV, gid, Sx);
+    p3_store(outT, gid, U);
+    return;
   }
-  p3 Vs;
+  p3 Vs, Y;
   p3_identity(Vs);
+#if MV_REDUCE_PF == 0
   for (int t = m - 1; t >= 0; t--) {
     p3_load(X, inT, base + t);
     p3_acc(U, X);
+    if (t > 0) p3_acc(Sx, U);
+    p3_load(Y, inV, base + t);
+    p3_acc(Vs, Y);
+  }
+  p3_dbl_n(Sx, shift);
+  p3_acc(Vs, Sx);
+  p3_store(outV, gid, Vs);
+  p3_store(outT, gid, U);
+  return;
+#endif
+  p3_load(X, inT, base + m - 1);
+  p3_load(Y, inV, base + m - 1);
+  for (int t = m - 1; t >= 0; t--) {
+    const p3 Xc = X, Yc = Y;
+    if (t > 0) {
+      p3_load(X, inT, base + t - 1);
+      p3_load(Y, inV, base + t - 1);
+    }
+    p3_acc(U, Xc);
     if (t > 0) p3_acc(Sx, U);  // sum_{t>=1} sum_{t'>=t} T_t' = sum t' T_t'
-    p3_load(X, inV, base + t);
-    p3_acc(Vs, X);
+    p3_acc(Vs, Yc);
   }
   p3_dbl_n(Sx, shift);
   p3_acc(Vs, Sx);
@@ -1123,7 +1158,9 @@ __global__ void __launch_bounds__(256) k_bv_reduce_q(const uint4* __restrict__ i
   fe U, Sx, X;
   qp_identity(U);
   qp_identity(Sx);
+  // each step's point(s) loaded one step ahead (a quad is a lone latency chain)
   if (!inV) {
+#if MV_REDUCE_PF == 0
     for (int t = m - 1; t >= 0; t--) {
       qp_load(X, inT, base + t);
       qp_add(U, X);
@@ -1132,15 +1169,45 @@ __global__ void __launch_bounds__(256) k_bv_reduce_q(const uint4* __restrict__ i
     qp_store(outV, gid, Sx);
     qp_store(outT, gid, U);
     return;
+#endif
+    qp_load(X, inT, base + m - 1);
+    for (int t = m - 1; t >= 0; t--) {
+      const fe Xc = X;
+      if (t > 0) qp_load(X, inT, base + t - 1);
+      qp_add(U, Xc);
+      qp_add(Sx, U);
+    }
+    qp_store(outV, gid, Sx);
+    qp_store(outT, gid, U);
+    return;
   }
-  fe Vs;
+  fe Vs, Y;
   qp_identity(Vs);
+#if MV_REDUCE_PF == 0
   for (int t = m - 1; t >= 0; t--) {
     qp_load(X, inT, base + t);
     qp_add(U, X);
     if (t > 0) qp_add(Sx, U);
-    qp_load(X, inV, base + t);
-    qp_add(Vs, X);
+    qp_load(Y, inV, base + t);
+    qp_add(Vs, Y);
+  }
+  qp_dbl_n(Sx, shift);
+  qp_add(Vs, Sx);
+  qp_store(outV, gid, Vs);
+  qp_store(outT, gid, U);
+  return;
+#endif
+  qp_load(X, inT, base + m - 1);
+  qp_load(Y, inV, base + m - 1);
+  for (int t = m - 1; t >= 0; t--) {
+    const fe Xc = X, Yc = Y;
+    if (t > 0) {
+      qp_load(X, inT, base + t - 1);
+      qp_load(Y, inV, base + t - 1);
+    }
+    qp_add(U, Xc);
+    if (t > 0) qp_add(Sx, U);
+    qp_add(Vs, Yc);
   }
   qp_dbl_n(Sx, shift);
   qp_add(Vs, Sx);
