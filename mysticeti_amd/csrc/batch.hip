@@ -1215,6 +1215,62 @@ __global__ void __launch_bounds__(256) k_bv_reduce_q(const uint4* __restrict__ i
   qp_store(outT, gid, U);
 }
 
+// The same level with one WAVE per element, one DPP row per coordinate (pt_r16.h), for the
+// small top levels (<= MV_REDUCE_ROWS elements: at most a wave or so per SIMD, where a quad's
+// lone chain of 24 additions is issue-bound): the element's 2 x fan inputs are loaded at once
+// (one word per lane each) and every point operation is two row products deep. On a big level
+// the quad form stays: a wave per element issues ~5x the instructions per element.
+__global__ void __launch_bounds__(256) k_bv_reduce_r(const uint4* __restrict__ inV, const uint4* __restrict__ inT,
+                                                     uint32_t cnt_in, int fan, int shift, uint32_t rows, uint32_t nw,
+                                                     uint32_t from_keys, uint4* __restrict__ outV,
+                                                     uint4* __restrict__ outT) {
+  const uint32_t cnt_out = (cnt_in + fan - 1) / fan;
+  const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one element per wave
+  if (gid >= cnt_out * rows) return;                                  // (uniform in the wave)
+  const uint32_t r = gid / cnt_out, q = gid % cnt_out;
+  const uint32_t rin = from_keys ? (r / nw) * BV_NW + r % nw : r;
+  const size_t base = (size_t)rin * cnt_in + (size_t)q * fan;
+  const int m = (int)min((uint32_t)fan, cnt_in - q * fan);
+  const r16::Consts K = r16::consts();
+  fe d2;
+  fe_const(d2, K_D2);
+  fer d2r;
+  fer_from_fe(d2r, d2);
+  fer T[BV_FAN], V[BV_FAN];
+#pragma unroll
+  for (int t = 0; t < BV_FAN; t++) {
+    T[t] = t < m ? r4::load(inT, base + t) : r4::identity();
+    V[t] = (inV && t < m) ? r4::load(inV, base + t) : r4::identity();
+  }
+  fer U = r4::identity(), Sx = r4::identity();
+  if (!inV) {
+#pragma unroll
+    for (int t = BV_FAN - 1; t >= 0; t--) {
+      if (t < m) {
+        r4::addp(U, T[t], d2r, K);
+        r4::addp(Sx, U, d2r, K);
+      }
+    }
+    r4::store(outV, gid, Sx);
+    r4::store(outT, gid, U);
+    return;
+  }
+  fer Vs = r4::identity();
+#pragma unroll
+  for (int t = BV_FAN - 1; t >= 0; t--) {
+    if (t < m) {
+      r4::addp(U, T[t], d2r, K);
+      if (t > 0) r4::addp(Sx, U, d2r, K);
+      r4::addp(Vs, V[t], d2r, K);
+    }
+  }
+#pragma unroll 1
+  for (int i = 0; i < shift; i++) r4::dbl(Sx, K);
+  r4::addp(Vs, Sx, d2r, K);
+  r4::store(outV, gid, Vs);
+  r4::store(outT, gid, U);
+}
+
 // ---------------------------------------------------------------- final check
 // One 128-thread block. Quad g of wave 0: Horner over group g's window sums (V of the last
 // reduction level, one per window), four lanes per point. Lane g of wave 1, meanwhile:
@@ -1578,7 +1634,10 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     const int fan = cnt >= (uint32_t)BV_FAN ? BV_FAN : (int)cnt;
     const uint32_t out = (cnt + fan - 1) / fan;
     const uint32_t lanes = out * rows;
-    if (lanes <= reduce_quad_max(kn))  // latency-bound level: four lanes per element
+    if (lanes <= (uint32_t)kn.reduce_rows)  // small top level: a wave per element
+      hipLaunchKernelGGL(k_bv_reduce_r, dim3((64 * lanes + 255) / 256), dim3(256), 0, s, inV, inT, cnt, fan, shift,
+                         rows, nw, inT == segT ? 1u : 0u, rv[pp], rt[pp]);
+    else if (lanes <= reduce_quad_max(kn))  // latency-bound level: four lanes per element
       hipLaunchKernelGGL(k_bv_reduce_q, dim3((4 * lanes + 255) / 256), dim3(256), 0, s, inV, inT, cnt, fan, shift,
                          rows, nw, inT == segT ? 1u : 0u, rv[pp], rt[pp]);
     else

@@ -2041,6 +2041,7 @@ const KnobDef kKnobs[] = {
     {"MV_FINAL_ROWS", &mvk::Knobs::final_rows, K_ON, false},
     {"MV_SCATTER_LDS", &mvk::Knobs::scatter_lds, K_ON, false},
     {"MV_FINE_LDS", &mvk::Knobs::fine_lds, K_ON, false},
+    {"MV_REDUCE_ROWS", &mvk::Knobs::reduce_rows, K_INT, false},
 };
 
 const KnobDef* find_knob(const char* name) {

@@ -60,6 +60,7 @@ struct Knobs {
   int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
   int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
   int64_t stream_msm = 0;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM (measured slower)
+  int64_t reduce_rows = 1024;            // MV_REDUCE_ROWS: reduction levels of <= this many elements a wave each (0: none)
   int64_t fine_lds = 1;                  // MV_FINE_LDS: the fine sort staged in registers + LDS (coalesced stores)
   int64_t scatter_lds = 1;               // MV_SCATTER_LDS: the partition scatter staged in LDS (coalesced stores)
   int64_t final_rows = 1;                // MV_FINAL_ROWS: k_bv_final's Horner with one DPP row per coordinate

@@ -110,6 +110,13 @@ MV_DEV void store(uint32_t* w36, const fer& v) {
   const uint32_t t = r16::lane();
   if (t < 9) w36[9 * row() + t] = v.v;
 }
+MV_DEV void store(uint4* base, size_t idx, const fer& v) { store(reinterpret_cast<uint32_t*>(base + idx * 9), v); }
+// the identity (0 : 1 : 1 : 0)
+MV_DEV fer identity() {
+  fer r;
+  r.v = (r16::lane() == 0 && (row() == 1u || row() == 2u)) ? 1u : 0u;
+  return r;
+}
 
 }  // namespace r4
 }  // namespace mv
