@@ -20,10 +20,14 @@
 //                 z_i = BLAKE2b(secret || call || i), scalars z_i and z_i k_i mod l,
 //                 affine points (y+x, y-x, 2dxy) to HBM, sum z_i s_i
 //   k_part_*, k_fine_sort   two-pass counting sort of the (bucket, point) entries
-//                 (LDS histograms and ranks; no global atomics)
-//   k_bv_bucket   lane per bucket: the bucket's sum T
+//                 (LDS histograms and ranks; no global atomics; the _lds forms stage
+//                 their output in LDS and store it coalesced)
+//   k_bv_bucket   lane per bucket: the bucket's sum T (k_bv_bucket_bal + _fix: the
+//                 same sums with an equal number of entries per lane)
 //   k_bv_reduce   tree over the buckets (fan-in 8) of the pairs (V, T) per window
-//   k_bv_final    Horner over the 16 window sums, -[sum z s]B, [8], identity test
+//                 (_q: four lanes per element, _r: a wave per element on small levels)
+//   k_bv_final    Horner over the 16 window sums (one DPP row per coordinate with one
+//                 equation), -[sum z s]B, [8], identity test
 // Sub-batch equations: the batch may be cut into up to BV_MAXG groups of whole 1024-
 // signature chunks, each with its own buckets and its own combined equation (one flag per
 // group). The fallback then re-verifies only the groups whose equation failed, so k bad
