@@ -135,6 +135,61 @@ def cpu_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, sample: int):
     }
 
 
+# Keys dropped below the top level of the stdout line (compact_line): prose and per-leg detail.
+# The driver keeps only the last ~8 KB of stdout; the full line goes to stderr.
+_VERBOSE = {"note", "impl", "host_cpu", "nproc", "data", "label", "kernel_ms_source", "frac_label", "work_per_sig",
+            "work", "per", "traffic_source", "stage_ms_as_run", "sha256_msg_digests_first_corpus", "mean_us",
+            "batches", "unit", "cpu_1t", "rss_after", "hbm_peak_at", "queue_calls", "online_launches",
+            "online_requests", "values", "bincode_GB", "seconds", "host_enqueue", "sample", "cores_source", "config",
+            "traffic_per_2^20_blocks", "work_per_block", "entries_per_s", "hbm_bincode_GBps"}
+
+
+def _prune(x, depth=0):
+    if isinstance(x, dict):
+        return {k: _prune(v, depth + 1) for k, v in x.items() if not (depth > 0 and k in _VERBOSE)}
+    if isinstance(x, list):
+        return [_prune(v, depth + 1) for v in x]
+    if isinstance(x, float):
+        return float(f"{x:.5g}") if abs(x) < 1e5 else round(x, 1)
+    return x
+
+
+def summary_of(out: dict) -> dict:
+    """Every leg's headline in one flat dict (the last key of the stdout line, so it survives any
+    tail of the driver's record). Units: sigs/s, blocks/s, GB/s, ms, us."""
+    g = lambda d, *ks: None if d is None else (d.get(ks[0]) if len(ks) == 1 else g(d.get(ks[0]), *ks[1:]))
+    s = {"c2_sigs_per_s": out["value"], "c2_ms_per_step": out["ms_per_step"],
+         "c2_sustained_median": g(out, "sustained", "median"), "c2_prep_frac": g(out, "roofline", "frac"),
+         "c2_step_frac": g(out, "pipeline", "frac"),
+         "c3_1pct_sigs_per_s": g(out, "adversarial", "config3_1pct", "value"),
+         "one_bad_per_batch_sigs_per_s": g(out, "adversarial", "one_bad_per_batch", "value"),
+         "e2e_pinned_sigs_per_s": g(out, "end_to_end", "value"),
+         "e2e_frac_of_resident": round(out["end_to_end"]["value"] / out["value"], 4) if out.get("end_to_end") else None,
+         "e2e_two_callers_sigs_per_s": g(out, "end_to_end", "two_callers", "value"),
+         "c4_blocks_per_s": g(out, "config4", "value"), "c4_ms_per_step": g(out, "config4", "ms_per_step"),
+         "c4_hash_frac": g(out, "config4", "roofline", "frac"),
+         "c4_host_fed_blocks_per_s": g(out, "config4", "host_fed", "value"),
+         "wal_GBps": g(out, "wal", "value"), "cpu_sigs_per_s": g(out, "cpu_baseline", "value"),
+         "cpu_cores": g(out, "cpu_baseline", "cores")}
+    shapes = g(out, "config5", "shapes") or {}
+    for k, v in shapes.items():
+        s[f"c5_{k}_64blk_p50_us"] = g(v, "gpu", "p50_us")
+        s[f"c5_{k}_64blk_cpu_p50_us"] = g(v, "cpu_16t", "p50_us")
+        for leg in ("concurrent_1_block_callers", "fan_in_callers"):
+            c = v.get(leg)
+            if c:
+                s[f"c5_{k}_{c['callers']}callers_gpu_over_cpu"] = c.get("gpu_over_cpu_blocks_per_s")
+    s["correct"] = out["correct"]
+    s["parity_sha256"] = out.get("parity_sha256")
+    return {k: v for k, v in s.items() if v is not None}
+
+
+def compact_line(out: dict) -> dict:
+    c = _prune(out)
+    c["summary"] = summary_of(out)
+    return c
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -360,8 +415,10 @@ def main():
                      "frac_of_value": round(float(np.median(vals)) / value, 4)}
 
     # adversarial batches (config 3 / a Byzantine signer): corrupted copies of the corpus,
-    # verdicts checked against the expected mask; each rate after 3 untimed steps (the
-    # adaptive policy's steady state: a failed equation cuts the next batches into groups)
+    # verdicts checked against the expected mask; each rate after 9 untimed steps (the
+    # adaptive policy's steady state: a failed equation cuts the next batches into groups, and
+    # dense failures send them to the single path; with three streams in flight the policy
+    # sees a batch's flags about three batches later)
     adversarial = None
     if args.path == "batch" and args.adversarial and not args.corrupt:
         adversarial = {}
@@ -380,12 +437,13 @@ def main():
                 st["i"] += 1
                 eng.dev_verify_batch(local_rank, d_msg, d_bad, d_pk, d_status[j], d_ok[j], streams[j].cuda_stream)
 
-            for _ in range(3):
+            for _ in range(9):
                 adv_step()
-            c0 = eng.batch_counters()
+            torch.cuda.synchronize(dev)
+            c0, r0 = eng.batch_counters(), eng.batch_routes()
             k = max(4, min(args.steps // 2, 200))
             e = timed_region(adv_step, k, lambda: torch.cuda.synchronize(dev), dist)
-            c1 = eng.batch_counters()
+            c1, r1 = eng.batch_counters(), eng.batch_routes()
             good = all((x.cpu().numpy() == want).all() for x in d_status)
             ok = ok and good
             rate = n * world * k / e
@@ -393,10 +451,12 @@ def main():
                                  "bad_signatures_per_batch": int(idx.size),
                                  "ratio_to_all_valid": round(rate / value, 4), "correct": bool(good),
                                  "groups_per_batch": round((c1[2] - c0[2]) / max(1, c1[0] - c0[0]), 2),
-                                 "groups_reverified_per_batch": round((c1[3] - c0[3]) / max(1, c1[0] - c0[0]), 2)}
+                                 "groups_reverified_per_batch": round((c1[3] - c0[3]) / max(1, c1[0] - c0[0]), 2),
+                                 "single_path_batches": r1[1] - r0[1], "equation_batches": r1[0] - r0[0]}
             del d_bad
         adversarial["note"] = ("one flipped s bit per bad signature (s < l, R decodes); the batch is re-verified "
-                               "only in the sub-batch equations that fail (DESIGN.md 2)")
+                               "only in the sub-batch equations that fail; dense failures go straight to the "
+                               "single path (DESIGN.md 2)")
         ok = all_ranks_ok(ok, dist)
         # the adversarial batches armed the guard (the next 64 batches in 8 sub-batch equations):
         # the legs below measure the unguarded default
@@ -538,7 +598,10 @@ def main():
         if cpu:
             out["speedup_vs_cpu"] = {"all_cores": round(value / world / cpu["value"], 1),
                                      "single_core": round(value / world / cpu["single_core_value"], 1)}
-        print(json.dumps(out), flush=True)
+        # the full line on stderr, the compact one (every leg's headline in `summary`, its last
+        # key) on stdout: the driver's record keeps the stdout tail
+        print("bench_full_line: " + json.dumps(out), file=sys.stderr, flush=True)
+        print(json.dumps(compact_line(out)), flush=True)
     eng.close()
     if dist:
         dist.destroy_process_group()

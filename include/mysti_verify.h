@@ -247,11 +247,20 @@ mv_status mv_batch_stats(mv_ctx* ctx, uint64_t* batches, uint64_t* fallbacks);
  * sub-batch, out[2] sub-batch equations checked, out[3] sub-batch equations that failed
  * (each re-verified signature by signature). Device-API calls are counted once complete. */
 mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out /* 4 */);
+/* Routes of batch-path calls under the adaptive policy (config 3, net_sync.rs:352-361: a peer
+ * that keeps sending bad signatures): out[0] batches checked by a combined equation (as
+ * mv_batch_stats), out[1] batches sent straight to per-signature verification because the
+ * failures were dense, out[2] dense failures seen (a guarded batch with at least half of its
+ * sub-batch equations failed). Device-API calls are counted once complete. */
+mv_status mv_batch_routes(mv_ctx* ctx, uint64_t* out /* 3 */);
 /* Sub-batch equations per batch-path call: the batch is cut into groups of whole 1024-signature
  * chunks, each with its own combined equation, and a failed equation re-verifies only its group.
  * groups = 0 (default): adaptive -- 1 group per batch; after a batch whose equation failed,
- * the next 64 batches are cut into 8. groups = 1..16 fixes the count. Every call clears the guard.
- * Verdicts never depend on it. */
+ * the next 64 batches are cut into 8; after a guarded batch in which at least half of the
+ * equations failed (dense failures: the combined check is wasted work), the next batches are
+ * verified signature by signature, each counting its invalid signatures, until one holds fewer
+ * than 4 (then the guarded equation again). groups = 1..16 fixes the count and disables the
+ * dense-failure route. Every call clears the guard. Verdicts never depend on it. */
 mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups);
 /* Stage timing: when enabled, every call records HIP events on its stream around its
  * stages: batch path 0..5 (prep, sort, bucket, reduce, final, fallback), block pipeline

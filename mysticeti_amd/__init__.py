@@ -46,7 +46,7 @@ EXPORTS = [
     "mv_create", "mv_destroy", "mv_last_error", "mv_version", "mv_set_committee", "mv_blake2b256",
     "mv_ed25519_verify", "mv_ed25519_sign", "mv_verify_blocks", "mv_dev_ed25519_verify",
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
-    "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_set_batch_groups",
+    "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_batch_routes", "mv_set_batch_groups",
     "mv_queue_stats", "mv_shard_plan", "mv_crc32", "mv_wal_verify", "mv_wal_layout", "mv_dev_wal_verify",
     "mv_dev_crc32", "mv_host_alloc", "mv_host_free", "mv_online_stats", "mv_set_option", "mv_get_option",
 ]
@@ -95,6 +95,7 @@ def load_library(path: str = LIB_PATH):
     lib.mv_dev_ed25519_verify_batch.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, u32, vp, vp, vp]
     lib.mv_batch_stats.argtypes = [vp, vp, vp]
     lib.mv_batch_counters.argtypes = [vp, vp]
+    lib.mv_batch_routes.argtypes = [vp, vp]
     lib.mv_set_batch_groups.argtypes = [vp, u32]
     lib.mv_queue_stats.argtypes = [vp, vp, vp]
     lib.mv_online_stats.argtypes = [vp, vp, vp]
@@ -312,6 +313,13 @@ class Engine:
         """(batches, batches with a failed equation, sub-batch equations, failed sub-batch equations)."""
         out = np.zeros(4, dtype=np.uint64)
         self._check(self.lib.mv_batch_counters(self.ctx, _p(out)), "mv_batch_counters")
+        return tuple(int(x) for x in out)
+
+    def batch_routes(self) -> Tuple[int, int, int]:
+        """(batches checked by a combined equation, batches verified signature by signature
+        because failures were dense, dense failures seen)."""
+        out = np.zeros(3, dtype=np.uint64)
+        self._check(self.lib.mv_batch_routes(self.ctx, _p(out)), "mv_batch_routes")
         return tuple(int(x) for x in out)
 
     def set_batch_groups(self, groups: int):

@@ -20,12 +20,14 @@ LIB = os.path.join(HERE, "libmysti_verify.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
-SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "wal.hip", "engine.cpp",
+SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "block_walk.hip", "wal.hip", "engine.cpp",
            "block_codec.cpp"]
 # per-source compiler flags of the product build (rust/mysti-verify-sys/build.rs mirrors them):
 # batch.hip under LLVM's max-ilp machine scheduler, config 2 +1.4% (294.4/294.7 -> 299.2/298.4 M
 # sigs/s, interleaved A/B, profiles/r04/ab_ilp.txt)
-SOURCE_FLAGS = {"batch.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+SOURCE_FLAGS = {"batch.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                "blake2b_lane.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                "ingest.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 HEADERS = ["asm_ops.h", "fe25519.h", "ge25519.h", "hash_dev.h", "scalar25519.h", "kernels.h", "block_codec.h", "tables.h", "carry32.h", "comb.h", "quad25519.h", "fe_q4.h", "fe_r16.h", "blake2b_quad.h", "block_verdict.h", "ingest_dev.h", "pt_r16.h"]
 
 

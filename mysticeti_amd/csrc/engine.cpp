@@ -37,29 +37,45 @@ namespace {
 
 constexpr int kBlockStage0 = mvk::BATCH_STAGES;  // parse, hash, verify, verdict
 constexpr int kGuardBatches = 64;  // batches cut into sub-batch equations after a failure
+// Dense failures (config 3: ~1% of the signatures bad, so every sub-batch equation fails and the
+// whole batch is re-verified after a wasted MSM): a guarded batch that failed in at least half
+// of its groups sends the next kSingleRun batches straight to the single path. Each of those
+// counts its rejected signatures; while a batch holds at least kDenseRejects of them the run is
+// renewed, otherwise the equation is tried again (guarded).
+constexpr int kSingleRun = 8;
+constexpr uint32_t kDenseRejects = 4;
+constexpr uint32_t kSingleMark = 0x80000000u;  // flag_groups entry of a single-path batch
 constexpr int kBlockStages = 4;
 constexpr int kWalStage0 = kBlockStage0 + kBlockStages;  // walk, crc
 static_assert(kWalStage0 + 2 == MV_NSTAGES, "stage count");
 
-// Buffers that grow retire the old allocation instead of freeing it: hipFree / hipHostFree
-// drain the whole device, which would wait for the resident online kernel (it lives while
-// online traffic flows) and for every other stream's calls. A retired block may still be read
-// by work in flight; it is freed by reap_retired (mv_destroy, mv_set_committee: with the
-// service stopped), when the device drain is harmless. (a buffer grown while the
-// service was live stalled the call for up to the kernel's lifetime.)
+// Buffers that grow retire the old allocation instead of freeing it at once: hipFree /
+// hipHostFree drain the whole device, which would wait for the resident online kernel (it lives
+// while online traffic flows) and for every other stream's calls. A retired block may still be
+// read by work in flight: `guard` (when set) is the completion event of the ring slot it served,
+// recorded after every call that used the slot, so its completion means no call still reads it
+// (a later record on the same slot completes later still); blocks without a guard served only
+// synchronous host-buffer calls, which had finished when they were retired. reap_ready frees
+// what is safe whenever the device's online service is not running (the drain is then bounded
+// by the calls in flight), and growth is geometric (x1.5), so a sequence of growing calls
+// retires O(log n) blocks, not one per call. reap_retired (mv_destroy,
+// mv_set_committee: the service stopped) frees the rest.
 struct Retired {
   int device;
   void* p;
   bool host;
+  hipEvent_t guard;
 };
 std::mutex g_retired_mu;
 std::vector<Retired> g_retired;
+std::atomic<int> g_retired_n{0};
 
-void retire(void* p, bool host) {
+void retire(void* p, bool host, hipEvent_t guard) {
   int d = 0;
   (void)hipGetDevice(&d);
   std::lock_guard<std::mutex> lk(g_retired_mu);
-  g_retired.push_back(Retired{d, p, host});
+  g_retired.push_back(Retired{d, p, host, guard});
+  g_retired_n.store((int)g_retired.size());
 }
 
 // Frees the retired blocks of `device` (its current device must be set; drains the device).
@@ -71,20 +87,52 @@ void reap_retired(int device) {
                                     [device](const Retired& r) { return r.device != device; });
     mine.assign(it, g_retired.end());
     g_retired.erase(it, g_retired.end());
+    g_retired_n.store((int)g_retired.size());
   }
   for (const Retired& r : mine) (void)(r.host ? hipHostFree(r.p) : hipFree(r.p));
 }
 
+// Frees the retired blocks of `device` that no call in flight can read (guard complete or
+// none); the caller has checked that no resident kernel runs on the device.
+void reap_ready(int device) {
+  if (g_retired_n.load(std::memory_order_relaxed) == 0) return;
+  std::vector<Retired> done;
+  {
+    std::lock_guard<std::mutex> lk(g_retired_mu);
+    auto it = std::stable_partition(g_retired.begin(), g_retired.end(), [device](const Retired& r) {
+      if (r.device != device) return true;
+      if (!r.guard) return false;
+      const hipError_t q = hipEventQuery(r.guard);
+      if (q != hipSuccess) (void)hipGetLastError();  // hipErrorNotReady: still in use
+      return q != hipSuccess;
+    });
+    done.assign(it, g_retired.end());
+    g_retired.erase(it, g_retired.end());
+    g_retired_n.store((int)g_retired.size());
+  }
+  for (const Retired& r : done) (void)(r.host ? hipHostFree(r.p) : hipFree(r.p));
+}
+
+// the size to allocate for `bytes` when `cap` is too small: x1.5 steps, exact on first use
+size_t grown(size_t cap, size_t bytes) { return std::max<size_t>({bytes, 4096, cap ? cap + cap / 2 : 0}); }
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
+  // guard: the completion event of the calls that used the buffer (see Retired), or null
+  hipError_t ensure(size_t bytes, hipEvent_t guard = nullptr) {
     if (bytes <= cap) return hipSuccess;
-    if (p) retire(p, false);
+    const size_t want = grown(cap, bytes);
+    if (p) retire(p, false, guard);
     p = nullptr;
     cap = 0;
-    size_t want = std::max<size_t>(bytes, 4096);
     hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess && want > bytes) {  // the geometric step does not fit: exactly
+      (void)hipGetLastError();
+      e = hipMalloc(&p, std::max<size_t>(bytes, 4096));
+      if (e == hipSuccess) cap = std::max<size_t>(bytes, 4096);
+      return e;
+    }
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -104,11 +152,17 @@ struct HostBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) retire(p, true);
+    const size_t want = grown(cap, bytes);
+    if (p) retire(p, true, nullptr);  // pinned staging: host-buffer calls only (synchronous)
     p = nullptr;
     cap = 0;
-    size_t want = std::max<size_t>(bytes, 4096);
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess && want > bytes) {
+      (void)hipGetLastError();
+      e = hipHostMalloc(&p, std::max<size_t>(bytes, 4096), hipHostMallocDefault);
+      if (e == hipSuccess) cap = std::max<size_t>(bytes, 4096);
+      return e;
+    }
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -161,6 +215,8 @@ struct Device {
   hipEvent_t slot_done[kSlots] = {};
   bool slot_used[kSlots] = {};
   int next_slot = 0;
+  // the single-path batches' rejected-signature counts, one device word per flag-ring entry
+  DevBuf rejects;
   // the batch flags of each call, copied to pinned host words behind it, in a ring larger
   // than the scratch ring: read (without blocking) once flag_ev has completed;
   // flag_groups[e] groups pending. A call blocks the host only with kFlagRing calls in flight.
@@ -249,6 +305,10 @@ struct mv_ctx {
   uint32_t base_groups = 1;
   uint32_t guard_groups = 8;
   std::atomic<int> guard_left{0};
+  // batches still to send straight to the single path (dense failures, kSingleRun), and the
+  // counts of batches by route
+  std::atomic<int> single_left{0};
+  std::atomic<uint64_t> single_batches{0}, dense_failures{0};
   // stage timing (mv_set_stage_timing): event sets of calls not yet read back
   bool stage_timing = false;
   std::mutex tmu;
@@ -390,6 +450,15 @@ void poll_flags(mv_ctx* ctx, Device& dev) {
     }
     dev.flag_groups[k] = 0;
     const uint32_t* f = dev.h_flags + k * Device::kFlagWords;
+    if (ng == kSingleMark) {  // a single-path batch: f[0] = its rejected signatures
+      if (f[0] >= kDenseRejects) {
+        ctx->single_left.store(kSingleRun);
+      } else {
+        ctx->single_left.store(0);
+        ctx->guard_left = kGuardBatches;  // back to the equation, guarded
+      }
+      continue;
+    }
     ctx->batches++;
     ctx->groups_run += ng;
     uint32_t bad = 0;
@@ -398,6 +467,10 @@ void poll_flags(mv_ctx* ctx, Device& dev) {
     if (!f[0]) {
       ctx->fallbacks++;
       ctx->guard_left = kGuardBatches;
+      if (ng >= 2 && 2 * bad >= ng && ctx->groups_fixed == 0) {  // dense: the MSM was wasted
+        ctx->dense_failures++;
+        ctx->single_left.store(kSingleRun);
+      }
     }
   }
 }
@@ -408,6 +481,13 @@ uint32_t pick_groups(mv_ctx* ctx) {
   ctx->guard_left.store(0);
   return ctx->base_groups;
 }
+
+mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
+                         const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s);
+mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig,
+                                   const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s,
+                                   const mvk::BlockVerdictOut* bv = nullptr, const mvk::BlockHashIn* hin = nullptr,
+                                   const mvk::BlockIngestIn* ing = nullptr);
 
 // Enqueues the batch path (batch.hip) for n signatures on stream s. flag_dst (optional,
 // device) receives the all-groups flag word.
@@ -430,11 +510,33 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
     HIPCHK(ctx, hipEventSynchronize(dev.flag_ev[fe]));
     poll_flags(ctx, dev);
   }
+  const bool com_a = d_key_idx && dev.committee_loaded && d_pk == dev.committee_pk.as<uint8_t>() &&
+                     !(ctx->flags & MV_FLAG_NO_COMB);
+  if (ctx->groups_fixed == 0 && ctx->single_left.load() > 0) {
+    // dense failures (kSingleRun): every signature verified alone, no combined equation; the
+    // rejected count decides whether the next batches try the equation again (poll_flags)
+    ctx->single_left--;
+    dev.next_slot = slot;  // no batch scratch used
+    if (gate && gate->n)
+      for (uint32_t c = 0; c < gate->n; c++) HIPCHK(ctx, hipStreamWaitEvent(s, gate->ready[c], 0));
+    mv_status st = com_a ? enqueue_committee_verify(ctx, dev, d_msg, d_sig, d_key_idx, n, d_status, s)
+                         : enqueue_verify(ctx, dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s);
+    if (st != MV_OK) return st;
+    HIPCHK(ctx, dev.rejects.ensure(sizeof(uint32_t) * Device::kFlagRing));
+    uint32_t* cnt = dev.rejects.as<uint32_t>() + fe;
+    HIPCHK(ctx, mvk::launch_count_rejects(d_status, n, cnt, s));
+    if (flag_dst) HIPCHK(ctx, hipMemsetAsync(flag_dst, 0, 4, s));  // no combination was checked
+    HIPCHK(ctx, hipMemcpyAsync(dev.h_flags + fe * Device::kFlagWords, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipEventRecord(dev.flag_ev[fe], s));
+    dev.flag_groups[fe] = kSingleMark;
+    ctx->single_batches++;
+    return MV_OK;
+  }
   if (dev.slot_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.slot_done[slot], 0));  // device-side order only
   const uint32_t groups = pick_groups(ctx);
   // scratch for the largest group count, so the adaptive policy never reallocates
-  HIPCHK(ctx, dev.bscr[slot].ensure(mvk::batch_scratch_bytes(n, mvk::BATCH_MAX_GROUPS)));
-  HIPCHK(ctx, dev.vscr[slot].ensure(mvk::verify_scratch_bytes(n)));
+  HIPCHK(ctx, dev.bscr[slot].ensure(mvk::batch_scratch_bytes(n, mvk::BATCH_MAX_GROUPS), dev.slot_done[slot]));
+  HIPCHK(ctx, dev.vscr[slot].ensure(mvk::verify_scratch_bytes(n), dev.slot_done[slot]));
   uint32_t key[10];
   memcpy(key, ctx->secret, 32);
   const uint64_t call = ctx->calls.fetch_add(1);
@@ -444,9 +546,8 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   std::vector<hipEvent_t> evs;
   mv_status st = make_events(ctx, mvk::BATCH_STAGES, evs);
   if (st != MV_OK) return st;
-  // committee keys: A comes from the comb tables built at mv_set_committee (no per-signature decode)
-  const bool com_a = d_key_idx && dev.committee_loaded && d_pk == dev.committee_pk.as<uint8_t>() &&
-                     !(ctx->flags & MV_FLAG_NO_COMB);
+  // committee keys (com_a): A comes from the comb tables built at mv_set_committee (no
+  // per-signature decode)
   hipEvent_t chain[2] = {};
   const bool chained = ctx->kn.prep_chain && !(gate && gate->n);
   if (chained) {
@@ -481,7 +582,7 @@ mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const u
   if (!dev.sscr_done[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.sscr_done[slot], hipEventDisableTiming));
   if (dev.sscr_used[slot]) HIPCHK(ctx, hipStreamWaitEvent(s, dev.sscr_done[slot], 0));
   // (growth retires the old buffer, which another stream's call may still read: no drain)
-  HIPCHK(ctx, dev.sscr[slot].ensure(mvk::verify_scratch_bytes(n)));
+  HIPCHK(ctx, dev.sscr[slot].ensure(mvk::verify_scratch_bytes(n), dev.sscr_done[slot]));
   HIPCHK(ctx, mvk::launch_verify(ctx->kn, d_msg, d_sig, d_pk, d_key_idx, n, dev.btab.p, dev.sscr[slot].p, d_status, s));
   HIPCHK(ctx, hipEventRecord(dev.sscr_done[slot], s));
   dev.sscr_used[slot] = true;
@@ -493,8 +594,8 @@ mv_status enqueue_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const u
 // bv: the block verdict fused into the comb kernel (the block path); null otherwise.
 mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig,
                                    const uint32_t* d_kidx, uint32_t n, uint8_t* d_status, hipStream_t s,
-                                   const mvk::BlockVerdictOut* bv = nullptr, const mvk::BlockHashIn* hin = nullptr,
-                                   const mvk::BlockIngestIn* ing = nullptr) {
+                                   const mvk::BlockVerdictOut* bv, const mvk::BlockHashIn* hin,
+                                   const mvk::BlockIngestIn* ing) {
   if (!(ctx->flags & MV_FLAG_NO_COMB)) {
     HIPCHK(ctx, mvk::launch_verify_comb(ctx->kn, d_msg, d_sig, dev.committee_pk.as<uint8_t>(), d_kidx, n, dev.combB.p,
                                         dev.combA.p, dev.keyok.as<uint8_t>(), d_status, s, bv, hin, ing));
@@ -546,7 +647,14 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   // (ingest_hash.hip; 2 waves/SIMD: config 4 measured 81 M blocks/s against 101 M for the
   // two-kernel form). The split comb path always uses the two-kernel form.
   const bool fused_ih = ctx->kn.blk_fused != 0;
-  const bool need_stage = split || !fused_ih;  // the two-kernel form stages P || sig
+  // batch-size calls (MV_BLK_WALK, default): k_block_check, then k_b2_walk hashes from the
+  // bincode itself, so no P || sig is staged (18.9 GB of HBM traffic less per 2^20
+  // config-4 blocks, and no stage buffer)
+  // MV_BLK_WALK=2 (default): k_block_walk does the parse, the checks and both digests in one
+  // pass over the bincode; 1: k_block_check + k_b2_walk (two passes)
+  const bool walk1 = batch && !split && !fused_ih && ctx->kn.blk_walk >= 2 && com.size() <= 512;
+  const bool walk = batch && !split && !fused_ih && ctx->kn.blk_walk && !walk1;
+  const bool need_stage = split || (!fused_ih && !walk && !walk1);  // the staged forms need P || sig
   o += need_stage ? al(buf_bytes + 256) : al(256);
   const size_t o_poff = o;
   o += al(8 * nn);
@@ -571,9 +679,9 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   if (!own && scr.cap < o) {
     // grow every ring slot at once, so the ring never allocates again at this size (the old
     // buffers are retired, not freed: another stream's call may still read them; no drain)
-    for (DevBuf& x : dev.blk) HIPCHK(ctx, x.ensure(o));
+    for (int k = 0; k < Device::kBlkSlots; k++) HIPCHK(ctx, dev.blk[k].ensure(o, dev.blk_done[k]));
   }
-  HIPCHK(ctx, scr.ensure(o));
+  HIPCHK(ctx, scr.ensure(o, own ? nullptr : dev.blk_done[slot]));
   char* b = scr.as<char>();
   uint8_t* stage = (uint8_t*)(b + o_stage);
   uint64_t* poff = (uint64_t*)(b + o_poff);
@@ -606,6 +714,10 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
                                com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed};
   if (ingest_in_comb) {
     HIPCHK(ctx, mark(1));
+  } else if (walk1) {
+    HIPCHK(ctx, mvk::launch_block_walk(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
+                                       com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
+    HIPCHK(ctx, mark(1));
   } else if (fused_ih && !split) {
     HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
                                               com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
@@ -623,9 +735,20 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
       if (!ax.ev[k]) HIPCHK(ctx, hipEventCreateWithFlags(&ax.ev[k], hipEventDisableTiming));
     hipStream_t aux = ax.stream;
     auto parse = [&](uint32_t lo, uint32_t hi, hipStream_t st) {
+      if (walk)
+        return mvk::launch_block_check(d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
+                                       com.epoch, com.quorum_threshold, poff + lo, plen + lo, sig + 64 * (size_t)lo,
+                                       kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
       return mvk::launch_block_parse(ctx->kn, d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
                                      com.epoch, com.quorum_threshold, stage, poff + lo, plen + lo, sig + 64 * (size_t)lo,
                                      kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
+    };
+    auto hash = [&](uint32_t lo, uint32_t hi) {
+      if (walk)
+        return mvk::launch_block_hash_walk(d_buf, d_off + lo, plen + lo, hi - lo, md + 32 * (size_t)lo,
+                                           bd + 32 * (size_t)lo, s);
+      return mvk::launch_block_hash(ctx->kn, stage, poff + lo, plen + lo, hi - lo, md + 32 * (size_t)lo,
+                                    bd + 32 * (size_t)lo, s);
     };
     HIPCHK(ctx, parse(0, h, s));
     HIPCHK(ctx, hipEventRecord(ax.ev[0], s));
@@ -633,9 +756,14 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, parse(h, n, aux));
     HIPCHK(ctx, hipEventRecord(ax.ev[1], aux));
     HIPCHK(ctx, mark(1));
-    HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff, plen, h, md, bd, s));
+    HIPCHK(ctx, hash(0, h));
     HIPCHK(ctx, hipStreamWaitEvent(s, ax.ev[1], 0));
-    HIPCHK(ctx, mvk::launch_block_hash(ctx->kn, stage, poff + h, plen + h, n - h, md + 32 * (size_t)h, bd + 32 * (size_t)h, s));
+    HIPCHK(ctx, hash(h, n));
+  } else if (walk) {
+    HIPCHK(ctx, mvk::launch_block_check(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
+                                        com.quorum_threshold, poff, plen, sig, kidx, facts, claimed, s));
+    HIPCHK(ctx, mark(1));
+    HIPCHK(ctx, mvk::launch_block_hash_walk(d_buf, d_off, plen, n, md, bd, s));
   } else {
     HIPCHK(ctx, mvk::launch_block_parse(ctx->kn, d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                         com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
@@ -2035,6 +2163,7 @@ const KnobDef kKnobs[] = {
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
     {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_OFF, false},
     {"MV_PREP_CHAIN", &mvk::Knobs::prep_chain, K_ON, false},
+    {"MV_BLK_WALK", &mvk::Knobs::blk_walk, K_ON, false},
     {"MV_BUCKET_BAL", &mvk::Knobs::bucket_bal, K_INT, false},
     {"MV_MSM_SEG_PCT", &mvk::Knobs::msm_seg_pct, K_INT, false},
     {"MV_STREAM_TAIL", &mvk::Knobs::stream_tail, K_OFF, false},
@@ -2087,6 +2216,33 @@ mvk::Knobs knobs_from_env() {
 extern "C" {
 
 const char* mv_version(void) { return "mysti_verify 0.2 gfx950"; }
+
+namespace {
+// Frees the retired buffers of `dev` that no call in flight reads (reap_ready), unless the
+// online service of its GPU is running (its kernel would hold the free's device drain). Called
+// with ctx->mu held at the start of the calls that grow buffers; o.mu is held across the check
+// and the frees, so no launch starts in between.
+void reap_idle(mv_ctx* ctx, Device& dev) {
+  if (g_retired_n.load(std::memory_order_relaxed) == 0) return;
+  std::shared_ptr<OnlineSvc> o;
+  for (Device& d : ctx->devs)
+    if (d.id == dev.id && d.online) o = d.online;  // one service per GPU (the first logical shard's)
+  if (!o) {
+    reap_ready(dev.id);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(o->mu);
+  if (o->stuck) return;
+  if (o->launched) {
+    const hipError_t q = hipEventQuery(o->exited);
+    if (q != hipSuccess) {
+      (void)hipGetLastError();  // running (hipErrorNotReady)
+      return;
+    }
+  }
+  reap_ready(dev.id);
+}
+}  // namespace
 
 mv_status mv_host_alloc(mv_ctx* ctx, uint64_t bytes, void** out) {
   if (!ctx || !out) return set_err(ctx, MV_E_INVALID_ARG, "bad host_alloc args");
@@ -2465,6 +2621,10 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
       if (key_idx[i] >= ctx->committee.size()) return set_err(ctx, MV_E_INVALID_ARG, "key_idx out of range");
   }
   const bool pinned = n && host_pinned(msg) && host_pinned(sig) && host_pinned(pk ? (const void*)pk : key_idx);
+  for (Device& d : ctx->devs) {
+    HIPCHK(ctx, hipSetDevice(d.id));
+    reap_idle(ctx, d);
+  }
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
     // large host-buffer batches, chunked with the copies of one chunk beside the verification
@@ -2730,6 +2890,7 @@ mv_status mv_dev_verify_blocks(mv_ctx* ctx, int device, const uint8_t* d_buf, ui
   Device* dev = find_dev(ctx, device);
   if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
   HIPCHK(ctx, hipSetDevice(dev->id));
+  reap_idle(ctx, *dev);
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
   return enqueue_blocks(ctx, *dev, d_buf, buf_bytes, d_off, d_len, n, d_status, d_msg_digest, d_block_digest, s);
 }
@@ -2743,6 +2904,7 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
   Device* dev = find_dev(ctx, device);
   if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
   HIPCHK(ctx, hipSetDevice(dev->id));
+  reap_idle(ctx, *dev);
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
   return enqueue_verify(ctx, *dev, d_msg, d_sig, d_pk, nullptr, n, d_status, s);
 }
@@ -2758,6 +2920,7 @@ mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_
   if (!dev) return set_err(ctx, MV_E_NO_DEVICE, "device not in context");
   if (n == 0) return MV_OK;
   HIPCHK(ctx, hipSetDevice(dev->id));
+  reap_idle(ctx, *dev);
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
   return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok);
 }
@@ -2770,11 +2933,20 @@ mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out) {
   return st;
 }
 
+mv_status mv_batch_routes(mv_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return MV_E_INVALID_ARG;
+  mv_status st = mv_batch_stats(ctx, out, nullptr);  // accounts every completed batch first
+  out[1] = ctx->single_batches.load();
+  out[2] = ctx->dense_failures.load();
+  return st;
+}
+
 mv_status mv_set_batch_groups(mv_ctx* ctx, uint32_t groups) {
   if (!ctx || groups > (uint32_t)mvk::BATCH_MAX_GROUPS) return set_err(ctx, MV_E_INVALID_ARG, "groups > 16");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->groups_fixed = groups;
   ctx->guard_left = 0;  // a new policy starts unguarded
+  ctx->single_left = 0;
   return MV_OK;
 }
 

@@ -68,6 +68,7 @@ struct Knobs {
   int64_t msm_seg_pct = 70;              // MV_MSM_SEG_PCT: streaming MSM's first segment (% of the batch; 0: per chunk)
   int64_t bucket_bal = 1;                // MV_BUCKET_BAL: equal entries per bucket-kernel lane (>1: entries per lane)
   int64_t prep_chain = 1;                // MV_PREP_CHAIN: a batch's k_bv_prep starts after the previous batch's
+  int64_t blk_walk = 2;                  // MV_BLK_WALK: batch-size block calls from the bincode: 2 one kernel (k_block_walk), 1 check + walk hash, 0 staged pre-image
 };
 
 size_t verify_scratch_bytes(uint32_t n);
@@ -81,6 +82,8 @@ hipError_t launch_verify(const Knobs& kn, const uint8_t* msg, const uint8_t* sig
 // (skip_group a multiple of 256; 0 = one group) are not verified when skip[g] != 0.
 // prep_pts (the batch path's fallback): R and A as k_bv_prep decoded them (A from the comb
 // tables prep_comb when it was summed per key), and prep's nonzero statuses kept.
+// *count = the number of items of status[0..n) equal to MV_SIG_INVALID; status 16-byte aligned
+hipError_t launch_count_rejects(const uint8_t* status, uint32_t n, uint32_t* count, hipStream_t s);
 hipError_t launch_sign(const uint8_t* seed, const uint8_t* msg, uint32_t n, const void* btab, uint8_t* pk,
                        uint8_t* sig, hipStream_t s);
 hipError_t launch_blake2b(const Knobs& kn, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n, uint8_t* out,
@@ -310,6 +313,21 @@ hipError_t launch_block_parse(const Knobs& kn, const uint8_t* buf, const uint64_
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s);
+// The walk form of batch-size block calls (MV_BLK_WALK): launch_block_parse's outputs but no
+// staged pre-image (k_block_check), then both digests from the bincode itself (k_b2_walk,
+// blake2b_lane.hip; blocks with pre_len 0 are skipped: the verdict zeroes their digests)
+hipError_t launch_block_check(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                              const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
+                              uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx, uint32_t* facts,
+                              uint8_t* claimed, hipStream_t s);
+hipError_t launch_block_hash_walk(const uint8_t* buf, const uint64_t* off, const uint64_t* plen, uint32_t n,
+                                  uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
+// block_walk.hip: launch_block_check's outputs and both digests in ONE pass over the bincode,
+// one lane per block (no pre-image staged or re-read); committees of <= 512 authorities
+hipError_t launch_block_walk(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
+                             const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
+                             uint8_t* sig, uint32_t* key_idx, uint32_t* facts, uint8_t* claimed, uint8_t* md,
+                             uint8_t* bd, hipStream_t s);
 // ingest_hash.hip: the block parse of launch_block_parse and both BLAKE2b digests in one
 // kernel, one quad per block, the pre-image streamed through LDS (never staged in HBM).
 // buf_bytes bounds the blocks' extent in buf (16 readable bytes past it).

@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "../../include/mysti_verify.h"
 #include "fe25519.h"
 #include "fe_q4.h"
 #include "fe_r16.h"
@@ -511,10 +512,43 @@ __global__ void __launch_bounds__(64) k_selftest(int op, const uint32_t* __restr
   for (int i = 0; i < 16; i++) out[16 * (size_t)gid + i] = y[i];
 }
 
+// The number of invalid signatures (status MV_SIG_INVALID: the failures a combined equation
+// can see; s >= l and undecodable points are excluded from it exactly) of n statuses, added to
+// *count (zeroed by the launcher): the single-path feedback of the batch policy (engine.cpp
+// enqueue_batch), one atomic per wave. 256 threads x 16 bytes per thread per block.
+__global__ void __launch_bounds__(256) k_count_rejects(const uint8_t* __restrict__ status, uint32_t n,
+                                                       uint32_t* __restrict__ count) {
+  const uint32_t base = (blockIdx.x * 256 + threadIdx.x) * 16;
+  uint32_t c = 0;
+  if (base + 16 <= n) {
+    const uint4 w = *reinterpret_cast<const uint4*>(status + base);
+    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      // bytes equal to 1 -> y's zero bytes; nonzero bytes of y get their high bit set
+      const uint32_t y = x[k] ^ 0x01010101u;
+      const uint32_t nz = (((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+      c += 4u - (uint32_t)__builtin_popcount(nz);
+    }
+  } else {
+    for (uint32_t i = base; i < n && i < base + 16; i++) c += status[i] == MV_SIG_INVALID;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += (uint32_t)__shfl_xor((int)c, m);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
 }  // namespace mv
 
 // ---------------------------------------------------------------- launchers
 namespace mvk {
+
+hipError_t launch_count_rejects(const uint8_t* status, uint32_t n, uint32_t* count, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess || n == 0) return e;
+  hipLaunchKernelGGL(mv::k_count_rejects, dim3((n + 4095) / 4096), dim3(256), 0, s, status, n, count);
+  return hipGetLastError();
+}
 
 size_t verify_scratch_bytes(uint32_t n) {
   size_t waves = (size_t)((n + 255) / 256) * 4;  // every wave of the 256-thread grid owns a slot

@@ -8,11 +8,15 @@ use std::path::PathBuf;
 use std::process::Command;
 
 const SOURCES: &[&str] = &[
-    "kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "wal.hip", "engine.cpp",
+    "kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "block_walk.hip", "wal.hip", "engine.cpp",
     "block_codec.cpp",
 ];
 // per-source flags (mysticeti_amd/build.py SOURCE_FLAGS)
-const SOURCE_FLAGS: &[(&str, &[&str])] = &[("batch.hip", &["-mllvm", "-amdgpu-sched-strategy=max-ilp"])];
+const SOURCE_FLAGS: &[(&str, &[&str])] = &[
+    ("batch.hip", &["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    ("blake2b_lane.hip", &["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+    ("ingest.hip", &["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+];
 
 fn main() {
     println!("cargo:rerun-if-env-changed=MYSTI_VERIFY_LIB_DIR");

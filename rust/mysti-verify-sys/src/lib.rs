@@ -98,6 +98,7 @@ extern "C" {
                         n: u32, d_out: *mut u32, stream: *mut c_void) -> i32;
     pub fn mv_batch_stats(ctx: *mut mv_ctx, batches: *mut u64, fallbacks: *mut u64) -> i32;
     pub fn mv_batch_counters(ctx: *mut mv_ctx, out: *mut u64) -> i32;
+    pub fn mv_batch_routes(ctx: *mut mv_ctx, out: *mut u64) -> i32;
     pub fn mv_set_batch_groups(ctx: *mut mv_ctx, groups: u32) -> i32;
     pub fn mv_set_stage_timing(ctx: *mut mv_ctx, enable: i32) -> i32;
     pub fn mv_stage_times(ctx: *mut mv_ctx, ms: *mut f64, calls: *mut u64, reset: i32) -> i32;

@@ -247,6 +247,79 @@ def test_adaptive_guard_after_a_failed_batch():
         assert (st == 0).all() and d == (1, 0, 1, 0)
 
 
+def routes_delta(engine, fn):
+    r0 = engine.batch_routes()
+    out = fn()
+    r1 = engine.batch_routes()
+    return out, tuple(b - a for a, b in zip(r0, r1))
+
+
+def test_dense_failures_route_to_the_single_path_and_back():
+    """Config 3 (~1% of the signatures bad): the first failed equation arms the guard; a guarded
+    batch failing in every group sends the next batches straight to per-signature verification
+    (no wasted MSM); a batch there with few invalid signatures sends the policy back to the
+    (guarded) equation. Verdicts stay exact on every route (crypto.rs:188, net_sync.rs:352-361)."""
+    with M.Engine(devices=(0,)) as eng:
+        n = 16384
+        msg, sig, pk = signed(eng, n, 33)
+        rng = np.random.default_rng(34)
+        bad = np.sort(rng.choice(n, n // 100, replace=False))
+        s_bad = sig.copy()
+        s_bad[bad, 40] ^= 0x10  # s stays < l, R decodes: only an equation or a single verify sees it
+        want = np.zeros(n, np.uint8)
+        want[bad] = 1
+        run = lambda s: lambda: eng.ed25519_verify(msg, s, pk)
+        st, d = routes_delta(eng, run(s_bad))  # one equation, failed: the guard is armed
+        assert (st == want).all() and d == (1, 0, 0)
+        st, d = routes_delta(eng, run(s_bad))  # 8 guarded equations, all failed: dense
+        assert (st == want).all() and d == (1, 0, 1)
+        st, d = routes_delta(eng, run(s_bad))  # straight to the single path
+        assert (st == want).all() and d == (0, 1, 0)
+        st, d = routes_delta(eng, run(s_bad))  # still dense: stays there
+        assert (st == want).all() and d == (0, 1, 0)
+        st, d = routes_delta(eng, run(sig))  # a clean batch on the single path ...
+        assert (st == 0).all() and d == (0, 1, 0)
+        st, d = counters_delta(eng, run(sig))  # ... sends the next one back to the guarded equation
+        assert (st == 0).all() and d == (1, 0, 8, 0)
+        st, d = routes_delta(eng, run(s_bad[:, :]))  # guarded, dense again: detected at once
+        assert (st == want).all() and d == (1, 0, 1)
+        eng.set_batch_groups(0)  # setting the policy clears the route too
+        st, d = routes_delta(eng, run(sig))
+        assert (st == 0).all() and d == (1, 0, 0)
+
+
+def test_dense_route_on_device_buffers():
+    """The same route through mv_dev_ed25519_verify_batch on three alternating streams (the
+    bench's adversarial leg): exact statuses on every call, d_batch_ok 0 on single-path calls."""
+    import torch
+
+    with M.Engine(devices=(0,)) as eng:
+        n = 8192
+        msg, sig, pk = signed(eng, n, 35)
+        bad = np.arange(7, n, 97)
+        sig = sig.copy()
+        sig[bad, 40] ^= 0x10
+        want = np.zeros(n, np.uint8)
+        want[bad] = 1
+        dev = torch.device("cuda", 0)
+        d_msg, d_sig, d_pk = (torch.from_numpy(x.copy()).to(dev) for x in (msg, sig, pk))
+        streams = [torch.cuda.Stream(dev) for _ in range(3)]
+        d_st = [torch.full((n,), 255, dtype=torch.uint8, device=dev) for _ in range(3)]
+        d_ok = [torch.full((1,), 7, dtype=torch.int32, device=dev) for _ in range(3)]
+        torch.cuda.synchronize()
+        r0 = eng.batch_routes()
+        for k in range(12):
+            j = k % 3
+            eng.dev_verify_batch(0, d_msg, d_sig, d_pk, d_st[j], d_ok[j], streams[j].cuda_stream)
+            if j == 2:
+                torch.cuda.synchronize()
+                for x in d_st:
+                    assert (x.cpu().numpy() == want).all()
+                assert all(int(x.item()) == 0 for x in d_ok)
+        d = [b - a for a, b in zip(r0, eng.batch_routes())]
+        assert d[1] >= 6 and d[2] >= 1 and d[0] + d[1] == 12
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("committee", [False, True])
 def test_pipelined_host_batches(engine, committee, pinned):

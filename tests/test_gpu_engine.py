@@ -394,6 +394,52 @@ def test_buffer_growth_does_not_wait_for_the_live_service(opts):
         assert eng.online_stats()[1] == l0  # the same launch served it
 
 
+def test_retired_buffers_stay_bounded_over_growing_calls():
+    """Calls of increasing size on the device API (three alternating streams, the bench's shape)
+    grow the scratch rings many times; the retired buffers are freed once the slots' last calls
+    are done (no resident kernel here), and growth is geometric, so the device memory held
+    stays within a small factor of what one call at the final size needs (before,
+    every growth kept the old allocation until mv_destroy)."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    n_max = 1 << 19
+    rng = np.random.default_rng(12)
+    seed = torch.from_numpy(rng.integers(0, 256, size=(n_max, 32), dtype=np.uint8)).to(dev)
+    msg = torch.from_numpy(rng.integers(0, 256, size=(n_max, 32), dtype=np.uint8)).to(dev)
+    pk = torch.empty((n_max, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((n_max, 64), dtype=torch.uint8, device=dev)
+    st = torch.empty((n_max,), dtype=torch.uint8, device=dev)
+    ok = torch.zeros(1, dtype=torch.int32, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+
+    def used():
+        torch.cuda.synchronize()
+        free, total = torch.cuda.mem_get_info(dev)
+        return total - free
+
+    def calls(eng, sizes):
+        for k, n in enumerate(sizes):
+            eng.dev_verify_batch(0, msg[:n], sig[:n], pk[:n], st[:n], ok, streams[k % 3].cuda_stream)
+        torch.cuda.synchronize()
+
+    with M.Engine(devices=(0,)) as eng:
+        eng.dev_sign(0, seed, msg, pk, sig, streams[0].cuda_stream)
+        torch.cuda.synchronize()
+        base = used()
+        calls(eng, [n_max] * 3)  # one call per slot at the final size
+        ref = used() - base
+        assert (st.cpu().numpy() == 0).all()
+    with M.Engine(devices=(0,)) as eng:
+        base = used()
+        sizes = [min(n_max, (int(8192 * 1.3 ** k) + 1023) & ~1023) for k in range(17)]
+        calls(eng, sizes + [n_max] * 6)  # ... then at the final size (the last retirees' slots done)
+        grown = used() - base
+        assert (st.cpu().numpy() == 0).all()
+    # without freeing the retirees the held memory is ~3-4x ref
+    assert grown <= 1.75 * ref + (64 << 20), (grown / 2**20, ref / 2**20)
+
+
 def test_context_with_online_service_is_destroyed_and_the_process_exits():
     """The driver's smoke shape in a fresh process: mv_create, one call through the resident
     service, mv_destroy, interpreter exit -- within a time limit, several times over (round 4's

@@ -15,15 +15,23 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["in_comb", "two_kernel", "fused", "separate_hash"], autouse=True)
+FORM = {"name": ""}
+
+
+@pytest.fixture(params=["in_comb", "two_kernel", "separate_hash", "batch_walk", "batch_check_walk", "batch_stage"],
+                autouse=True)
 def ingest_form(request, opts):
-    """Every test runs on the four device ingest forms: on small calls the parse and the
-    digests inside k_verify_comb16 (the default), k_block_ingest + the digests inside
-    k_verify_comb16 (MV_INGEST_IN_COMB=0), the fused k_block_ingest_hash (ingest_hash.hip,
-    MV_BLK_FUSED=1), and k_block_ingest + a separate k_b2_quad launch (MV_HASH_IN_COMB=0)."""
-    opts("MV_BLK_FUSED", request.param == "fused")
+    """Every test runs on the device ingest forms: on small calls the parse and the digests
+    inside k_verify_comb16 (the default), k_block_ingest + the digests inside k_verify_comb16
+    (MV_INGEST_IN_COMB=0) and k_block_ingest + a separate k_b2_quad launch (MV_HASH_IN_COMB=0);
+    at batch size (agree() repeats the inputs to >= MV_BATCH_MIN blocks) the one-pass walk
+    (k_block_walk: parse, checks and both digests from the bincode, the default), the check-only
+    ingest + the walk hash (k_block_check + k_b2_walk, MV_BLK_WALK=1) and the staged form
+    (k_block_ingest + k_b2_lane, MV_BLK_WALK=0)."""
     opts("MV_HASH_IN_COMB", request.param != "separate_hash")
     opts("MV_INGEST_IN_COMB", request.param != "two_kernel")
+    opts("MV_BLK_WALK", {"batch_stage": 0, "batch_check_walk": 1}.get(request.param, 2))
+    FORM["name"] = request.param
     return request.param
 
 
@@ -41,7 +49,19 @@ def committee(c):
 def agree(engine, host_engine, bins, pks, stakes, epoch):
     engine.set_committee(pks, stakes, epoch)
     host_engine.set_committee(pks, stakes, epoch)
-    st, md, bd = engine.verify_blocks(bins)
+    if FORM["name"].startswith("batch") and len(bins) < M.BATCH_MIN:
+        # the batch-size forms: the same blocks repeated to one batch-path call; every copy
+        # must get the verdict and digests of the first
+        n = len(bins)
+        reps = -(-M.BATCH_MIN // n)
+        st, md, bd = engine.verify_blocks(bins * reps)
+        for r in range(1, reps):
+            assert (st[r * n:(r + 1) * n] == st[:n]).all(), r
+            ok = st[:n] != M.BLOCK_PARSE_ERROR
+            assert (md[r * n:(r + 1) * n][ok] == md[:n][ok]).all() and (bd[r * n:(r + 1) * n][ok] == bd[:n][ok]).all(), r
+        st, md, bd = st[:n], md[:n], bd[:n]
+    else:
+        st, md, bd = engine.verify_blocks(bins)
     hst, hmd, hbd = host_engine.verify_blocks(bins)
     assert (st == hst).all(), np.nonzero(st != hst)[0][:10]
     for i in range(len(bins)):
