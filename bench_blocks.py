@@ -476,24 +476,33 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     roof = None
     from bench import pmc_traffic
 
-    # the batch-size hash kernel (blake2b_lane.hip; MV_B2_LANE=0: the quad kernel)
-    kname = "k_b2_quad" if os.environ.get("MV_B2_LANE") == "0" else "k_b2_lane"
-    if os.environ.get("MV_BLK_FUSED") == "1":  # the fused parse + hash kernel (the "parse" stage)
-        kname, hash_ms = "k_block_ingest_hash", stage_ms.get("parse")
+    # the dominant kernel: by default the one-pass walk (block_walk.hip, the "parse" stage: parse,
+    # checks and both digests); MV_BLK_WALK=1: the walk hash after the check-only ingest;
+    # MV_BLK_WALK=0: the staged form's hash (k_b2_lane, or k_b2_quad with MV_B2_LANE=0)
+    walk = os.environ.get("MV_BLK_WALK", "2")
+    if walk not in ("0", "1"):
+        kname, hash_ms = "k_block_walk", stage_ms.get("parse")
+    elif walk == "1":
+        kname = "k_b2_walk"
+    else:
+        kname = "k_b2_quad" if os.environ.get("MV_B2_LANE") == "0" else "k_b2_lane"
     traffic, traffic_src = pmc_traffic(kname, "c4")
     if hash_ms:
         ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
-        # kernel_ms is one launch over the call's n blocks (stage timing runs the hash as one
-        # launch); the PMC pass (tools/gpu.sh pmc:c4s1) launches it over 2^20 blocks, so its
-        # bytes are scaled to n: both numbers are per the same n blocks
+        # kernel_ms is one launch over the call's n blocks (stage timing runs it as one launch);
+        # the PMC pass (tools/gpu.sh pmc:c4s1) launches it over 2^20 blocks, so its bytes are
+        # scaled to n: both numbers are per the same n blocks
         traffic_n = round(traffic * n / (1 << 20)) if traffic else None
         roof = {"bound": "valu", "kernel": kname, "kernel_ms": hash_ms,
                 "achieved": round(ach / 1e12, 3), "peak": round(PEAK_VALU_OPS / 1e12, 2), "unit": "TOP/s",
                 "frac": round(ach / PEAK_VALU_OPS, 4), "traffic": traffic_n,
                 "per": f"one launch over {n} blocks (kernel_ms, traffic, achieved)",
                 "traffic_per_2^20_blocks": traffic, "traffic_source": traffic_src,
+                "traffic_over_bincode": round(traffic / ((1 << 20) * L), 3) if traffic else None,
+                "bincode_GBps": round(n * L / (hash_ms * 1e-3) / 1e9, 1),
                 "work_per_block": f"{comp_exec} BLAKE2b compressions executed (shared prefix; {comp_alg} "
-                                  f"algorithmic) x {W_BLAKE2B_OPS} ops"}
+                                  f"algorithmic) x {W_BLAKE2B_OPS} ops; the transcode and checks are not "
+                                  f"counted"}
     host_fed = None
     if int(os.environ.get("RANK", "0")) == 0 and host_blocks > 0:
         host_fed = config4_host_fed(eng, torch, dev, buf, off, ln, nb, span, host_blocks)

@@ -159,7 +159,8 @@ mv_status mv_queue_stats(mv_ctx* ctx, uint64_t* calls, uint64_t* passes);
  * calls of <= 64 blocks and <= 128 KB of bincode, every block inside the device ingest's 10-KB
  * window (short and config-4-shape long blocks alike; MV_ONLINE_LONG=0 restricts the service to
  * calls averaging < MV_COMB_SPLIT_BYTES per block), are posted to a ring in page-locked memory
- * that a kernel resident on a CU-masked stream polls; the caller's thread spins on its
+ * that a kernel resident on a highest-priority stream (a hardware queue of its own) polls; the
+ * caller's thread spins on its
  * request's done word (no launch, no event, no wake-up per call). The kernel exits after
  * MV_ONLINE_IDLE_US (default 10,000) without work and is relaunched by the next call; calls it
  * does not take (more blocks or bytes, a block past the window, MV_FLAG_NO_ONLINE, MV_ONLINE=0)

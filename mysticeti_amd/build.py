@@ -20,7 +20,7 @@ LIB = os.path.join(HERE, "libmysti_verify.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
-SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "block_walk.hip", "wal.hip", "engine.cpp",
+SOURCES = ["kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "blake2b_quad.hip", "blake2b_lane.hip", "block_walk.hip", "wal.hip", "engine.cpp",
            "block_codec.cpp"]
 # per-source compiler flags of the product build (rust/mysti-verify-sys/build.rs mirrors them):
 # batch.hip under LLVM's max-ilp machine scheduler, config 2 +1.4% (294.4/294.7 -> 299.2/298.4 M

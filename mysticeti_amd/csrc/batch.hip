@@ -1497,10 +1497,10 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
   e = hipMemsetAsync(bsum, 0, (size_t)BV_MAXG * BSUM_WORDS * 8, s);  // k_bv_prep accumulates per group
   if (e != hipSuccess) return e;
   const uint32_t seg = bucket_segment(kn);
-  const bool msm = gate && gate->n && gate->msm && gate->prep_done && G.count == 1 && seg == 1;
   const uint32_t nk = G.count * BV_NKG;
-  // bucket sums of the sorted entries of m signatures (acc: added to the sums in segT)
-  auto buckets = [&](uint64_t m, uint32_t acc) {
+  // bucket sums of the sorted entries of m signatures
+  auto buckets = [&](uint64_t m) {
+    const uint32_t acc = 0;
     if (seg == 1 && kn.bucket_bal > 0) {
       // equal entries per lane (the carries in segV: at most one per lane): 64 per lane, but at
       // least 3 waves per SIMD (196,608 lanes) while lanes keep >= 8 entries, so a small batch or
@@ -1518,80 +1518,15 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
                          G.count, seg, nw, acc, segV, segT);
     }
   };
-  if (msm) {
-    // streaming MSM: chunk c's preparation on aux (after its copy); once a segment's chunks are
-    // prepared, on s its bucket entries are sorted (the partition sort over the segment's
-    // signatures alone) and added into the persistent bucket sums segT; the reduction and the
-    // final follow the last segment
+  if (gate && gate->n) {
     const uint32_t* end = gate->end;
     if (end[gate->n - 1] != n) return hipErrorInvalidValue;
-    hipStream_t ps = gate->aux ? gate->aux : s;
-    if (gate->aux) {
-      if ((e = hipEventRecord(gate->fork, s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(gate->aux, gate->fork, 0)) != hipSuccess) return e;
-    }
-    // segments (gate->seg_end, ascending, the last = n; none: every chunk is one): the entries of
-    // a segment's signatures are sorted and added into the buckets once its last chunk is prepared
-    uint32_t sg = 0, seg_lo = 0;
-    for (uint32_t c = 0, lo = 0; c < gate->n; lo = end[c++]) {
-      const uint32_t hi = end[c], nc = hi - lo;
-      if (hi <= lo || lo % PART_CHUNK) return hipErrorInvalidValue;
-      if ((e = hipStreamWaitEvent(ps, gate->ready[c], 0)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_bv_prep, dim3((nc + 255) / 256), dim3(256), 0, ps, msg, sig, pk, key_idx, n, k, ca,
-                         pts, scal, bsum, status, lo / 256, G.cpg * PART_CHUNK);
-      while (gate->n_seg && sg + 1 < gate->n_seg && gate->seg_end[sg] <= lo) sg++;
-      const bool seg_done = !gate->n_seg || hi == n || hi >= gate->seg_end[sg];
-      if (!seg_done) continue;
-      if (gate->aux) {
-        if ((e = hipEventRecord(gate->prep_done[c], ps)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(s, gate->prep_done[c], 0)) != hipSuccess) return e;
-      }
-      const uint32_t m = hi - seg_lo;
-      const uint32_t c0 = seg_lo / PART_CHUNK, ncc = (m + PART_CHUNK - 1) / PART_CHUNK;
-      const BvGroups Gc{1, ncc};
-      const uint4* sc = scal + (size_t)seg_lo * SC_QUADS;
-      hipLaunchKernelGGL(k_part_count, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, agg ? 1u : 0u,
-                         pcount + (size_t)c0 * BV_NPG);
-      hipLaunchKernelGGL(k_part_scan, dim3(BV_NPG / 64), dim3(64 * SCAN_SUB), 0, s, pcount + (size_t)c0 * BV_NPG, ncc,
-                         Gc, poff + (size_t)c0 * BV_NPG, ptot);
-      hipLaunchKernelGGL(k_part_top, dim3(1), dim3(256), 0, s, ptot, (uint32_t)BV_NPG, pstart);
-      if (kn.scatter_lds)
-        hipLaunchKernelGGL(k_part_scatter_lds, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, pcount + (size_t)c0 * BV_NPG,
-                           poff + (size_t)c0 * BV_NPG, pstart, Gc, agg ? 1u : 0u, n, seg_lo, tmp);
-      else
-        hipLaunchKernelGGL(k_part_scatter, dim3(ncc), dim3(PART_CHUNK), 0, s, sc, m, poff + (size_t)c0 * BV_NPG, pstart,
-                           Gc, agg ? 1u : 0u, n, seg_lo, tmp);
-      if (kn.fine_lds)
-        hipLaunchKernelGGL(k_fine_sort_lds, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
-      else
-        hipLaunchKernelGGL(k_fine_sort, dim3(BV_NPG), dim3(FINE_NT), 0, s, tmp, pstart, 1u, ents, offs);
-      buckets(m, seg_lo ? 1u : 0u);
-      seg_lo = hi;
-    }
-    if (gate->aux) {  // (s has waited for every chunk's preparation)
-      if ((e = hipEventRecord(gate->join, gate->aux)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(s, gate->join, 0)) != hipSuccess) return e;
-    }
-    mark(1);
-    mark(2);
-  } else if (gate && gate->n) {
-    const uint32_t* end = gate->end;
-    if (end[gate->n - 1] != n) return hipErrorInvalidValue;
-    if (gate->aux) {
-      if ((e = hipEventRecord(gate->fork, s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(gate->aux, gate->fork, 0)) != hipSuccess) return e;
-    }
     for (uint32_t c = 0, lo = 0; c < gate->n; lo = end[c++]) {
       const uint32_t hi = end[c];
       if (hi <= lo || lo % 256 || (hi % 256 && hi != n)) return hipErrorInvalidValue;
-      hipStream_t ps = gate->aux && (c & 1) ? gate->aux : s;
-      if ((e = hipStreamWaitEvent(ps, gate->ready[c], 0)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_bv_prep, dim3((hi - lo + 255) / 256), dim3(256), 0, ps, msg, sig, pk, key_idx, n, k, ca,
+      if ((e = hipStreamWaitEvent(s, gate->ready[c], 0)) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_bv_prep, dim3((hi - lo + 255) / 256), dim3(256), 0, s, msg, sig, pk, key_idx, n, k, ca,
                          pts, scal, bsum, status, lo / 256, G.cpg * PART_CHUNK);
-    }
-    if (gate->aux) {
-      if ((e = hipEventRecord(gate->join, gate->aux)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(s, gate->join, 0)) != hipSuccess) return e;
     }
   } else {
     if (chain && chain[0] && (e = hipStreamWaitEvent(s, chain[0], 0)) != hipSuccess) return e;
@@ -1599,7 +1534,7 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
                        status, 0u, G.cpg * PART_CHUNK);
     if (chain && (e = hipEventRecord(chain[1], s)) != hipSuccess) return e;
   }
-  if (!msm) {
+  {
     mark(1);
     hipLaunchKernelGGL(k_part_count, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, n, agg ? 1u : 0u, pcount);
     hipLaunchKernelGGL(k_part_scan, dim3(G.count * (BV_NPG / 64)), dim3(64 * SCAN_SUB), 0, s, pcount, nchunk, G, poff,
@@ -1619,7 +1554,7 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
     // buckets per bucket-kernel lane: one per lane while the grid is small; with many groups,
     // a lane walks `seg` buckets and emits their running sums, so the bucket cells never go
     // through memory and the reduction stays the size of one group's
-    buckets(n, 0u);
+    buckets(n);
   }
   if (agg) {
     hipLaunchKernelGGL(k_bv_keyacc, dim3(nchunk), dim3(PART_CHUNK), 0, s, scal, key_idx, n, n_keys, kpart);

@@ -151,249 +151,6 @@ __global__ void __launch_bounds__(64) k_b2_lane(const uint8_t* __restrict__ buf,
   }
 }
 
-// ---------------------------------------------------------------- the walk hash
-// k_b2_walk: both block digests straight from the bincode, one lane per block, with no staged
-// pre-image (config 4: the check-only ingest reads the 9.9 GB of bincode per 2^20 blocks and
-// this kernel reads it again; the staged form also wrote and re-read 8.6 GB of pre-images).
-// The lane transcodes its block into its own LDS row as it hashes: before each compression it
-// emits whole pieces of the pre-image (crypto.rs:85-128; the same encodings as ingest_lane's
-// PreWriter) into the row until the block's 128 bytes are there; a piece that runs past them
-// stays in the row's slack and moves to the row's start after the compression. Bincode fields
-// are read with unaligned 8-byte loads and pieces written with unaligned 8-byte LDS stores,
-// so a field costs a load, a store and, for integers, a byte swap: a few percent of the
-// compression's ~2,000 instructions.
-// Only blocks the check-only ingest parsed (|P| = plen > 0) are hashed, so the walk trusts
-// their structure; others keep whatever their digest slots held (the verdict zeroes them).
-namespace walk {
-
-constexpr uint32_t ROW = 200;  // bytes per lane: one message block + the longest piece (72 B)
-
-MV_DEV uint64_t ld64(const uint8_t* p) {
-  uint64_t v;
-  __builtin_memcpy(&v, p, 8);
-  return v;
-}
-MV_DEV uint32_t ld32(const uint8_t* p) {
-  uint32_t v;
-  __builtin_memcpy(&v, p, 4);
-  return v;
-}
-MV_DEV void st64(uint8_t* q, uint64_t v) { __builtin_memcpy(q, &v, 8); }
-MV_DEV void st_be(uint8_t* q, const uint8_t* e) { st64(q, __builtin_bswap64(ld64(e))); }
-// BlockReference at e (authority, round, u64 length 32, digest) as its CryptoHash: 48 bytes
-MV_DEV void st_ref(uint8_t* q, const uint8_t* e) {
-  st_be(q, e);
-  st_be(q + 8, e + 8);
-#pragma unroll
-  for (int m = 0; m < 4; m++) st64(q + 16 + 8 * m, ld64(e + 24 + 8 * m));
-}
-
-enum : uint32_t { HDR, INC, NST, STMT, META, SIG, DONE };
-
-// Where the walk of one block stands: the phase, the element's bincode offset, the element
-// count and index of the phase; inside a statement, SHARE (payload bytes left at psrc) or
-// REJ2 (Reject(Some)'s second locator at psrc) is pending.
-struct Walk {
-  const uint8_t* blk;
-  uint32_t phase, src, cnt, k, sub, rem, psrc;
-};
-constexpr uint32_t SUB_NONE = 0, SUB_SHARE = 1, SUB_REJ2 = 2;
-
-// Emits the next piece of the pre-image at q (<= 72 bytes written; bytes past the returned
-// length may be overwritten by the next piece); returns its length.
-MV_DEV uint32_t piece(Walk& w, uint8_t* q) {
-  const uint8_t* b = w.blk;
-  if (w.phase == HDR) {  // own reference: author, round (types.rs:661-691)
-    st_be(q, b);
-    st_be(q + 8, b + 8);
-    w.cnt = (uint32_t)ld64(b + 56);
-    w.src = 64;
-    w.k = 0;
-    w.phase = w.cnt ? INC : NST;
-    return 16;
-  }
-  if (w.phase == INC) {  // includes
-    st_ref(q, b + w.src);
-    w.src += 56;
-    if (++w.k == w.cnt) w.phase = NST;
-    return 48;
-  }
-  if (w.phase == NST) {
-    w.cnt = (uint32_t)ld64(b + w.src);
-    w.src += 8;
-    w.k = 0;
-    w.sub = SUB_NONE;
-    w.phase = w.cnt ? STMT : META;
-    return 0;
-  }
-  if (w.phase == STMT) {
-    uint32_t n = 0;
-    bool done = true;
-    if (w.sub == SUB_SHARE) {  // Share payload, 64 bytes at a time
-      const uint8_t* e = b + w.psrc;
-#pragma unroll
-      for (int j = 0; j < 8; j++) st64(q + 8 * j, ld64(e + 8 * j));
-      n = min(w.rem, 64u);
-      w.rem -= n;
-      w.psrc += n;
-      done = w.rem == 0;
-    } else if (w.sub == SUB_REJ2) {  // Reject(Some): the second locator
-      const uint8_t* e = b + w.psrc;
-      st_ref(q, e);
-      st_be(q + 48, e + 56);
-      n = 56;
-    } else {
-      const uint8_t* e = b + w.src;
-      const uint32_t tag = ld32(e);
-      if (tag == 0) {  // Share(Transaction): tag 0, then the raw bytes
-        const uint32_t l = (uint32_t)ld64(e + 4);
-        q[0] = 0;
-        w.psrc = w.src + 12;
-        w.rem = l;
-        w.src += 12 + l;
-        n = 1;
-        done = l == 0;
-        w.sub = SUB_SHARE;
-      } else if (tag == 1) {  // Vote(locator, Accept | Reject(None) | Reject(Some(locator)))
-        const uint32_t vote = ld32(e + 68);
-        const uint32_t some = vote ? (uint32_t)e[72] : 0u;
-        q[0] = (uint8_t)(vote == 0 ? 1 : (some ? 3 : 2));
-        st_ref(q + 1, e + 4);
-        st_be(q + 49, e + 60);
-        n = 57;
-        if (some) {
-          w.psrc = w.src + 73;
-          w.sub = SUB_REJ2;
-          done = false;
-        }
-        w.src += vote == 0 ? 72 : (some ? 137 : 73);
-      } else {  // VoteRange(locator range): tag 4, locator, start, end
-        q[0] = 4;
-        st_ref(q + 1, e + 4);
-        st_be(q + 49, e + 60);
-        st_be(q + 57, e + 68);
-        w.src += 76;
-        n = 65;
-      }
-    }
-    if (done) {
-      w.sub = SUB_NONE;
-      if (++w.k == w.cnt) w.phase = META;
-    }
-    return n;
-  }
-  const uint8_t* e = b + w.src;
-  if (w.phase == META) {  // creation time (u128, big-endian), epoch marker, epoch
-    st_be(q, e + 8);
-    st_be(q + 8, e);
-    q[16] = e[16];
-    st_be(q + 17, e + 17);
-    w.phase = SIG;
-    return 25;
-  }
-  // SIG: the signature's 64 bytes (the bincode's u64 length 64 at e + 25)
-#pragma unroll
-  for (int j = 0; j < 8; j++) st64(q + 8 * j, ld64(e + 33 + 8 * j));
-  w.phase = DONE;
-  return 64;
-}
-
-}  // namespace walk
-
-// out0 = B2(P), out1 = B2(P || sig) of each block the check-only ingest parsed (plen[i] = |P|
-// > 0), from the bincode at buf + off[i]. 64 blocks per 64-lane workgroup. The step order is
-// Plan<true>'s (k_b2_lane): the shared prefix, P's final block (its digest from a copy of the
-// state), then the rest of P || sig.
-__global__ void __launch_bounds__(64) k_b2_walk(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
-                                                const uint64_t* __restrict__ plen, uint32_t n,
-                                                uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
-  __shared__ uint64_t rows[64 * walk::ROW / 8];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t i = blockIdx.x * 64 + lane;
-  const uint64_t L = i < n ? plen[i] : 0;
-  const bool live = L > 0;
-  Plan<true> pl;
-  pl.init(L, live);
-  const uint32_t nmax = b2q::wave_max(pl.nsteps);
-  uint8_t* const row = reinterpret_cast<uint8_t*>(rows) + walk::ROW * lane;
-  const uint64_t* const row64 = rows + (walk::ROW / 8) * lane;
-  walk::Walk w{buf + (live ? off[i] : 0), walk::HDR, 0, 0, 0, walk::SUB_NONE, 0, 0};
-  if (!live) w.phase = walk::DONE;
-  uint32_t pos = 0;  // row bytes written
-  uint64_t h[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) h[k] = IV[k];
-  h[0] ^= 0x01010020ull;  // depth 1, fanout 1, nn = 32
-  for (uint32_t s = 0; s < nmax; s++) {
-    uint64_t b, lim, t;
-    bool fin, mfin;
-    pl.at(s, b, lim, t, fin, mfin);
-    const uint64_t base = 128 * b;
-    const uint32_t lrel = lim > base ? (uint32_t)min(lim - base, (uint64_t)128) : 0u;
-    while (pos < lrel && w.phase != walk::DONE) pos += walk::piece(w, row + pos);
-    uint64_t m[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      uint64_t v = row64[j];
-      const uint32_t at = 8 * j;
-      if (at + 8 > lrel) v = at >= lrel ? 0ull : v & ((1ull << (8 * (lrel - at))) - 1);
-      m[j] = v;
-    }
-    uint64_t v[16];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      v[k] = h[k];
-      v[8 + k] = IV[k];
-    }
-    v[12] ^= t;
-    v[14] = fin ? ~v[14] : v[14];
-#define MV_LG(a, bb, c, d, x, y) \
-  a = add64(add64(a, bb), x);    \
-  d = ror32(d ^ a);              \
-  c = add64(c, d);               \
-  bb = ror24(bb ^ c);            \
-  a = add64(add64(a, bb), y);    \
-  d = ror16(d ^ a);              \
-  c = add64(c, d);               \
-  bb = ror63(bb ^ c);
-#pragma unroll
-    for (int r = 0; r < 12; r++) {
-      MV_LG(v[0], v[4], v[8], v[12], m[SIGMA[r][0]], m[SIGMA[r][1]])
-      MV_LG(v[1], v[5], v[9], v[13], m[SIGMA[r][2]], m[SIGMA[r][3]])
-      MV_LG(v[2], v[6], v[10], v[14], m[SIGMA[r][4]], m[SIGMA[r][5]])
-      MV_LG(v[3], v[7], v[11], v[15], m[SIGMA[r][6]], m[SIGMA[r][7]])
-      MV_LG(v[0], v[5], v[10], v[15], m[SIGMA[r][8]], m[SIGMA[r][9]])
-      MV_LG(v[1], v[6], v[11], v[12], m[SIGMA[r][10]], m[SIGMA[r][11]])
-      MV_LG(v[2], v[7], v[8], v[13], m[SIGMA[r][12]], m[SIGMA[r][13]])
-      MV_LG(v[3], v[4], v[9], v[14], m[SIGMA[r][14]], m[SIGMA[r][15]])
-    }
-#undef MV_LG
-    const bool step = s < pl.nsteps;
-    if (step && mfin) {  // B2(P): its final block on a copy of the state
-      uint64_t* o = reinterpret_cast<uint64_t*>(out0 + 32 * (size_t)i);
-#pragma unroll
-      for (int k = 0; k < 4; k++) o[k] = h[k] ^ v[k] ^ v[8 + k];
-    } else if (step) {
-#pragma unroll
-      for (int k = 0; k < 8; k++) h[k] ^= v[k] ^ v[8 + k];
-      // the block is done: the bytes emitted past it move to the row's start
-      if (pos >= 128) {
-#pragma unroll
-        for (int j = 0; j < 9; j++)
-          if (128 + 8 * j < pos) rows[(walk::ROW / 8) * lane + j] = row64[16 + j];
-        pos -= 128;
-      } else {
-        pos = 0;
-      }
-    }
-  }
-  if (live) {
-    uint64_t* o = reinterpret_cast<uint64_t*>(out1 + 32 * (size_t)i);
-#pragma unroll
-    for (int k = 0; k < 4; k++) o[k] = h[k];
-  }
-}
-
 }  // namespace b2l
 }  // namespace mv
 
@@ -412,13 +169,6 @@ hipError_t launch_block_hash_lane(const uint8_t* buf, const uint64_t* off, const
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL((mv::b2l::k_b2_lane<true>), dim3((n + 63) / 64), dim3(64), 0, s, buf, off, len, n, msg_out,
                      dig_out);
-  return hipGetLastError();
-}
-
-hipError_t launch_block_hash_walk(const uint8_t* buf, const uint64_t* off, const uint64_t* plen, uint32_t n,
-                                  uint8_t* msg_out, uint8_t* dig_out, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mv::b2l::k_b2_walk, dim3((n + 63) / 64), dim3(64), 0, s, buf, off, plen, n, msg_out, dig_out);
   return hipGetLastError();
 }
 

@@ -32,38 +32,33 @@ constexpr uint8_t WH[16] = {0, 1, 0, 2, 0, 3, 0, 1, 1, 2, 1, 2, 3, 3, 2, 3};
 template <int NS>
 constexpr uint32_t woff(int w) { return (uint32_t)WH[w] * 64u * NS + WG[w]; }  // u64 units from the string's base
 
-// LIN: the message block is 16 consecutive u64 (the fused ingest+hash kernel's pre-image
-// ring, ingest_hash.hip) instead of the class layout.
-template <int NS, bool LIN>
-constexpr uint32_t woff_any(int w) { return LIN ? (uint32_t)w : woff<NS>(w); }
-
 // The u64 offset lane q reads in round r, slot k (0/1: column step x/y, 2/3: diagonal step
 // x/y) is woff(SIGMA[r][8 (k >> 1) + 2q + (k & 1)]); packed 8 bits per lane (NS = 1) or 16
 // bits per lane (NS = 2).
-template <int NS, bool LIN>
+template <int NS>
 constexpr uint64_t msel(int r, int k) {
   uint64_t c = 0;
   for (int q = 0; q < 4; q++)
-    c |= (uint64_t)woff_any<NS, LIN>(SIGMA[r][8 * (k >> 1) + 2 * q + (k & 1)]) << ((NS == 1 ? 8 : 16) * q);
+    c |= (uint64_t)woff<NS>(SIGMA[r][8 * (k >> 1) + 2 * q + (k & 1)]) << ((NS == 1 ? 8 : 16) * q);
   return c;
 }
 template <int NS>
 struct Sel {
   uint64_t v[12][4];
 };
-template <int NS, bool LIN>
+template <int NS>
 constexpr Sel<NS> make_sel() {
   Sel<NS> s{};
   for (int r = 0; r < 12; r++)
-    for (int k = 0; k < 4; k++) s.v[r][k] = msel<NS, LIN>(r, k);
+    for (int k = 0; k < 4; k++) s.v[r][k] = msel<NS>(r, k);
   return s;
 }
-template <int NS, bool LIN = false>
-constexpr Sel<NS> SEL = make_sel<NS, LIN>();
-template <int NS, bool LIN = false>
+template <int NS>
+constexpr Sel<NS> SEL = make_sel<NS>();
+template <int NS>
 MV_DEV uint32_t sel_at(int r, int k, uint32_t q) {
-  if (NS == 1) return __builtin_amdgcn_ubfe((uint32_t)SEL<1, LIN>.v[r][k], 8 * q, 8);  // one v_bfe_u32
-  return (uint32_t)(SEL<NS, LIN>.v[r][k] >> (16 * q)) & 0xffffu;
+  if (NS == 1) return __builtin_amdgcn_ubfe((uint32_t)SEL<1>.v[r][k], 8 * q, 8);  // one v_bfe_u32
+  return (uint32_t)(SEL<NS>.v[r][k] >> (16 * q)) & 0xffffu;
 }
 
 constexpr uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
@@ -113,7 +108,7 @@ MV_DEV uint64_t qrot(uint64_t x) {
 // (< 2^64), fin = final block.
 // HOIST (the latency path: one wave per SIMD): no per-round barrier, so the scheduler issues
 // the message reads ahead of the G chains and the LDS latency leaves the critical path
-template <int NS, bool LIN = false, bool HOIST = false>
+template <int NS, bool HOIST = false>
 MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* const (&m)[NS], uint32_t q,
                      uint64_t iv0, uint64_t iv1, const uint64_t (&t)[NS], const bool (&fin)[NS]) {
   uint64_t va[NS], vb[NS], vc[NS], vd[NS];
@@ -131,8 +126,8 @@ MV_DEV void compress(uint64_t (&h0)[NS], uint64_t (&h1)[NS], const uint64_t* con
     // (what the scheduler does unchecked) doubles the VGPRs and halves the waves per SIMD
     if (!HOIST) asm volatile("" ::: "memory");
     const uint32_t qq = q;
-    const uint32_t i0 = sel_at<NS, LIN>(r, 0, qq), i1 = sel_at<NS, LIN>(r, 1, qq);
-    const uint32_t i2 = sel_at<NS, LIN>(r, 2, qq), i3 = sel_at<NS, LIN>(r, 3, qq);
+    const uint32_t i0 = sel_at<NS>(r, 0, qq), i1 = sel_at<NS>(r, 1, qq);
+    const uint32_t i2 = sel_at<NS>(r, 2, qq), i3 = sel_at<NS>(r, 3, qq);
     uint64_t x0[NS], y0[NS], x1[NS], y1[NS];
 #pragma unroll
     for (int k = 0; k < NS; k++) {
@@ -332,7 +327,7 @@ MV_DEV void quad_hash_range(uint32_t first, uint32_t count, const uint8_t* __res
       t[k] = 128ull * (s + 1);
       fin[k] = false;
     }
-    compress<NS, false, HOIST>(h0, h1, mrow, q, iv0, iv1, t, fin);
+    compress<NS, HOIST>(h0, h1, mrow, q, iv0, iv1, t, fin);
 #pragma unroll
     for (int k = 0; k < NS; k++)
 #pragma unroll
@@ -353,7 +348,7 @@ MV_DEV void quad_hash_range(uint32_t first, uint32_t count, const uint8_t* __res
       s0[k] = h0[k];
       s1[k] = h1[k];
     }
-    compress<NS, false, HOIST>(h0, h1, mrow, q, iv0, iv1, t, fin);
+    compress<NS, HOIST>(h0, h1, mrow, q, iv0, iv1, t, fin);
 #pragma unroll
     for (int k = 0; k < NS; k++) {
       if (DUAL && mfin[k] && s < pl[k].nsteps) reinterpret_cast<uint64_t*>(out0 + 32 * (size_t)idx[k])[q] = h0[k];

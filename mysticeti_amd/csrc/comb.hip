@@ -586,9 +586,6 @@ __global__ void __launch_bounds__(C16_THREADS) k_verify_comb16(const uint8_t* ms
 // loop also tests the launch's end, so all waves leave.
 constexpr uint32_t ON_BATCH = 64;  // the poller's window (requests it can move per pass): one wave's lanes
 constexpr uint32_t ON_COPY_UNROLL = 8;  // 16-B input loads per poller thread in flight
-constexpr uint32_t ON_MHDR = 64;        // a merge area's off[4] | len[4] before its input region
-static_assert(ON_MHDR + 4 * (16 + mvk::INGEST_WINDOW_BYTES + 32) <= mvk::ONLINE_IN_STRIDE,
-              "four one-block inputs fit a merge area's input region");
 static_assert(IG_WIN == mvk::INGEST_WINDOW_BYTES, "the host's eligibility test uses the ingest window");
 static_assert(ON_BATCH <= mvk::ONLINE_SLOTS && ON_BATCH <= 64 && mvk::ONLINE_SLOTS % 64 == 0,
               "the window's lanes cover distinct slots, one wave");
@@ -601,18 +598,11 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   __shared__ uint32_t pre[ON_BATCH + 1];  // 16-B chunk prefix over the batch's inputs
   __shared__ uint32_t nblk[ON_BATCH];
   __shared__ uint32_t qoff[ON_BATCH];     // request - ready of each moved request
-  __shared__ uint64_t dstp[ON_BATCH];     // where its input goes: its slot's scratch or a merge area
-  __shared__ uint32_t marea[ON_BATCH];    // merged: its area (else ~0u) and its input's byte offset
-  __shared__ uint32_t mbyte[ON_BATCH];    // in the area's input region
+  __shared__ uint64_t dstp[ON_BATCH];     // where its input goes: its slot's scratch
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
   uint64_t t_busy = t_start;
   uint64_t why = 0;  // wave 0: why the launch ends (mvk::ONLINE_EXIT_*)
-  // thread 0: merge groups formed by this launch (the area of the next one); a register, not
-  // memory: a store does not refresh this CU's L1 copy of the line, so a counter kept in HBM and
-  // read back through L1 repeated areas still in use (and lost their requests). Per launch is
-  // enough: every area of an earlier launch is finished when a launch starts.
-  uint64_t groups = 0;
   if (t == 0) {  // this launch's setup: tickets of earlier launches are void
     const unsigned long long tl = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&dev->jobs_head, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -709,30 +699,13 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    if (t == 0) {
-      // chunk prefix; and the merge groups (A.merge): the pass's one-block requests four to an
-      // area, each request's input copied into the area's input region (a merged job's ingest
-      // then reads and stages its blocks inside the area, as a request's does inside its slot)
-      uint32_t c = 0, gcnt = 0, garea = 0, gbytes = 0;
+    if (t == 0) {  // chunk prefix; each request's input goes to its slot's scratch
+      uint32_t c = 0;
       for (uint32_t i = 0; i < cnt; i++) {
         const uint32_t k = pre[i];
         pre[i] = c;
         c += k;
-        const uint32_t slot = (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS);
-        if (A.merge && nblk[i] == 1) {
-          if (gcnt == 0) {
-            garea = (uint32_t)(groups++ % mvk::ONLINE_SLOTS);
-            gbytes = 0;
-          }
-          marea[i] = garea;
-          mbyte[i] = gbytes;
-          dstp[i] = (uint64_t)(A.mscr + mvk::ONLINE_SCR_STRIDE * garea + ON_MHDR + gbytes);
-          gbytes += 16 * k;
-          if (++gcnt == C16_SIGS) gcnt = 0;
-        } else {
-          marea[i] = ~0u;
-          dstp[i] = (uint64_t)(A.scr + mvk::ONLINE_SCR_STRIDE * slot);
-        }
+        dstp[i] = (uint64_t)(A.scr + mvk::ONLINE_SCR_STRIDE * (uint32_t)((rdy + qoff[i]) % mvk::ONLINE_SLOTS));
       }
       pre[cnt] = c;
     }
@@ -779,40 +752,16 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
     __syncthreads();
     if (t == 0) {
       unsigned long long jt = __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // merge groups (formed above, in the same order): each area's off / len (the header) and
-      // its requests, then one job per area
-      uint32_t gcnt = 0, garea = 0;
-      auto close_group = [&]() {
-        dev->mcount[garea] = gcnt;
-        dev->jobs[jt % mvk::ONLINE_JOBS] = mvk::ONLINE_JOB_MERGED | garea;
-        jt++;
-        gcnt = 0;
-      };
       for (uint32_t i = 0; i < cnt; i++) {
         const uint64_t q = rdy + qoff[i];
         const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS), nj = (nblk[i] + C16_SIGS - 1) / C16_SIGS;
         dev->n[slot] = nblk[i];
         __hip_atomic_store(&dev->moved[slot], (unsigned long long)(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (nj == 0) {  // a void request: complete it here
+        if (nj == 0)  // a void request: complete it here
           __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else if (marea[i] != ~0u) {
-          garea = marea[i];
-          // the request's off[0] / len[0], just copied into the area by the other threads (read
-          // past this CU's L1, which may hold the area's previous contents)
-          uint8_t* area = A.mscr + mvk::ONLINE_SCR_STRIDE * garea;
-          uint64_t* hdr = reinterpret_cast<uint64_t*>(area + ON_MHDR + mbyte[i]);
-          const uint64_t o0 = __hip_atomic_load(hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t l0 = __hip_atomic_load(hdr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          uint64_t* ao = reinterpret_cast<uint64_t*>(area);
-          ao[gcnt] = mbyte[i] + 16 + o0;  // the block's bincode, from the input region (area + ON_MHDR)
-          ao[4 + gcnt] = l0;              // its length
-          dev->mq[garea][gcnt] = q;
-          if (++gcnt == C16_SIGS) close_group();
-        } else {
+        else
           for (uint32_t j = 0; j < nj; j++, jt++) dev->jobs[jt % mvk::ONLINE_JOBS] = ((unsigned long long)q << 8) | j;
-        }
       }
-      if (gcnt) close_group();
       __hip_atomic_store(&dev->ready, (unsigned long long)(rdy + adv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&dev->jobs_tail, jt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -823,68 +772,12 @@ MV_DEV void online_poller(const mvk::OnlineArgs& A) {
   }
 }
 
-// A merged job (OnlineArgs::merge): up to four one-block requests in merge area `area`: the
-// poller copied their inputs into the area's input region (area + ON_MHDR) and wrote the blocks'
-// off / len there (its header); the pre-images, digests and verdicts go to the area; then each
-// block's outputs to its request's page-locked slot (index 0) and, after one system-scope
-// fence, each request's done word.
-MV_DEV void online_merged_job(const mvk::OnlineArgs& A, uint32_t area) {
-  mvk::OnlineCtl* ctl = A.ctl;
-  mvk::OnlineDev* dev = A.dev;
-  const uint32_t t = threadIdx.x;
-  const uint32_t n = __builtin_amdgcn_readfirstlane(dev->mcount[area]);
-  uint8_t* sc = A.mscr + mvk::ONLINE_SCR_STRIDE * area;
-  const uint64_t* off = reinterpret_cast<const uint64_t*>(sc);
-  uint8_t* out = sc + mvk::ONLINE_O_OUT;
-  uint8_t* md = out;
-  uint8_t* bd = out + 32 * mvk::ONLINE_MAX_BLOCKS;
-  uint8_t* st = out + 64 * mvk::ONLINE_MAX_BLOCKS;
-  uint8_t* stage = sc + mvk::ONLINE_O_STAGE;
-  uint64_t* poff = reinterpret_cast<uint64_t*>(sc + mvk::ONLINE_O_POFF);
-  uint64_t* plen = reinterpret_cast<uint64_t*>(sc + mvk::ONLINE_O_PLEN);
-  uint8_t* sig = sc + mvk::ONLINE_O_SIG;
-  uint32_t* kidx = reinterpret_cast<uint32_t*>(sc + mvk::ONLINE_O_KIDX);
-  uint32_t* facts = reinterpret_cast<uint32_t*>(sc + mvk::ONLINE_O_FACTS);
-  uint8_t* claimed = sc + mvk::ONLINE_O_CLAIMED;
-  const mvk::BlockVerdictOut bv{facts, claimed, md, bd, st};
-  const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
-  // the blocks' bincode sits in the area's input region (area + ON_MHDR), so their staged
-  // pre-images (at the same offsets in `stage`) stay inside the area
-  const mvk::BlockIngestIn ing{sc + ON_MHDR, off, off + 4, A.stakes, A.n_auth, A.epoch, A.quorum_thr,
-                               stage, poff, plen, sig, kidx, facts, claimed};
-  comb16_wg(0, md, sig, A.pk, kidx, n, (const uint4*)A.combB, (const uint4*)A.combA, A.key_ok,
-            sc + mvk::ONLINE_O_SST, bv, hin, ing, nullptr);
-  __syncthreads();  // the job's digests and verdicts are in HBM (workgroup scope)
-  if (t < 16 * n) {  // block b's md (words 0..7) and bd (8..15) -> its request's slot, index 0
-    const uint32_t b = t / 16, w = t % 16;
-    const uint32_t slot = (uint32_t)(dev->mq[area][b] % mvk::ONLINE_SLOTS);
-    uint8_t* oh = A.out_host + mvk::ONLINE_OUT_STRIDE * slot;
-    const size_t src = w < 8 ? 32 * (size_t)b + 4 * w : 32 * ((size_t)mvk::ONLINE_MAX_BLOCKS + b) + 4 * (w - 8);
-    const size_t dst = w < 8 ? 4 * (size_t)w : 32 * (size_t)mvk::ONLINE_MAX_BLOCKS + 4 * (w - 8);
-    *reinterpret_cast<uint32_t*>(oh + dst) = *reinterpret_cast<const uint32_t*>(out + src);
-  } else if (t >= 64 && t < 64 + n) {
-    const uint32_t b = t - 64;
-    const uint32_t slot = (uint32_t)(dev->mq[area][b] % mvk::ONLINE_SLOTS);
-    A.out_host[mvk::ONLINE_OUT_STRIDE * slot + 64 * (size_t)mvk::ONLINE_MAX_BLOCKS] =
-        out[64 * (size_t)mvk::ONLINE_MAX_BLOCKS + b];
-  }
-  if (t < 128) __threadfence_system();  // the writers' outputs (waves 0, 1) before the done words
-  __syncthreads();
-  if (t < n) {
-    const uint64_t q = dev->mq[area][t];
-    const uint32_t slot = (uint32_t)(q % mvk::ONLINE_SLOTS);
-    __hip_atomic_store(&ctl->trace[slot][3], on_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&ctl->done[slot], q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __syncthreads();  // mcount / mq of this area are read before the next claim reuses LDS
-}
-
 // Workgroups 1..: take a ticket, wait until the ring's tail passes it, run that job from HBM,
 // hand its outputs to the host.
 MV_DEV void online_worker(const mvk::OnlineArgs& A) {
   mvk::OnlineCtl* ctl = A.ctl;
   mvk::OnlineDev* dev = A.dev;
-  __shared__ uint32_t job[4];  // kind (1 work, 2 exit, 3 merged job), request (merged: area) lo / hi, job
+  __shared__ uint32_t job[4];  // kind (1 work, 2 exit), request lo / hi, job
   const uint32_t t = threadIdx.x;
   const uint64_t t_start = on_now();
   bool setup = false;
@@ -909,15 +802,9 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
           if (tk < __hip_atomic_load(&dev->jobs_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const unsigned long long e = dev->jobs[tk % mvk::ONLINE_JOBS];
-            if (e & mvk::ONLINE_JOB_MERGED) {  // a merge area: q holds the area
-              q = e & 0xffffffffull;
-              j = 0;
-              kind = 3;
-            } else {
-              q = e >> 8;
-              j = (uint32_t)(e & 0xffu);
-              kind = 1;
-            }
+            q = e >> 8;
+            j = (uint32_t)(e & 0xffu);
+            kind = 1;
             break;
           }
           if (__hip_atomic_load(&dev->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
@@ -928,10 +815,6 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
         if (kind == 1 && j == 0)
           __hip_atomic_store(&ctl->trace[q % mvk::ONLINE_SLOTS][2], on_now(), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
-        if (kind == 3)
-          for (uint32_t b = 0; b < dev->mcount[q]; b++)
-            __hip_atomic_store(&ctl->trace[dev->mq[q][b] % mvk::ONLINE_SLOTS][2], on_now(), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
       }
       job[0] = kind;
       job[1] = (uint32_t)q;
@@ -944,10 +827,6 @@ MV_DEV void online_worker(const mvk::OnlineArgs& A) {
     const uint32_t j = __builtin_amdgcn_readfirstlane(job[3]);
     __syncthreads();  // job[] is rewritten by the next claim only after every wave read it
     if (kind == 2) return;
-    if (kind == 3) {
-      online_merged_job(A, (uint32_t)q);
-      continue;
-    }
     const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(q % mvk::ONLINE_SLOTS));
     const uint32_t n = __builtin_amdgcn_readfirstlane(dev->n[slot]);
     // the slot's HBM scratch (kernels.h layout): everything below is uniform address arithmetic

@@ -188,14 +188,18 @@ struct Device {
   // (three input buffer sets: the streamed pinned path's batches rotate over them)
   static constexpr int kPinBufs = 3;
   DevBuf pin_msg[kPinBufs], pin_sig[kPinBufs], pin_pk[kPinBufs], pin_st[kPinBufs];
-  HostBuf h_stage[2];
   hipEvent_t pin_free[kPinBufs] = {};
-  // pinned inputs: per-chunk "copied" events of the two input buffers (verify_host_streamed)
+  // pinned inputs: per-chunk "copied" events of the input buffers (verify_host_streamed)
   static constexpr int kMaxChunks = 64;
   hipEvent_t chunk_ev[kPinBufs][kMaxChunks] = {};
-  // the streaming MSM's per-chunk preparation events (aux -> compute stream) and fork / join
-  hipEvent_t prep_ev[kMaxChunks] = {};
-  hipEvent_t msm_fork = nullptr, msm_join = nullptr;
+  int pin_next = 0;  // the next batch's input buffer and compute stream (rotating across calls)
+  // Pinned signature calls in flight (verify_host_streamed): each holds one of kSigCalls status
+  // staging slots from its enqueue until its verdicts are copied out; the enqueue runs under
+  // ctx->mu, the wait does not, so one caller's copies run beside another's verification.
+  static constexpr int kSigCalls = 4;
+  HostBuf sig_stage[kSigCalls];
+  hipEvent_t sig_done[kSigCalls][2] = {};
+  bool sig_busy[kSigCalls] = {};
   // the batch path's preparation chain (MV_PREP_CHAIN): recorded after each batch's k_bv_prep;
   // the next batch's k_bv_prep waits for it (prep_chained: recorded at least once)
   hipEvent_t prep_chain = nullptr;
@@ -316,6 +320,7 @@ struct mv_ctx {
   double stage_ms[MV_NSTAGES] = {0};
   uint64_t stage_calls[MV_NSTAGES] = {0};
   std::atomic<bool> has_committee{false};
+  std::condition_variable sig_cv;  // a pinned signature call released its staging slot (Device::sig_busy)
   mvh::Committee committee;
   // block submission queue (mv_verify_blocks): concurrent callers' requests are merged into
   // one device pass by whichever caller finds the engine idle (flat combining)
@@ -605,10 +610,11 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
   return MV_OK;
 }
 
-// The device block pipeline on stream s (enqueue only): k_block_ingest_hash (or, for small
-// batches of long blocks, k_block_ingest -> k_hash_comb_pre) -> signatures (batch path for
-// >= MV_BATCH_MIN blocks, else committee verify) -> k_block_verdict. d_md / d_bd may be null
-// (scratch then).
+// The device block pipeline on stream s (enqueue only): batch-size calls k_block_walk (parse,
+// checks and both digests in one pass over the bincode) -> k_block_digest_gate -> batch path
+// -> k_block_verdict; smaller calls the committee comb kernels (which parse and hash their own
+// blocks on the online path; k_block_ingest -> k_hash_comb_pre -> k_comb_post for small
+// batches of long blocks). d_md / d_bd may be null (scratch then).
 // own: scratch owned by the caller (a submission-queue pass set, whose reuse is ordered by its
 // own completion event): no ring slot, no slot events (two runtime calls less per pass).
 mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_t buf_bytes, const uint64_t* d_off,
@@ -642,19 +648,12 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   const size_t nn = n;
   size_t o = 0;
   const size_t o_stage = o;
-  // k_block_ingest stages the pre-image in HBM, then k_b2_quad hashes it. MV_BLK_FUSED=1: the
-  // parse and both digests in one kernel with the pre-image streamed through LDS
-  // (ingest_hash.hip; 2 waves/SIMD: config 4 measured 81 M blocks/s against 101 M for the
-  // two-kernel form). The split comb path always uses the two-kernel form.
-  const bool fused_ih = ctx->kn.blk_fused != 0;
-  // batch-size calls (MV_BLK_WALK, default): k_block_check, then k_b2_walk hashes from the
-  // bincode itself, so no P || sig is staged (18.9 GB of HBM traffic less per 2^20
-  // config-4 blocks, and no stage buffer)
-  // MV_BLK_WALK=2 (default): k_block_walk does the parse, the checks and both digests in one
-  // pass over the bincode; 1: k_block_check + k_b2_walk (two passes)
-  const bool walk1 = batch && !split && !fused_ih && ctx->kn.blk_walk >= 2 && com.size() <= 512;
-  const bool walk = batch && !split && !fused_ih && ctx->kn.blk_walk && !walk1;
-  const bool need_stage = split || (!fused_ih && !walk && !walk1);  // the staged forms need P || sig
+  // Batch-size calls (MV_BLK_WALK=1, default): k_block_walk reads each block's bincode once and
+  // writes only the per-block outputs, so no P || sig is staged (18.9 GB of HBM
+  // traffic less per 2^20 config-4 blocks, and no stage buffer). MV_BLK_WALK=0: the staged form
+  // (k_block_ingest stages P || sig, k_b2_lane hashes it); small calls always stage.
+  const bool walk = batch && !split && ctx->kn.blk_walk && com.size() <= 512;
+  const bool need_stage = !walk;
   o += need_stage ? al(buf_bytes + 256) : al(256);
   const size_t o_poff = o;
   o += al(8 * nn);
@@ -704,7 +703,7 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   // short blocks on the online path: the digests are computed inside the committee verify
   // (k_verify_comb16's A wave hashes its blocks before the challenge), one launch less
   // (MV_HASH_IN_COMB=0, A/B: a separate hash launch)
-  const bool hash_in_comb = !fused_ih && !split && !batch && !(ctx->flags & MV_FLAG_NO_COMB) &&
+  const bool hash_in_comb = !split && !batch && !(ctx->flags & MV_FLAG_NO_COMB) &&
                             mvk::comb_short_chain(ctx->kn, n) && ctx->kn.hash_in_comb;
   const mvk::BlockHashIn hin{stage, poff, plen, md, bd};
   // ... and the parse too: k_verify_comb16 ingests its own blocks (one wave per block), so an
@@ -714,13 +713,9 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
                                com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed};
   if (ingest_in_comb) {
     HIPCHK(ctx, mark(1));
-  } else if (walk1) {
+  } else if (walk) {
     HIPCHK(ctx, mvk::launch_block_walk(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                        com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
-    HIPCHK(ctx, mark(1));
-  } else if (fused_ih && !split) {
-    HIPCHK(ctx, mvk::launch_block_ingest_hash(d_buf, buf_bytes, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(),
-                                              com.epoch, com.quorum_threshold, sig, kidx, facts, claimed, md, bd, s));
     HIPCHK(ctx, mark(1));
   } else if (batch && !split && !ctx->stage_timing && n >= 2 * MV_BATCH_MIN + 64 && ctx->kn.blk_pipe && (!own || own_aux)) {
     // Batch-size calls, two halves: the HBM-bound parse of the second half runs on another
@@ -735,18 +730,11 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
       if (!ax.ev[k]) HIPCHK(ctx, hipEventCreateWithFlags(&ax.ev[k], hipEventDisableTiming));
     hipStream_t aux = ax.stream;
     auto parse = [&](uint32_t lo, uint32_t hi, hipStream_t st) {
-      if (walk)
-        return mvk::launch_block_check(d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
-                                       com.epoch, com.quorum_threshold, poff + lo, plen + lo, sig + 64 * (size_t)lo,
-                                       kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
       return mvk::launch_block_parse(ctx->kn, d_buf, d_off + lo, d_len + lo, hi - lo, dev.stakes.as<uint64_t>(), com.size(),
                                      com.epoch, com.quorum_threshold, stage, poff + lo, plen + lo, sig + 64 * (size_t)lo,
                                      kidx + lo, facts + lo, claimed + 32 * (size_t)lo, st);
     };
     auto hash = [&](uint32_t lo, uint32_t hi) {
-      if (walk)
-        return mvk::launch_block_hash_walk(d_buf, d_off + lo, plen + lo, hi - lo, md + 32 * (size_t)lo,
-                                           bd + 32 * (size_t)lo, s);
       return mvk::launch_block_hash(ctx->kn, stage, poff + lo, plen + lo, hi - lo, md + 32 * (size_t)lo,
                                     bd + 32 * (size_t)lo, s);
     };
@@ -759,11 +747,6 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
     HIPCHK(ctx, hash(0, h));
     HIPCHK(ctx, hipStreamWaitEvent(s, ax.ev[1], 0));
     HIPCHK(ctx, hash(h, n));
-  } else if (walk) {
-    HIPCHK(ctx, mvk::launch_block_check(d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
-                                        com.quorum_threshold, poff, plen, sig, kidx, facts, claimed, s));
-    HIPCHK(ctx, mark(1));
-    HIPCHK(ctx, mvk::launch_block_hash_walk(d_buf, d_off, plen, n, md, bd, s));
   } else {
     HIPCHK(ctx, mvk::launch_block_parse(ctx->kn, d_buf, d_off, d_len, n, dev.stakes.as<uint64_t>(), com.size(), com.epoch,
                                         com.quorum_threshold, stage, poff, plen, sig, kidx, facts, claimed, s));
@@ -1184,7 +1167,7 @@ struct OnlineSvc {
   uint8_t* in = nullptr;
   uint8_t* out = nullptr;
   void *ctl_d = nullptr, *req_d = nullptr, *in_d = nullptr, *out_d = nullptr;  // device views
-  DevBuf dctl, scr, mscr;
+  DevBuf dctl, scr;
   std::unique_ptr<std::atomic<uint64_t>[]> freed;  // slot released by its owner: request + 1
   // Waiting callers (round 5). At most max_spinners callers spin on their done word; the others
   // sleep on a futex word of their slot, which the reaper thread sets and wakes once the done
@@ -1234,7 +1217,7 @@ bool online_eligible(mv_ctx* ctx, uint32_t n, uint64_t bytes, uint64_t longest) 
   const uint64_t split_bytes = (uint64_t)std::max<int64_t>(0, kn.comb_split_bytes);
   const uint64_t buf_bytes = (bytes + 16 + 15) & ~15ull;
   if (!kn.online_long && split_bytes && buf_bytes >= split_bytes * (uint64_t)n) return false;
-  if (kn.blk_fused || !kn.hash_in_comb || !kn.ingest_in_comb) return false;
+  if (!kn.hash_in_comb || !kn.ingest_in_comb) return false;
   return mvk::comb_short_chain(kn, n);
 }
 
@@ -1307,7 +1290,6 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   HIPCHK(ctx, o.dctl.ensure(sizeof(mvk::OnlineDev)));
   HIPCHK(ctx, hipMemset(o.dctl.p, 0, sizeof(mvk::OnlineDev)));
   HIPCHK(ctx, o.scr.ensure(mvk::ONLINE_SCR_STRIDE * kOnSlots));
-  HIPCHK(ctx, o.mscr.ensure(mvk::ONLINE_SCR_STRIDE * kOnSlots));  // merge areas (MV_ONLINE_MERGE)
   o.freed.reset(new std::atomic<uint64_t>[kOnSlots]);
   o.dwake.reset(new std::atomic<uint32_t>[kOnSlots]);
   o.sleep_q.reset(new std::atomic<uint64_t>[kOnSlots]);
@@ -1326,27 +1308,14 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     o.rstop = false;
     o.reaper = std::thread(online_reaper, &o);
   }
-  // CU mask: MV_ONLINE_CUS (default 64) CUs spread evenly over the chip; 0 = an ordinary stream
-  int cus = 0;
-  HIPCHK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev.id));
   // The service's stream needs a hardware queue of its own: a kernel queued behind the resident
-  // one on a shared queue would wait for it. Default (round 5): a stream of the highest priority
-  // (the runtime keeps a queue per priority level, and the engine's other streams are all of
-  // the default priority). Round 4 used a CU-masked stream (MV_ONLINE_CUS > 0, still
-  // selectable): tearing one down left a later hipStreamDestroy of an unrelated stream waiting
-  // forever on a runtime lock, in about 1 of 10 processes (the driver's round-4
-  // smoke; 0 stalls in 78 processes without it). MV_ONLINE_CUS = 0 and MV_ONLINE_PRIO = 0: an
-  // ordinary stream (shares a queue; A/B only).
-  int want = (int)ctx->kn.online_cus;
-  if (want > cus) want = cus;
-  if (want > 0 && want < cus) {
-    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-    for (int k = 0; k < want; k++) {
-      const int cu = (int)((int64_t)k * cus / want);
-      mask[cu / 32] |= 1u << (cu % 32);
-    }
-    HIPCHK(ctx, hipExtStreamCreateWithCUMask(&o.stream, (uint32_t)mask.size(), mask.data()));
-  } else if (ctx->kn.online_prio) {
+  // one on a shared queue would wait for it. A stream of the highest priority (the runtime keeps
+  // a queue per priority level, and the engine's other streams are all of the default
+  // priority). Round 4 used a CU-masked stream: tearing one down left a later hipStreamDestroy
+  // of an unrelated stream waiting forever on a runtime lock in about 1 of 10 processes
+  // (the driver's round-4 smoke); that form was removed in round 6.
+  // MV_ONLINE_PRIO = 0: an ordinary stream (shares a queue; A/B only).
+  if (ctx->kn.online_prio) {
     int least = 0, greatest = 0;
     HIPCHK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIPCHK(ctx, hipStreamCreateWithPriority(&o.stream, hipStreamNonBlocking, greatest));
@@ -1363,8 +1332,8 @@ mv_status online_init(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
     else
       (void)hipGetLastError();
   }
-  const int64_t ge = ctx->kn.online_wgs;  // resident workgroups (4-block jobs in flight; 0: 64, or one per CU of the mask)
-  o.grid = (uint32_t)(ge > 0 ? std::max<int64_t>(2, ge) : (want > 0 ? want : 64));  // >= 2: the poller + workers
+  const int64_t ge = ctx->kn.online_wgs;  // resident workgroups (4-block jobs in flight; 0: 64)
+  o.grid = (uint32_t)(ge > 0 ? std::max<int64_t>(2, ge) : 64);  // >= 2: the poller + workers
   o.grid = std::min<uint32_t>(o.grid, mvk::ONLINE_MAX_WGS);
   o.ready = true;
   return MV_OK;
@@ -1412,8 +1381,6 @@ mv_status online_ensure_running(mv_ctx* ctx, Device& dev, OnlineSvc& o) {
   a.in_host = static_cast<const uint8_t*>(o.in_d);
   a.out_host = static_cast<uint8_t*>(o.out_d);
   a.scr = o.scr.as<uint8_t>();
-  a.mscr = o.mscr.as<uint8_t>();
-  a.merge = ctx->kn.online_merge ? 1u : 0u;
   a.combB = dev.combB.p;
   a.combA = dev.combA.p;
   a.key_ok = dev.keyok.as<uint8_t>();
@@ -1524,7 +1491,6 @@ void online_release(OnlineSvc& o) {
     if (h) (void)hipHostFree(h);
   o.dctl.release();
   o.scr.release();
-  o.mscr.release();
   o.ready = false;
 }
 
@@ -1771,20 +1737,6 @@ void run_block_requests(mv_ctx* ctx, std::deque<mv_ctx::BlockReq*>& reqs, int se
   }
 }
 
-// memcpy with up to `threads` host threads (pageable -> pinned staging)
-void par_memcpy(void* dst, const void* src, size_t bytes, unsigned threads) {
-  if (threads <= 1 || bytes < (4u << 20)) {
-    memcpy(dst, src, bytes);
-    return;
-  }
-  std::vector<std::thread> th;
-  const size_t part = ((bytes + threads - 1) / threads + 4095) & ~(size_t)4095;
-  for (size_t o = part; o < bytes; o += part)
-    th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
-  memcpy(dst, src, std::min(part, bytes));
-  for (auto& t : th) t.join();
-}
-
 // True if p is page-locked host memory the DMA engines can read directly (mv_host_alloc,
 // hipHostMalloc, hipHostRegister, torch pin_memory).
 bool host_pinned(const void* p) {
@@ -1813,162 +1765,23 @@ bool pinned_range_holds(const void* p, uint64_t bytes) {
   return b >= a && b - a <= size && bytes <= size - (b - a);
 }
 
-// mv_ed25519_verify's batch path over [lo, hi) of the caller's arrays, in chunks of
-// >= MV_BATCH_MIN signatures on two streams, so the H2D copy of chunk c + 1 runs beside the
-// verification of chunk c (double-buffered device inputs, stream-ordered reuse); statuses
-// return by one D2H per chunk into pinned staging. pk rows by item, or committee keys by
-// key_idx. direct = true: the DMA engines read the caller's arrays themselves (pinned inputs,
-// or MV_PIPELINE=2 on pageable ones); false: the host first packs chunk c + 1 into pinned
-// staging with several threads (MV_PIPELINE=1, pageable inputs).
-mv_status verify_host_pipelined(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
-                                const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status, bool direct) {
-  const uint64_t m = hi - lo;
-  const int chunk_log2 = (int)std::min<int64_t>(30, std::max<int64_t>(10, ctx->kn.pipe_chunk_log2));  // MV_PIPE_CHUNK_LOG2
-  uint64_t chunks = (m + (1ull << chunk_log2) - 1) >> chunk_log2;
-  if (chunks < 2) chunks = 2;
-  uint64_t cs = ((m + chunks - 1) / chunks + 1023) & ~1023ull;
-  if (cs < MV_BATCH_MIN) cs = MV_BATCH_MIN;
-  if (cs > ctx->max_batch) cs = ctx->max_batch;
-  const size_t rowb = 32 + 64 + (pk ? 32 : 4);  // staged bytes per signature: msg | sig | pk or key index
-  for (int k = 0; k < 2; k++) {
-    if (!dev.pstream[k]) HIPCHK(ctx, hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking));
-    if (!dev.pin_free[k]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[k], hipEventDisableTiming));
-    HIPCHK(ctx, dev.pin_msg[k].ensure(32 * cs));
-    HIPCHK(ctx, dev.pin_sig[k].ensure(64 * cs));
-    HIPCHK(ctx, dev.pin_pk[k].ensure((pk ? 32 : 4) * cs));
-    HIPCHK(ctx, dev.pin_st[k].ensure(cs));
-    if (!direct) HIPCHK(ctx, dev.h_stage[k].ensure(rowb * cs));
-  }
-  HIPCHK(ctx, dev.h_out.ensure(m));
-  uint8_t* hst = dev.h_out.as<uint8_t>();
-  const uint8_t* dpk_com = dev.committee_pk.as<uint8_t>();
-  const unsigned hw = std::thread::hardware_concurrency();
-  const unsigned max_thr = (unsigned)std::max<int64_t>(1, ctx->kn.pipe_threads);  // MV_PIPE_THREADS: host staging threads
-  const unsigned threads = hw == 0 ? 4u : std::min(max_thr, hw);
-  bool staged_used[2] = {false, false};
-  const bool trace = ctx->kn.pipe_trace != 0;  // diagnostics (MV_PIPE_TRACE): host-side stage times
-  auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  const double t0 = now();
-  uint64_t c = 0;
-  for (uint64_t i = lo; i < hi; i += cs, c++) {
-    const uint32_t b = (uint32_t)(c & 1);
-    const uint32_t k = (uint32_t)std::min<uint64_t>(cs, hi - i);
-    hipStream_t st = dev.pstream[b];
-    // pinned staging b is free once chunk c - 2's H2D copies (on stream b) are done
-    const double ta = now();
-    if (staged_used[b]) HIPCHK(ctx, hipEventSynchronize(dev.pin_free[b]));
-    const double tb = now();
-    const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);
-    if (direct) {
-      HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, msg + 32 * i, 32 * (size_t)k, hipMemcpyHostToDevice, st));
-      HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, sig + 64 * i, 64 * (size_t)k, hipMemcpyHostToDevice, st));
-      HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, src_pk, (pk ? 32 : 4) * (size_t)k, hipMemcpyHostToDevice, st));
-    } else {
-      uint8_t* hs = dev.h_stage[b].as<uint8_t>();
-      par_memcpy(hs, msg + 32 * i, 32 * (size_t)k, threads);
-      par_memcpy(hs + 32 * cs, sig + 64 * i, 64 * (size_t)k, threads);
-      par_memcpy(hs + 96 * cs, src_pk, (pk ? 32 : 4) * (size_t)k, threads);
-      HIPCHK(ctx, hipMemcpyAsync(dev.pin_msg[b].p, hs, 32 * (size_t)k, hipMemcpyHostToDevice, st));
-      HIPCHK(ctx, hipMemcpyAsync(dev.pin_sig[b].p, hs + 32 * cs, 64 * (size_t)k, hipMemcpyHostToDevice, st));
-      HIPCHK(ctx, hipMemcpyAsync(dev.pin_pk[b].p, hs + 96 * cs, (pk ? 32 : 4) * (size_t)k, hipMemcpyHostToDevice, st));
-      HIPCHK(ctx, hipEventRecord(dev.pin_free[b], st));
-      staged_used[b] = true;
-    }
-    mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
-                                 pk ? dev.pin_pk[b].as<uint8_t>() : dpk_com,
-                                 pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), st,
-                                 nullptr);
-    if (rc != MV_OK) return rc;
-    HIPCHK(ctx, hipMemcpyAsync(hst + (i - lo), dev.pin_st[b].p, k, hipMemcpyDeviceToHost, st));
-    if (trace) fprintf(stderr, "[pipe] chunk %lu: wait %.0f us, stage+enqueue %.0f us\n", (unsigned long)c, tb - ta, now() - tb);
-  }
-  const double t1 = now();
-  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[0]));
-  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[1]));
-  if (trace) fprintf(stderr, "[pipe] issue %.0f us, drain %.0f us, threads %u\n", t1 - t0, now() - t1, threads);
-  poll_flags(ctx, dev);
-  memcpy(status + lo, hst, m);
-  return MV_OK;
-}
-
-// mv_ed25519_verify's batch path over [lo, hi) of pinned caller arrays, zero-copy: k_bv_prep
-// reads msg / sig / pk straight from the page-locked host memory over PCIe (each input byte
-// once, the reads spread over the kernel by its waves) and the other kernels work on device
-// scratch, so there is no copy phase and no chunk gating; two batches on two compute streams
-// (batch 2's prep runs beside batch 1's sort, buckets and tail). false: the caller's pointers
-// have no device mapping (the caller falls back to verify_host_streamed).
-bool verify_host_zerocopy(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
-                          const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status, mv_status& rc) {
-  auto dptr = [](const void* h) -> const uint8_t* {
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, const_cast<void*>(h), 0) != hipSuccess || !d) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    return static_cast<const uint8_t*>(d);
-  };
-  const uint8_t* dm = dptr(msg + 32 * lo);
-  const uint8_t* ds = dptr(sig + 64 * lo);
-  const uint8_t* dk = pk ? dptr(pk + 32 * lo) : dptr(key_idx + lo);
-  if (!dm || !ds || !dk) return false;
-  rc = MV_OK;
-  const uint64_t m = hi - lo;
-  const double first_frac = ctx->kn.zc_first;  // the first batch's share (MV_ZC_FIRST, A/B)
-  uint64_t b0 = m <= MV_BATCH_MIN * 2 ? m : (((uint64_t)(m * first_frac) + 1023) & ~1023ull);
-  if (b0 > ctx->max_batch) b0 = ctx->max_batch;
-  if (m - b0 > ctx->max_batch) b0 = m - ctx->max_batch;  // two batches at most per max_batch pair
-  for (int b = 0; b < 2; b++) {
-    if (!dev.pstream[b]) HIPCHK_RC(ctx, rc, hipStreamCreateWithFlags(&dev.pstream[b], hipStreamNonBlocking));
-    HIPCHK_RC(ctx, rc, dev.pin_st[b].ensure(std::max<uint64_t>(b0, m - b0) + 256));
-  }
-  HIPCHK_RC(ctx, rc, dev.h_out.ensure(m));
-  uint8_t* hst = dev.h_out.as<uint8_t>();
-  uint64_t i = 0;
-  for (int t = 0; i < m && rc == MV_OK; t++) {
-    const uint64_t k = t == 0 ? b0 : std::min<uint64_t>(m - i, ctx->max_batch);
-    hipStream_t cs = dev.pstream[t & 1];
-    if (t >= 2) HIPCHK_RC(ctx, rc, hipStreamSynchronize(cs));  // pin_st[t & 1] reuse (more than two batches)
-    rc = enqueue_batch(ctx, dev, dm + 32 * i, ds + 64 * i, pk ? dk + 32 * i : dev.committee_pk.as<uint8_t>(),
-                       pk ? nullptr : reinterpret_cast<const uint32_t*>(dk) + i, (uint32_t)k,
-                       dev.pin_st[t & 1].as<uint8_t>(), cs, nullptr);
-    if (rc == MV_OK)
-      HIPCHK_RC(ctx, rc, hipMemcpyAsync(hst + i, dev.pin_st[t & 1].p, k, hipMemcpyDeviceToHost, cs));
-    i += k;
-  }
-  // drain what was queued (it reads the caller's memory) before returning, error or not
-  const hipError_t e0 = hipStreamSynchronize(dev.pstream[0]), e1 = hipStreamSynchronize(dev.pstream[1]);
-  if (rc == MV_OK && (e0 != hipSuccess || e1 != hipSuccess))
-    rc = set_err(ctx, MV_E_HIP, std::string("zero-copy verify: ") + hipGetErrorString(e0 != hipSuccess ? e0 : e1));
-  if (rc != MV_OK) return true;
-  poll_flags(ctx, dev);
-  memcpy(status + lo, hst, m);
-  return true;
-}
-
 // mv_ed25519_verify's batch path over [lo, hi) of pinned caller arrays, in a few large
 // batches (two by default) on two compute streams. The DMA engines copy a batch's inputs
 // chunk by chunk on a copy stream, and k_bv_prep of chunk c starts as soon as chunk c has
 // landed, so the PCIe copy overlaps the preparation; batch t + 1's copy and preparation run
 // beside batch t's sort, buckets and tail (two input buffers, reuse ordered by events).
+// Enqueue only (ctx->mu held): the statuses land in dev.sig_stage[slot], complete once both of
+// dev.sig_done[slot] have; the caller waits for them without the lock (mv_ed25519_verify).
 mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk,
-                               const uint32_t* key_idx, uint64_t lo, uint64_t hi, uint8_t* status) {
+                               const uint32_t* key_idx, uint64_t lo, uint64_t hi, int slot) {
   const int chunk_log2 = (int)std::min<int64_t>(24, std::max<int64_t>(8, ctx->kn.stream_chunk_log2));  // MV_STREAM_CHUNK_LOG2
   const uint64_t m = hi - lo;
   // Batch sizes: shares of the call (MV_STREAM_FRACS, separated by ',' or '/'; default 0.7,0.3). The
   // last batch's prep, sort, buckets and tail follow the last copy, so the shares decrease;
   // every batch is whole 1,024s, >= MV_BATCH_MIN and <= max_batch (more batches when needed).
-  // Streaming MSM (MV_STREAM_MSM=1, off by default): the call is one batch whose chunks are sorted
-  // and added into persistent buckets during the copy window in segments (launch_verify_batch,
-  // ChunkGate::msm; MV_MSM_SEG_PCT), so only the last segment's sort and buckets, the reduction
-  // and the final follow the last copy. Measured slower: per chunk 181-196 M/s, in two segments
-  // 197-198 M/s against 208 M/s for two batches on two streams (2^20 pinned signatures,
-  // profiles/r05/e2e_msm.txt, e2e_msm_segments.txt): the call is bound by its compute (the
-  // preparations take the chip through the copy window, so the first segment's buckets run
-  // after it either way; profiles/r05/e2e/timeline_*.txt).
-  const bool msm = ctx->kn.stream_msm && m <= ctx->max_batch && ctx->kn.bv_seg <= 1;
-  const std::vector<double> fracs = msm ? std::vector<double>{1.0}
-                                        : std::vector<double>(ctx->kn.stream_fracs,
-                                                              ctx->kn.stream_fracs + ctx->kn.n_stream_fracs);
+  // (A streaming MSM -- one batch whose chunks are sorted and bucketed during the copy window --
+  // measured slower, 181-198 against 208 M/s, and was removed in round 6: DESIGN.md 13.)
+  const std::vector<double> fracs(ctx->kn.stream_fracs, ctx->kn.stream_fracs + ctx->kn.n_stream_fracs);
   std::vector<uint32_t> sizes;
   {
     double tot = 0.0;
@@ -1994,9 +1807,7 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   uint32_t chunk = 1u << chunk_log2;
   while ((cap + chunk - 1) / chunk > (uint32_t)Device::kMaxChunks / 2) chunk <<= 1;
   // chunk schedule of a batch of k: the first batch starts with small chunks (2^14, 2^15, ...
-  // signatures), so the chip starts preparing after ~40 us of copying instead of a whole chunk's.
-  // MV_STREAM_TAIL: the last chunk halved down to 2^14 signatures (2^16, 2^15, 2^14, 2^14 of a
-  // 2^17 chunk), so the preparation that follows the last copy is a short one
+  // signatures), so the chip starts preparing after ~40 us of copying instead of a whole chunk's
   auto schedule = [&](int first, uint32_t k) {
     std::vector<uint32_t> cut;
     uint32_t o = 0, c = first ? std::min<uint32_t>(chunk, 1u << 14) : chunk;
@@ -2004,14 +1815,6 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
       cut.push_back(o);
       o += c;
       if (c < chunk) c *= 2;
-    }
-    if (ctx->kn.stream_tail && cut.size() >= 1) {
-      uint32_t a = cut.back(), left = k - a;
-      while (left > (1u << 14) && (left / 2) % 1024 == 0 && cut.size() + 2 < (size_t)Device::kMaxChunks) {
-        a += left / 2;
-        left -= left / 2;
-        cut.push_back(a);
-      }
     }
     cut.push_back(k);
     return cut;
@@ -2023,13 +1826,17 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     if (!dev.pin_free[b]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.pin_free[b], hipEventDisableTiming));
     for (int c = 0; c < Device::kMaxChunks; c++)
       if (!dev.chunk_ev[b][c]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.chunk_ev[b][c], hipEventDisableTiming));
-    HIPCHK(ctx, dev.pin_msg[b].ensure(32 * (size_t)cap));
-    HIPCHK(ctx, dev.pin_sig[b].ensure(64 * (size_t)cap));
-    HIPCHK(ctx, dev.pin_pk[b].ensure(kb * cap));
-    HIPCHK(ctx, dev.pin_st[b].ensure(cap));
+    // (a buffer grown while another call's batch still reads it is retired behind pin_free[b])
+    HIPCHK(ctx, dev.pin_msg[b].ensure(32 * (size_t)cap, dev.pin_free[b]));
+    HIPCHK(ctx, dev.pin_sig[b].ensure(64 * (size_t)cap, dev.pin_free[b]));
+    HIPCHK(ctx, dev.pin_pk[b].ensure(kb * cap, dev.pin_free[b]));
+    HIPCHK(ctx, dev.pin_st[b].ensure(cap, dev.pin_free[b]));
   }
-  HIPCHK(ctx, dev.h_out.ensure(m));
-  uint8_t* hst = dev.h_out.as<uint8_t>();
+  for (int k = 0; k < 2; k++)
+    if (!dev.sig_done[slot][k]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.sig_done[slot][k], hipEventDisableTiming));
+  HIPCHK(ctx, dev.sig_stage[slot].ensure(m));
+  uint8_t* hst = dev.sig_stage[slot].as<uint8_t>();
+  bool used[2] = {false, false};
   // copies on the device stream (host-buffer signature calls are serialised by ctx->mu, and the
   // block passes have streams of their own); batch t computes on pstream[t & 1]. mv_create makes
   // these three streams first, so they sit on three distinct hardware queues (GPU_MAX_HW_QUEUES
@@ -2038,10 +1845,14 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
   hipStream_t xs = dev.stream;
   uint64_t i = lo;
   for (size_t t = 0; t < sizes.size(); i += sizes[t], t++) {
-    const int b = (int)(t % Device::kPinBufs);
-    hipStream_t cs = dev.pstream[t & 1];
+    // input buffers and compute streams rotate across calls too, so a second caller's first batch
+    // copies into a buffer the first caller's batches are not using
+    const int rot = dev.pin_next++;
+    const int b = rot % Device::kPinBufs, ci = rot & 1;
+    hipStream_t cs = dev.pstream[ci];
+    used[ci] = true;
     const uint32_t k = sizes[t];
-    // buffer b is free once batch t - kPinBufs (or the previous call's batch on it) is done
+    // buffer b is free once the last batch that used it (this call's or another's) is done
     HIPCHK(ctx, hipStreamWaitEvent(xs, dev.pin_free[b], 0));
     const uint8_t* src_pk = pk ? pk + 32 * i : (const uint8_t*)(key_idx + i);
     const std::vector<uint32_t> cut = schedule(t == 0, k);
@@ -2060,28 +1871,7 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
     }
     // every chunk's prep on cs (a second prep stream per compute stream measured slower:
     // 163-167 vs 175-180 M/s; more streams than the 4 hardware queues share queues)
-    if (msm) {
-      for (size_t c = 0; c < marks.size(); c++)
-        if (!dev.prep_ev[c]) HIPCHK(ctx, hipEventCreateWithFlags(&dev.prep_ev[c], hipEventDisableTiming));
-      for (hipEvent_t* ev : {&dev.msm_fork, &dev.msm_join})
-        if (!*ev) HIPCHK(ctx, hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    }
-    // msm: the chunks' preparations on the other compute stream, sort + buckets on cs, in two
-    // segments: the chunks up to MV_MSM_SEG_PCT % of the batch (sorted and bucketed while the
-    // rest is copied), then the rest (MV_MSM_SEG_PCT = 0: every chunk a segment)
-    std::vector<uint32_t> seg_end;
-    if (msm && ctx->kn.msm_seg_pct > 0) {
-      for (uint32_t e : marks)
-        if ((uint64_t)e * 100 >= (uint64_t)k * (uint64_t)ctx->kn.msm_seg_pct) {
-          if (e < k) seg_end.push_back(e);
-          break;
-        }
-      seg_end.push_back(k);
-    }
-    const mvk::ChunkGate gate{dev.chunk_ev[b], (uint32_t)marks.size(), marks.data(),
-                              msm ? dev.pstream[(t & 1) ^ 1] : nullptr, msm ? dev.msm_fork : nullptr,
-                              msm ? dev.msm_join : nullptr, msm, msm ? dev.prep_ev : nullptr,
-                              seg_end.empty() ? nullptr : seg_end.data(), (uint32_t)seg_end.size()};
+    const mvk::ChunkGate gate{dev.chunk_ev[b], (uint32_t)marks.size(), marks.data()};
     mv_status rc = enqueue_batch(ctx, dev, dev.pin_msg[b].as<uint8_t>(), dev.pin_sig[b].as<uint8_t>(),
                                  pk ? dev.pin_pk[b].as<uint8_t>() : dev.committee_pk.as<uint8_t>(),
                                  pk ? nullptr : dev.pin_pk[b].as<uint32_t>(), k, dev.pin_st[b].as<uint8_t>(), cs,
@@ -2098,10 +1888,7 @@ mv_status verify_host_streamed(mv_ctx* ctx, Device& dev, const uint8_t* msg, con
       return set_err(ctx, MV_E_HIP, std::string("streamed verify: ") + hipGetErrorString(e));
     }
   }
-  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[0]));
-  HIPCHK(ctx, hipStreamSynchronize(dev.pstream[1]));
-  poll_flags(ctx, dev);
-  memcpy(status + lo, hst, m);
+  for (int k = 0; k < 2; k++) HIPCHK(ctx, hipEventRecord(dev.sig_done[slot][k], dev.pstream[used[k] ? k : 1 - k]));
   return MV_OK;
 }
 
@@ -2122,7 +1909,6 @@ struct KnobDef {
 const KnobDef kKnobs[] = {
     {"MV_BLK_PIPE", &mvk::Knobs::blk_pipe, K_ON, false},
     {"MV_COMB_SPLIT_BYTES", &mvk::Knobs::comb_split_bytes, K_INT, false},
-    {"MV_BLK_FUSED", &mvk::Knobs::blk_fused, K_OFF, false},
     {"MV_HASH_IN_COMB", &mvk::Knobs::hash_in_comb, K_ON, false},
     {"MV_INGEST_IN_COMB", &mvk::Knobs::ingest_in_comb, K_ON, false},
     {"MV_VERDICT_FUSED", &mvk::Knobs::verdict_fused, K_ON, false},
@@ -2136,7 +1922,6 @@ const KnobDef kKnobs[] = {
     {"MV_Q_SPIN_US", &mvk::Knobs::q_spin_us, K_INT, false},
     {"MV_ONLINE", &mvk::Knobs::online, K_ON, false},
     {"MV_ONLINE_LONG", &mvk::Knobs::online_long, K_ON, false},
-    {"MV_ONLINE_CUS", &mvk::Knobs::online_cus, K_INT, false},
     {"MV_ONLINE_PRIO", &mvk::Knobs::online_prio, K_ON, false},
     {"MV_ONLINE_WGS", &mvk::Knobs::online_wgs, K_INT, false},
     {"MV_ONLINE_IDLE_US", &mvk::Knobs::online_idle_us, K_INT, false},
@@ -2144,12 +1929,6 @@ const KnobDef kKnobs[] = {
     {"MV_ONLINE_DEBUG", &mvk::Knobs::online_debug, K_FLAG, false},
     {"MV_ONLINE_INJECT", &mvk::Knobs::online_inject, K_OFF, false},
     {"MV_ONLINE_SPINNERS", &mvk::Knobs::online_spinners, K_INT, false},
-    {"MV_ONLINE_MERGE", &mvk::Knobs::online_merge, K_OFF, false},
-    {"MV_PIPELINE", &mvk::Knobs::pipeline, K_INT, false},
-    {"MV_PIPE_CHUNK_LOG2", &mvk::Knobs::pipe_chunk_log2, K_INT, false},
-    {"MV_PIPE_THREADS", &mvk::Knobs::pipe_threads, K_INT, false},
-    {"MV_PIPE_TRACE", &mvk::Knobs::pipe_trace, K_FLAG, false},
-    {"MV_SIG_ZEROCOPY", &mvk::Knobs::sig_zerocopy, K_OFF, false},
     {"MV_STREAM_CHUNK_LOG2", &mvk::Knobs::stream_chunk_log2, K_INT, false},
     {"MV_GUARD_GROUPS", &mvk::Knobs::guard_groups, K_INT, true},
     {"MV_BASE_GROUPS", &mvk::Knobs::base_groups, K_INT, true},
@@ -2161,12 +1940,9 @@ const KnobDef kKnobs[] = {
     {"MV_COMB_QUAD", &mvk::Knobs::comb_quad, K_INT, false},
     {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
-    {"MV_STREAM_MSM", &mvk::Knobs::stream_msm, K_OFF, false},
     {"MV_PREP_CHAIN", &mvk::Knobs::prep_chain, K_ON, false},
     {"MV_BLK_WALK", &mvk::Knobs::blk_walk, K_ON, false},
     {"MV_BUCKET_BAL", &mvk::Knobs::bucket_bal, K_INT, false},
-    {"MV_MSM_SEG_PCT", &mvk::Knobs::msm_seg_pct, K_INT, false},
-    {"MV_STREAM_TAIL", &mvk::Knobs::stream_tail, K_OFF, false},
     {"MV_FINAL_ROWS", &mvk::Knobs::final_rows, K_ON, false},
     {"MV_SCATTER_LDS", &mvk::Knobs::scatter_lds, K_ON, false},
     {"MV_FINE_LDS", &mvk::Knobs::fine_lds, K_ON, false},
@@ -2191,10 +1967,6 @@ mvk::Knobs knobs_from_env() {
       case K_FLAG: k.*d.field = 1; break;
       case K_INT: k.*d.field = atoll(e); break;
     }
-  }
-  if (const char* e = getenv("MV_ZC_FIRST")) {  // the first zero-copy batch's share, in (0, 1)
-    const double v = atof(e);
-    if (v > 0.0 && v < 1.0) k.zc_first = v;
   }
   if (const char* e = getenv("MV_STREAM_FRACS")) {  // shares separated by ',' or '/'
     int n = 0;
@@ -2335,9 +2107,9 @@ mv_status mv_create(const mv_config* cfg, mv_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking);
     for (int k = 0; k < 2 && e == hipSuccess; k++) e = hipStreamCreateWithFlags(&dev.pstream[k], hipStreamNonBlocking);
     // every other stream the engine uses, now: the runtime spreads streams over its hardware
-    // queues (GPU_MAX_HW_QUEUES) in creation order, and the online service's CU-masked stream
-    // must be created after all of them, or a stream made later can share its queue and wait
-    // behind the resident kernel (test_online_service_does_not_block_other_streams)
+    // queues (GPU_MAX_HW_QUEUES) in creation order, and the online service's stream must be
+    // created after all of them, or a stream made later can share its queue and wait behind the
+    // resident kernel (test_online_service_does_not_block_other_streams)
     for (int k = 0; k < Device::kPassSets && e == hipSuccess; k++)
       e = hipStreamCreateWithFlags(&dev.qstream[k], hipStreamNonBlocking);
     for (int k = 0; k < Device::kPassSets && e == hipSuccess; k++)
@@ -2473,14 +2245,8 @@ void mv_destroy(mv_ctx* ctx) {
       for (hipEvent_t ev : dev.chunk_ev[k])
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : dev.prep_ev)
-      if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : {dev.msm_fork, dev.msm_join, dev.prep_chain}) {
-      if (ev) (void)hipEventDestroy(ev);
-    }
+    if (dev.prep_chain) (void)hipEventDestroy(dev.prep_chain);
     for (int k = 0; k < 2; k++) {
-      watch.phase("frees: host staging");
-      dev.h_stage[k].release();
       watch.phase("frees: copy stream");
       if (dev.pstream[k]) (void)hipStreamDestroy(dev.pstream[k]);
     }
@@ -2614,7 +2380,7 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
                             const uint32_t* key_idx, uint32_t n, uint8_t* status) {
   if (!ctx || (n && (!msg || !sig || !status || (!pk == !key_idx))))
     return set_err(ctx, MV_E_INVALID_ARG, "bad verify args: exactly one of pk / key_idx");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::unique_lock<std::mutex> lk(ctx->mu);
   if (key_idx) {
     if (!ctx->has_committee) return set_err(ctx, MV_E_NO_COMMITTEE, "key_idx given but no committee set");
     for (uint32_t i = 0; i < n; i++)
@@ -2625,27 +2391,76 @@ mv_status mv_ed25519_verify(mv_ctx* ctx, const uint8_t* msg, const uint8_t* sig,
     HIPCHK(ctx, hipSetDevice(d.id));
     reap_idle(ctx, d);
   }
+  // Pinned inputs (mv_host_alloc) of a large call stream: chunked DMA copies gate k_bv_prep
+  // chunk by chunk (verify_host_streamed). The enqueue holds ctx->mu; the wait for the verdicts
+  // does not, so concurrent callers' calls overlap (one's copies beside another's MSM; the
+  // reference verifies in one task per peer, net_sync.rs:214-221). (Pageable inputs: one direct
+  // H2D per max_batch below; a chunked pack into pinned staging and k_bv_prep reading pinned
+  // inputs over PCIe measured slower and were removed in round 6)
+  const bool streamed = pinned && !(ctx->flags & MV_FLAG_NO_BATCH);
+  if (streamed) {
+    const size_t nd = ctx->devs.size();
+    std::vector<uint64_t> cut(nd + 1);
+    for (size_t d = 0; d <= nd; d++) cut[d] = nd == 1 || n < 2 * 256 ? (d ? n : 0) : (uint64_t)n * d / nd;
+    bool big = true;
+    for (size_t d = 0; d < nd; d++) big &= cut[d + 1] == cut[d] || cut[d + 1] - cut[d] > 8ull * MV_BATCH_MIN;
+    if (big) {
+      // one staging slot per device for this call (wait while another call holds them all)
+      std::vector<int> slot(nd, -1);
+      auto free_slot = [&](Device& d) {
+        for (int k = 0; k < Device::kSigCalls; k++)
+          if (!d.sig_busy[k]) return k;
+        return -1;
+      };
+      ctx->sig_cv.wait(lk, [&] {
+        for (Device& d : ctx->devs)
+          if (free_slot(d) < 0) return false;
+        return true;
+      });
+      for (size_t d = 0; d < nd; d++) {
+        slot[d] = free_slot(ctx->devs[d]);
+        ctx->devs[d].sig_busy[slot[d]] = true;
+      }
+      mv_status rc = for_each_cut(ctx, cut, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
+        HIPCHK(ctx, hipSetDevice(dev.id));
+        return verify_host_streamed(ctx, dev, msg, sig, pk, key_idx, lo, hi, slot[&dev - ctx->devs.data()]);
+      });
+      lk.unlock();
+      // wait for this call's batches alone (events, not stream drains: another caller's batches
+      // may follow on the same streams), then copy the verdicts out
+      std::vector<hipError_t> werr(nd, hipSuccess);
+      for (size_t d = 0; d < nd; d++) {
+        if (cut[d + 1] == cut[d]) continue;
+        Device& dev = ctx->devs[d];
+        (void)hipSetDevice(dev.id);
+        for (int k = 0; k < 2 && werr[d] == hipSuccess; k++) werr[d] = hipEventSynchronize(dev.sig_done[slot[d]][k]);
+        if (rc == MV_OK && werr[d] == hipSuccess)
+          memcpy(status + cut[d], dev.sig_stage[slot[d]].p, cut[d + 1] - cut[d]);
+      }
+      lk.lock();
+      for (size_t d = 0; d < nd; d++) {
+        Device& dev = ctx->devs[d];
+        if (rc != MV_OK || werr[d] != hipSuccess) {  // drain what was queued before the slot is reused
+          (void)hipSetDevice(dev.id);
+          (void)hipStreamSynchronize(dev.stream);
+          for (hipStream_t ps : dev.pstream) (void)hipStreamSynchronize(ps);
+        }
+        dev.sig_busy[slot[d]] = false;
+        if (cut[d + 1] > cut[d]) {
+          (void)hipSetDevice(dev.id);
+          poll_flags(ctx, dev);
+        }
+      }
+      ctx->sig_cv.notify_all();
+      if (rc != MV_OK) return rc;
+      for (size_t d = 0; d < nd; d++)
+        if (werr[d] != hipSuccess)
+          return set_err(ctx, MV_E_HIP, std::string("streamed verify: ") + hipGetErrorString(werr[d]));
+      return MV_OK;
+    }
+  }
   return for_each_shard(ctx, n, [&](Device& dev, uint64_t lo, uint64_t hi) -> mv_status {
     HIPCHK(ctx, hipSetDevice(dev.id));
-    // large host-buffer batches, chunked with the copies of one chunk beside the verification
-    // of the previous: opt-in (MV_PIPELINE=1). Measured on MI355X + EPYC 9575F for 2^20
-    // signatures it is slower than one direct pageable H2D per call (118-127 vs 132 M/s over
-    // 2^18..2^20-signature chunks and 8 or 16 staging threads): host memcpy into pinned
-    // staging runs at ~10 GB/s per thread, and chunks below 2^20 cost the batch path's
-    // fixed per-batch work
-    // Pinned inputs (mv_host_alloc) stream: chunked DMA copies gate k_bv_prep chunk by chunk.
-    const int pipeline = (int)ctx->kn.pipeline;
-    if (!(ctx->flags & MV_FLAG_NO_BATCH) && hi - lo > 8ull * MV_BATCH_MIN) {
-      if (pinned) {
-        // MV_SIG_ZEROCOPY=1: k_bv_prep reads the pinned arrays over PCIe (no copy phase); measured
-        // slower than the chunked copies (175-185 vs 191-195 M/s, profiles/r03/e2e_zerocopy_ab.txt)
-        const bool zc = ctx->kn.sig_zerocopy != 0;
-        mv_status zrc = MV_OK;
-        if (zc && verify_host_zerocopy(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, zrc)) return zrc;
-        return verify_host_streamed(ctx, dev, msg, sig, pk, key_idx, lo, hi, status);
-      }
-      if (pipeline) return verify_host_pipelined(ctx, dev, msg, sig, pk, key_idx, lo, hi, status, pipeline == 2);
-    }
     for (uint64_t i = lo; i < hi; i += ctx->max_batch) {
       uint32_t m = (uint32_t)std::min<uint64_t>(ctx->max_batch, hi - i);
       HIPCHK(ctx, dev.msg.ensure(32 * (size_t)m));

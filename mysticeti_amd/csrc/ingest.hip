@@ -50,16 +50,6 @@ __global__ void __launch_bounds__(64) k_block_ingest(const uint8_t* __restrict__
   ingest_block<false>(blockIdx.x, buf, off, len, cv, io, L);
 }
 
-// k_block_check: k_block_ingest without the pre-image (PRE = false): the checks, facts, claimed
-// digest, signature, key index and |P| only. The walk hash (blake2b_lane.hip, k_b2_walk) reads
-// the bincode itself, so no P || sig is staged in HBM.
-__global__ void __launch_bounds__(64) k_block_check(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
-                                                    const uint64_t* __restrict__ len, uint32_t n, CommitteeView cv,
-                                                    IngestOut io) {
-  __shared__ IngestLds L;
-  ingest_block<false, false>(blockIdx.x, buf, off, len, cv, io, L);
-}
-
 // Between the hashes and the signature check: a parsed block whose digest differs from the
 // claimed one gets DIGEST_MISMATCH whatever its signature (types.rs:327-332 comes before the
 // signature check at :346-348), so its s is set to 2^256 - 1 (>= l): it is then excluded
@@ -104,17 +94,6 @@ hipError_t launch_block_parse(const Knobs& kn, const uint8_t* buf, const uint64_
   else  // (capping its workgroups per CU with padded LDS, to leave room for the other stream's
         // kernels, measured slower: 79 vs 103 M config-4 blocks/s, profiles/r03/ab/)
     hipLaunchKernelGGL(mv::k_block_ingest, dim3(n), dim3(64), 0, s, buf, off, len, n, cv, io);
-  return hipGetLastError();
-}
-
-hipError_t launch_block_check(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
-                              const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
-                              uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx, uint32_t* facts,
-                              uint8_t* claimed, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  const mv::CommitteeView cv{stakes, n_auth, epoch, quorum_thr};
-  const mv::IngestOut io{nullptr, pre_off, pre_len, sig, key_idx, facts, claimed};
-  hipLaunchKernelGGL(mv::k_block_check, dim3(n), dim3(64), 0, s, buf, off, len, n, cv, io);
   return hipGetLastError();
 }
 

@@ -66,9 +66,7 @@ struct BcReader {
   }
 };
 
-// pre-image writer: bytes gathered into aligned 64-bit stores (STORE = false: the length only,
-// for the check-only ingest of the walk hash, blake2b_lane.hip)
-template <bool STORE = true>
+// pre-image writer: bytes gathered into aligned 64-bit stores
 struct PreWriter {
   uint64_t* out;
   uint64_t acc;
@@ -79,8 +77,7 @@ struct PreWriter {
     acc |= v << (8 * nb);
     const uint32_t t = nb + k;
     if (t >= 8) {
-      if (STORE) *out = acc;
-      out++;
+      *out++ = acc;
       acc = nb ? v >> (64 - 8 * nb) : 0ull;
       nb = t - 8;
     } else {
@@ -99,8 +96,7 @@ struct PreWriter {
     raw(d, 32);
   }
   MV_DEV void flush() {
-    if (STORE && nb) *out = acc;
-    if (nb) out++;
+    if (nb) *out++ = acc;
     acc = 0;
     nb = 0;
   }
@@ -127,16 +123,13 @@ struct CommitteeView {
 // because the bincode is at least |P| + 128 bytes long; writes happen only after the bytes
 // they come from were read, so a malformed block never writes outside its span either.
 // seen[k * stride], k < 16: a zeroed authority bitmap (<= 512 authorities) for this lane.
-// PRE = false: the checks, facts, signature and |P| only; no pre-image is written (the walk
-// hash, blake2b_lane.hip, builds it from the bincode itself).
-template <bool PRE = true>
 MV_DEV void ingest_lane(const uint8_t* buf, uint64_t o, uint64_t L, uint32_t i, const CommitteeView& cv,
                         const IngestOut& io, uint32_t* seen, int stride) {
   const uint32_t n_auth = cv.n_auth;
   const uint64_t so = (o + 7) & ~7ull;
   uint8_t* const stage = io.stage;
   BcReader r{buf + o, L, 0, true};
-  PreWriter<PRE> w{reinterpret_cast<uint64_t*>(stage + so), 0, 0, 0};
+  PreWriter w{reinterpret_cast<uint64_t*>(stage + so), 0, 0, 0};
 
   uint64_t me_a, me_r;
   const uint8_t* me_d;
@@ -181,12 +174,8 @@ MV_DEV void ingest_lane(const uint8_t* buf, uint64_t o, uint64_t L, uint32_t i, 
     if (tag == 0) {  // Share(Transaction): raw bytes, no length in the pre-image
       const uint64_t l = r.u64();
       if (!r.take(l)) break;
-      if (PRE) {
-        w.put(0, 1);
-        w.raw(r.p + r.pos, l);
-      } else {
-        w.len += 1 + l;
-      }
+      w.put(0, 1);
+      w.raw(r.p + r.pos, l);
       r.pos += l;
     } else if (tag == 1) {  // Vote(TransactionLocator, Vote)
       uint64_t a, rd;
@@ -370,10 +359,8 @@ MV_DEV void ig_sync() {
 }
 
 // Block i by one wave (k_block_ingest's body; WAVE: the wave is one of several in its
-// workgroup and syncs alone). L: the wave's own LDS. PRE = false (k_block_check): the same
-// checks, facts, claimed digest, signature and |P|, but no pre-image is built or written (the
-// walk hash, blake2b_lane.hip, transcodes the bincode itself).
-template <bool WAVE, bool PRE = true>
+// workgroup and syncs alone). L: the wave's own LDS.
+template <bool WAVE>
 MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
                          const uint64_t* __restrict__ len, const CommitteeView& cv, const IngestOut& io,
                          IngestLds& Ls) {
@@ -395,7 +382,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
   if (lane < 16) seen[lane] = 0;
   if (d + L + 16 > IG_WIN) {  // does not fit the window: one lane from global memory
     ig_sync<WAVE>();
-    if (lane == 0) ingest_lane<PRE>(buf, o, L, i, cv, io, seen, 1);
+    if (lane == 0) ingest_lane(buf, o, L, i, cv, io, seen, 1);
     return;
   }
   {
@@ -437,7 +424,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
   const uint32_t claimed_w = (ok && lane < 8) ? rd32(24 + 4 * lane) : 0u;
   uint32_t bad = 0, inc_first = 0xffffffffu;
   if (ok) {
-    if (PRE && lane < 8) {
+    if (lane < 8) {
       pre[lane] = (uint8_t)(me_a >> (56 - 8 * lane));
       pre[8 + lane] = (uint8_t)(me_r >> (56 - 8 * lane));
     }
@@ -447,17 +434,15 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
       const uint32_t p = 64 + 56 * k;
       const uint64_t a = rd64(p), r = rd64(p + 8);
       bad |= rd64(p + 16) != 32;
-      if (PRE) {
-        uint64_t dg[4];
+      uint64_t dg[4];
 #pragma unroll
-        for (int m = 0; m < 4; m++) dg[m] = rd64(p + 24 + 8 * m);  // digest bytes as they lie
-        // pre-image offset 16 + 48 k is 8-byte aligned: six 64-bit LDS stores, not 48 byte stores
-        uint64_t* pq = pre64 + 2 + 6 * k;
-        pq[0] = __builtin_bswap64(a);  // big-endian u64 (pre_be64)
-        pq[1] = __builtin_bswap64(r);
+      for (int m = 0; m < 4; m++) dg[m] = rd64(p + 24 + 8 * m);  // digest bytes as they lie
+      // pre-image offset 16 + 48 k is 8-byte aligned: six 64-bit LDS stores, not 48 byte stores
+      uint64_t* pq = pre64 + 2 + 6 * k;
+      pq[0] = __builtin_bswap64(a);  // big-endian u64 (pre_be64)
+      pq[1] = __builtin_bswap64(r);
 #pragma unroll
-        for (int m = 0; m < 4; m++) pq[2 + m] = dg[m];
-      }
+      for (int m = 0; m < 4; m++) pq[2 + m] = dg[m];
       const uint32_t code = a >= n_auth ? MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY : (r >= me_r ? MV_BLOCK_INCLUDE_ROUND : 0u);
       if (code && inc_first == 0xffffffffu) inc_first = (k << 4) | code;
       if (me_r > 0 && r == me_r - 1 && a < n_auth) atomicOr(&seen[(uint32_t)a >> 5], 1u << (a & 31));
@@ -556,7 +541,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
         a = rd64(p + 4);
         r = rd64(p + 12);
         bad |= rd64(p + 20) != 32;
-        if (PRE) win_read32(dg, win, d + p + 28);
+        win_read32(dg, win, d + p + 28);
         x = rd64(p + 60);
         if (tag == 1) {
           const uint32_t vote = rd32(p + 68);
@@ -566,7 +551,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
             a2 = rd64(p + 73);
             r2 = rd64(p + 81);
             bad |= rd64(p + 89) != 32;
-            if (PRE) win_read32(dg2, win, d + p + 97);
+            win_read32(dg2, win, d + p + 97);
             z2 = rd64(p + 129);
           }
         } else {  // tag 2
@@ -579,7 +564,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
     }
     // (b) Share payloads, moved down by the whole wave 64 bytes at a time (each round reads
     // before it writes, and the destination lies below the source)
-    uint64_t shares = PRE ? __ballot(kind == 1) : 0ull;
+    uint64_t shares = __ballot(kind == 1);
     while (shares) {
       const uint32_t j = (uint32_t)__builtin_ctzll(shares);
       shares &= shares - 1;
@@ -591,8 +576,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
       }
     }
     // (c) every lane writes its statement's pre-image
-    if (!PRE) {
-    } else if (kind == 1) {
+    if (kind == 1) {
       pre[q] = 0;
     } else if (kind >= 2 && kind <= 4) {
       pre[q] = (uint8_t)(kind - 1);
@@ -636,16 +620,14 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
   const uint32_t spos = pos + 33;  // signature
   uint32_t f = 0;
   if (ok) {
-    if (PRE && lane == 0) {
+    if (lane == 0) {
       pre_be64(pre, ppos, thi);
       pre_be64(pre, ppos + 8, tlo);
       pre[ppos + 16] = (uint8_t)marker;
       pre_be64(pre, ppos + 17, ep);
     }
-    if (PRE) {
-      const uint32_t sb = rd8(spos + lane);  // P || sig (read by every lane before any writes)
-      pre[ppos + 25 + lane] = (uint8_t)sb;
-    }
+    const uint32_t sb = rd8(spos + lane);  // P || sig (read by every lane before any writes)
+    pre[ppos + 25 + lane] = (uint8_t)sb;
     // threshold clock: stake of the distinct round r-1 authorities among the includes
     // (lane j sums authorities j, j + 64, ...: independent loads, one latency)
     uint64_t stake = 0;
@@ -665,7 +647,7 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
   ig_sync<WAVE>();
   const uint64_t so = (o + 7) & ~7ull;
   const uint32_t plen = ppos + 25;
-  if (PRE && ok) {  // P || sig to the stage (it stays inside the block's own span, see ingest_lane)
+  if (ok) {  // P || sig to the stage (it stays inside the block's own span, see ingest_lane)
     uint64_t* dst = reinterpret_cast<uint64_t*>(io.stage + so);
     const uint32_t nw = (plen + 64 + 7) >> 3;
     for (uint32_t k = lane; k < nw; k += 64) dst[k] = pre64[k];
@@ -674,10 +656,9 @@ MV_DEV void ingest_block(uint32_t i, const uint8_t* __restrict__ buf, const uint
   if (lane == 0) {
     io.pre_off[i] = so;
     io.pre_len[i] = ok ? plen : 0;
-    uint32_t sw[16];  // the signature, from its pre-image copy (its bincode was overwritten) or,
-                      // without a pre-image, from the bincode
+    uint32_t sw[16];  // the signature, from its pre-image copy (its bincode was overwritten)
 #pragma unroll
-    for (int q = 0; q < 16; q++) sw[q] = ok ? lds_u32(win, PRE ? plen + 4 * q : d + spos + 4 * q) : 0u;
+    for (int q = 0; q < 16; q++) sw[q] = ok ? lds_u32(win, plen + 4 * q) : 0u;
     const bool sig_decides = ok && (f & BF_EPOCH_OK) && (f & BF_AUTHOR_OK) && !(f & BF_GENESIS);
     if (!sig_decides) {
 #pragma unroll

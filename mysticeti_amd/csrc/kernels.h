@@ -14,7 +14,6 @@ struct Knobs {
   // block path (engine.cpp)
   int64_t blk_pipe = 1;                  // MV_BLK_PIPE: batch-size block calls in two halves on two streams
   int64_t comb_split_bytes = 2048;       // MV_COMB_SPLIT_BYTES: bytes per block from which the split comb path runs
-  int64_t blk_fused = 0;                 // MV_BLK_FUSED: the fused ingest + hash kernel
   int64_t hash_in_comb = 1;              // MV_HASH_IN_COMB: online passes hash inside k_verify_comb16
   int64_t ingest_in_comb = 1;            // MV_INGEST_IN_COMB: ... and parse there
   int64_t verdict_fused = 1;             // MV_VERDICT_FUSED: the block verdict inside the comb kernels
@@ -29,25 +28,17 @@ struct Knobs {
   // the resident online service
   int64_t online = 1;                    // MV_ONLINE: small block calls take the service
   int64_t online_long = 1;               // MV_ONLINE_LONG: long blocks take it too
-  int64_t online_cus = 0;                // MV_ONLINE_CUS: > 0: a CU-masked service stream of that many CUs (round 4)
   int64_t online_prio = 1;               // MV_ONLINE_PRIO: the service stream at the highest priority (its own queue)
   int64_t online_wgs = 0;                // MV_ONLINE_WGS: resident workgroups (0: = CUs)
   int64_t online_idle_us = 10000;        // MV_ONLINE_IDLE_US: the launch ends after this long idle
   int64_t online_trace = 0;              // MV_ONLINE_TRACE: per-stage means on stderr at release
   int64_t online_debug = 0;              // MV_ONLINE_DEBUG: launch lines, long waits on stderr
   int64_t online_inject = 0;             // MV_ONLINE_INJECT: fault injection (tests): launches fail
-  int64_t online_merge = 0;              // MV_ONLINE_MERGE: one-block requests share 4-signature jobs
   int64_t online_spinners = 0;           // MV_ONLINE_SPINNERS: callers spinning on their verdict (0: 1/4 of the CPU share)
   // signature path
-  int64_t pipeline = 0;                  // MV_PIPELINE: pageable signature staging experiment
-  int64_t pipe_chunk_log2 = 18;          // MV_PIPE_CHUNK_LOG2
-  int64_t pipe_threads = 8;              // MV_PIPE_THREADS
-  int64_t pipe_trace = 0;                // MV_PIPE_TRACE
-  int64_t sig_zerocopy = 0;              // MV_SIG_ZEROCOPY: k_bv_prep reads pinned inputs over PCIe
   int64_t stream_chunk_log2 = 17;        // MV_STREAM_CHUNK_LOG2: signatures per copy chunk
   int64_t guard_groups = 8;              // MV_GUARD_GROUPS: sub-batches while guarded
   int64_t base_groups = 1;               // MV_BASE_GROUPS: sub-batches when not guarded
-  double zc_first = 0.5;                 // MV_ZC_FIRST: the first zero-copy batch's share
   double stream_fracs[8] = {0.7, 0.3};   // MV_STREAM_FRACS: the streamed batches' shares
   int n_stream_fracs = 2;
   // kernel forms (the launchers)
@@ -59,16 +50,13 @@ struct Knobs {
   int64_t comb_quad = -1;                // MV_COMB_QUAD: force k_verify_comb16 (1) / k_verify_comb (0)
   int64_t ingest_lane = 0;               // MV_INGEST_LANE: the lane-per-block ingest kernel
   int64_t verify_occ = 2;                // MV_VERIFY_OCC: k_verify's waves per SIMD (1, 2, 3)
-  int64_t stream_msm = 0;                // MV_STREAM_MSM: pinned signature calls as one streaming MSM (measured slower)
   int64_t reduce_rows = 1024;            // MV_REDUCE_ROWS: reduction levels of <= this many elements a wave each (0: none)
   int64_t fine_lds = 1;                  // MV_FINE_LDS: the fine sort staged in registers + LDS (coalesced stores)
   int64_t scatter_lds = 1;               // MV_SCATTER_LDS: the partition scatter staged in LDS (coalesced stores)
   int64_t final_rows = 1;                // MV_FINAL_ROWS: k_bv_final's Horner with one DPP row per coordinate
-  int64_t stream_tail = 0;               // MV_STREAM_TAIL: pinned calls' last copy chunk halved down to 2^14
-  int64_t msm_seg_pct = 70;              // MV_MSM_SEG_PCT: streaming MSM's first segment (% of the batch; 0: per chunk)
   int64_t bucket_bal = 1;                // MV_BUCKET_BAL: equal entries per bucket-kernel lane (>1: entries per lane)
   int64_t prep_chain = 1;                // MV_PREP_CHAIN: a batch's k_bv_prep starts after the previous batch's
-  int64_t blk_walk = 2;                  // MV_BLK_WALK: batch-size block calls from the bincode: 2 one kernel (k_block_walk), 1 check + walk hash, 0 staged pre-image
+  int64_t blk_walk = 1;                  // MV_BLK_WALK: batch-size block calls in one pass over the bincode (k_block_walk); 0: staged pre-image
 };
 
 size_t verify_scratch_bytes(uint32_t n);
@@ -113,18 +101,6 @@ struct ChunkGate {
   const hipEvent_t* ready;
   uint32_t n;
   const uint32_t* end;
-  hipStream_t aux;  // may be null: every chunk on s
-  hipEvent_t fork, join;
-  // streaming MSM (msm = true, one group, chunk starts multiples of 1,024): each chunk's bucket
-  // entries are sorted and added into persistent bucket sums as soon as its preparation is
-  // done, so only the reduction and the final follow the last chunk. prep_done (n events):
-  // chunk c's preparation on aux -> s.
-  bool msm;
-  const hipEvent_t* prep_done;
-  // msm: the chunks are sorted and bucketed in segments ending at seg_end[0..n_seg) (chunk ends,
-  // ascending, the last = n); n_seg = 0: every chunk is a segment
-  const uint32_t* seg_end;
-  uint32_t n_seg;
 };
 constexpr int BATCH_STAGES = 6;  // prep, sort, bucket, reduce, final, fallback
 constexpr int BATCH_MAX_GROUPS = 16;
@@ -142,9 +118,7 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
 // instead of all starting together and leaving the tails to run side by side.
 // gate (optional): the inputs arrive in chunks (H2D copies on another stream). Chunk c =
 // signatures [end[c - 1], end[c]) (ends multiples of 256 except the last = n); k_bv_prep runs
-// chunk by chunk, each launch after hipStreamWaitEvent on ready[c], alternating between s and
-// aux (when set) so one chunk's latency-bound preparation overlaps the next's; fork / join
-// order aux after s's earlier work and s's later stages after aux's preparations.
+// chunk by chunk on s, each launch after hipStreamWaitEvent on ready[c].
 // comb_b (required): the comb table of B (mv_create), for the -[sum z s]B term.
 // comb_a / key_ok (optional, with key_idx): the committee's comb tables (comb.hip, tables of
 // -A) and per-key decode flags; k_bv_prep then reads each signature's A from entry [0][1]
@@ -263,10 +237,6 @@ struct OnlineDev {
   uint32_t n[ONLINE_SLOTS];
   uint32_t jobs_done[ONLINE_SLOTS];
   unsigned long long moved[ONLINE_SLOTS];  // request + 1 last moved from each slot (the poller's)
-  // merged jobs (OnlineArgs::merge): up to four one-block requests verified by one job in merge
-  // area a (ONLINE_SCR_STRIDE of HBM each, mscr): their request numbers and count
-  unsigned long long mq[ONLINE_SLOTS][4];
-  uint32_t mcount[ONLINE_SLOTS];
   unsigned long long jobs[ONLINE_JOBS];  // (request << 8) | job
   uint64_t sink[2 * 1024];               // 16 B per poller thread: where its copy lanes past the end go
 };
@@ -286,10 +256,7 @@ struct OnlineArgs {
   uint32_t n_auth;
   uint32_t launch;                // launch number (the epoch handshake)
   uint64_t idle_ticks, max_ticks;
-  uint8_t* mscr;                  // HBM merge areas, ONLINE_SCR_STRIDE each (ONLINE_SLOTS of them)
-  uint32_t merge;                 // 1: one-block requests of a pass share 4-signature jobs
 };
-constexpr unsigned long long ONLINE_JOB_MERGED = 1ull << 62;  // job entry: merged, area in the low bits
 hipError_t launch_online(const OnlineArgs& a, uint32_t grid, hipStream_t s);
 hipError_t launch_verify_comb(const Knobs& kn, const uint8_t* msg, const uint8_t* sig, const uint8_t* pk, const uint32_t* key_idx,
                               uint32_t n, const void* combB, const void* combA, const uint8_t* key_ok,
@@ -313,28 +280,12 @@ hipError_t launch_block_parse(const Knobs& kn, const uint8_t* buf, const uint64_
                               const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                               uint8_t* stage, uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx,
                               uint32_t* facts, uint8_t* claimed, hipStream_t s);
-// The walk form of batch-size block calls (MV_BLK_WALK): launch_block_parse's outputs but no
-// staged pre-image (k_block_check), then both digests from the bincode itself (k_b2_walk,
-// blake2b_lane.hip; blocks with pre_len 0 are skipped: the verdict zeroes their digests)
-hipError_t launch_block_check(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
-                              const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
-                              uint64_t* pre_off, uint64_t* pre_len, uint8_t* sig, uint32_t* key_idx, uint32_t* facts,
-                              uint8_t* claimed, hipStream_t s);
-hipError_t launch_block_hash_walk(const uint8_t* buf, const uint64_t* off, const uint64_t* plen, uint32_t n,
-                                  uint8_t* msg_out, uint8_t* dig_out, hipStream_t s);
-// block_walk.hip: launch_block_check's outputs and both digests in ONE pass over the bincode,
-// one lane per block (no pre-image staged or re-read); committees of <= 512 authorities
+// block_walk.hip: launch_block_parse's outputs (but no staged pre-image) and both digests in
+// ONE pass over the bincode, one lane per block; committees of <= 512 authorities
 hipError_t launch_block_walk(const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                              const uint64_t* stakes, uint32_t n_auth, uint64_t epoch, uint64_t quorum_thr,
                              uint8_t* sig, uint32_t* key_idx, uint32_t* facts, uint8_t* claimed, uint8_t* md,
                              uint8_t* bd, hipStream_t s);
-// ingest_hash.hip: the block parse of launch_block_parse and both BLAKE2b digests in one
-// kernel, one quad per block, the pre-image streamed through LDS (never staged in HBM).
-// buf_bytes bounds the blocks' extent in buf (16 readable bytes past it).
-hipError_t launch_block_ingest_hash(const uint8_t* buf, uint64_t buf_bytes, const uint64_t* off, const uint64_t* len,
-                                    uint32_t n, const uint64_t* stakes, uint32_t n_auth, uint64_t epoch,
-                                    uint64_t quorum_thr, uint8_t* sig, uint32_t* key_idx, uint32_t* facts,
-                                    uint8_t* claimed, uint8_t* md, uint8_t* bd, hipStream_t s);
 // sig[i]'s s := 2^256 - 1 (outside the batch equation) for every parsed block whose computed
 // digest differs from its claimed one
 hipError_t launch_block_digest_gate(const uint8_t* claimed, const uint8_t* digest, const uint32_t* facts, uint32_t n,

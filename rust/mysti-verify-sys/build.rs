@@ -8,7 +8,7 @@ use std::path::PathBuf;
 use std::process::Command;
 
 const SOURCES: &[&str] = &[
-    "kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "ingest_hash.hip", "blake2b_quad.hip", "blake2b_lane.hip", "block_walk.hip", "wal.hip", "engine.cpp",
+    "kernels.hip", "batch.hip", "comb.hip", "ingest.hip", "blake2b_quad.hip", "blake2b_lane.hip", "block_walk.hip", "wal.hip", "engine.cpp",
     "block_codec.cpp",
 ];
 // per-source flags (mysticeti_amd/build.py SOURCE_FLAGS)

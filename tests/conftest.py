@@ -41,6 +41,15 @@ def engine():
     eng.close()
 
 
+@pytest.fixture(autouse=True)
+def _fresh_batch_policy(request):
+    """Every test starts the session engine's adaptive batch policy afresh (no guard or
+    dense-failure route armed by an earlier test's bad signatures)."""
+    if "engine" in request.fixturenames:
+        request.getfixturevalue("engine").set_batch_groups(0)
+    yield
+
+
 @pytest.fixture
 def opts(engine):
     """opts(name, value[, eng]): sets a runtime switch (mv_set_option; the library reads the

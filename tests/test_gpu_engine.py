@@ -200,7 +200,7 @@ def test_online_service_relaunches_after_idle_exit(engine, opts):
 
 
 def test_online_service_does_not_block_other_streams(engine, opts):
-    """The resident kernel sits on a CU-masked stream of its own: while it is live (idle limit
+    """The resident kernel sits on a highest-priority stream (a queue of its own): while it is live (idle limit
     5 s here), a batch-path signature call and a queue-path block call on the engine's other
     streams complete at once, and the service is still the same launch afterwards."""
     import time
@@ -465,18 +465,15 @@ def test_context_with_online_service_is_destroyed_and_the_process_exits():
 
 
 @pytest.mark.parametrize("kmax", [2, 5])
-def test_online_service_merged_jobs(engine, golden, opts, kmax):
-    """MV_ONLINE_MERGE: the poller packs the one-block requests of a pass four to a job (each
-    block read from its own request's slot, its verdict and digests routed back to that
-    request). 16 threads posting one block (kmax 2) or 1-4 blocks (kmax 5) at a time, and every
-    golden edge case one per call from 8 threads at once: the queue path's verdicts and digests."""
+def test_online_service_one_block_callers(engine, golden, opts, kmax):
+    """16 threads posting one block (kmax 2) or 1-4 blocks (kmax 5) at a time through the
+    resident service, and every golden edge case one per call from 8 threads at once: the
+    queue path's verdicts and digests, and the fixture's statuses."""
     bins, pks, stakes = ragged_blocks(n_rounds=40, seed=17)
     engine.set_committee(pks, stakes, 0)
     opts("MV_ONLINE", 0)
     st_ref, md_ref, bd_ref = engine.verify_blocks(bins)
     opts("MV_ONLINE", 1)
-    opts("MV_ONLINE_MERGE", 1)
-    engine.set_committee(pks, stakes, 0)  # the next launch reads the switch
     st, md, bd = _concurrent(engine, bins, kmax=kmax)
     assert (st == st_ref).all() and (md == md_ref).all() and (bd == bd_ref).all()
     fx = golden("block_edge.json")
@@ -486,5 +483,4 @@ def test_online_service_merged_jobs(engine, golden, opts, kmax):
     want = np.array([c["status"] for c in fx["cases"]] * 4, dtype=np.uint8)
     est, _, _ = _concurrent(engine, ebins, threads=8, rounds=1, kmax=2)
     assert (est == want).all(), np.nonzero(est != want)[0][:8]
-    opts("MV_ONLINE_MERGE", 0)
-    engine.set_committee(pks, stakes, 0)  # stops the merging launch
+    engine.set_committee(pks, stakes, 0)

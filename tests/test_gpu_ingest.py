@@ -18,19 +18,17 @@ pytestmark = pytest.mark.gpu
 FORM = {"name": ""}
 
 
-@pytest.fixture(params=["in_comb", "two_kernel", "separate_hash", "batch_walk", "batch_check_walk", "batch_stage"],
-                autouse=True)
+@pytest.fixture(params=["in_comb", "two_kernel", "separate_hash", "batch_walk", "batch_stage"], autouse=True)
 def ingest_form(request, opts):
     """Every test runs on the device ingest forms: on small calls the parse and the digests
     inside k_verify_comb16 (the default), k_block_ingest + the digests inside k_verify_comb16
     (MV_INGEST_IN_COMB=0) and k_block_ingest + a separate k_b2_quad launch (MV_HASH_IN_COMB=0);
     at batch size (agree() repeats the inputs to >= MV_BATCH_MIN blocks) the one-pass walk
-    (k_block_walk: parse, checks and both digests from the bincode, the default), the check-only
-    ingest + the walk hash (k_block_check + k_b2_walk, MV_BLK_WALK=1) and the staged form
-    (k_block_ingest + k_b2_lane, MV_BLK_WALK=0)."""
+    (k_block_walk: parse, checks and both digests from the bincode, the default) and the staged
+    form (k_block_ingest + k_b2_lane, MV_BLK_WALK=0)."""
     opts("MV_HASH_IN_COMB", request.param != "separate_hash")
     opts("MV_INGEST_IN_COMB", request.param != "two_kernel")
-    opts("MV_BLK_WALK", {"batch_stage": 0, "batch_check_walk": 1}.get(request.param, 2))
+    opts("MV_BLK_WALK", request.param != "batch_stage")
     FORM["name"] = request.param
     return request.param
 
