@@ -10,9 +10,10 @@
 //
 // Both run ITERS dependent squarings per lane (a) on one wave (latency: the online path's
 // floor) and (b) on the full chip, 8 waves per SIMD (throughput: issue slots per squaring =
-// device cycles x 1,024 SIMDs x 2 slots per cycle / squarings, at the clock the kernel saw,
-// from s_memtime). The two chains start from the same values; their results are compared
-// mod p on the device (bit-exact canonical encodings).
+// device cycles / 2 per SIMD over the wave-squarings it ran, at the clock the kernel saw, from
+// s_memtime). Result (profiles/r06/microbench_sq.jsonl): fe32 costs 1.8x fe29 on the full chip
+// (373 against 203 slots) and 2.7x on a lone wave's chain, so the 9 x 29 form stays. The two
+// chains start from the same values; their results are compared mod p (canonical encodings).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I mysticeti_amd/csrc tools/microbench_sq.hip -o tools/microbench_sq
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -198,9 +199,9 @@ int main() {
     if (run(f.name, f.k, full_blocks, iters, f.d, dc, &usf, &cycf)) return 1;
     const double sq_full = (double)full_blocks * 256 * iters;
     const double ghz = cycf / (usf * 1e3);
-    // issue slots per squaring at the full chip: SIMD cycles x 2 slots (a wave64 full-rate
-    // instruction takes 2 cycles) / squarings per SIMD
-    const double slots = (cycf * 2.0) / (sq_full / (cus * 4.0));
+    // issue slots per squaring at the full chip: a SIMD issues one full-rate wave64 instruction
+    // per 2 cycles, so its slots = cycles / 2, over the wave-squarings it ran (lane count / 64)
+    const double slots = (cycf / 2.0) / (sq_full / (cus * 4.0) / 64.0);
     printf("{\"form\": \"%s\", \"lone_wave_ns_per_sq\": %.2f, \"lone_wave_cycles_per_sq\": %.1f, "
            "\"full_chip_sq_per_s\": %.4g, \"clock_GHz\": %.3f, \"issue_slots_per_sq\": %.1f}\n",
            f.name, us1 * 1e3 / iters, cyc1 / iters, sq_full / (usf * 1e-6), ghz, slots);
