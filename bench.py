@@ -277,6 +277,10 @@ def main():
             print(f"bench: {what} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
 
     eng = M.Engine(devices=(local_rank,))
+    if "MV_PREP_CHAIN" not in os.environ:
+        # the steps rotate over this script's own streams: let each step's k_bv_prep follow the
+        # previous one's on them too (the library chains only its own streams by default)
+        eng.set_option("MV_PREP_CHAIN", 2)
     n = args.batch
 
     # ---- corpus: host hashes, GPU signing (library signer), all resident in HBM ----

@@ -102,6 +102,8 @@ def run(args) -> int:
     import mysticeti_amd as M
 
     eng = M.Engine(devices=(local_rank,))
+    if "MV_PREP_CHAIN" not in os.environ:
+        eng.set_option("MV_PREP_CHAIN", 2)  # the steps' streams are this script's (bench.py main)
     try:
         if args.workload == "config5":
             return config5(args, eng, rank)

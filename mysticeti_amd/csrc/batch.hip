@@ -705,11 +705,9 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort_lds(const unsigned long l
 #ifndef MV_BUCKET_OCC
 #define MV_BUCKET_OCC 3
 #endif
-// acc (streaming MSM, seg = 1): the bucket sums continue from segT (the earlier chunks')
 __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ ents, uint32_t ngroups, uint32_t seg,
-                                                   uint32_t nw, uint32_t acc, uint4* __restrict__ segV,
-                                                   uint4* segT) {
+                                                   uint32_t nw, uint4* __restrict__ segV, uint4* __restrict__ segT) {
   const uint32_t nsw = BV_NB / seg;  // segments per (group, window) row
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
   if (lin >= ngroups * nw * nsw) return;  // windows nw.. carry no entries (per-key A term)
@@ -743,7 +741,6 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* _
   p3 T;
   p3_identity(T);
   if (seg > 1) v_store(T);  // V = identity
-  if (acc) p3_load(T, segT, sidx);
   const uint32_t e_lo = offs[key0];
   uint32_t e = offs[key0 + seg];
   uint4 q[7];
@@ -812,8 +809,8 @@ MV_DEV uint32_t bv_key_of(const uint32_t* __restrict__ offs, uint32_t k0, uint32
 __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint4* __restrict__ pts,
                                                                      const uint32_t* __restrict__ offs,
                                                                      const uint32_t* __restrict__ ents, uint32_t nk,
-                                                                     uint32_t nlanes, uint32_t acc,
-                                                                     uint4* __restrict__ carry, uint4* segT) {
+                                                                     uint32_t nlanes, uint4* __restrict__ carry,
+                                                                     uint4* __restrict__ segT) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nlanes) return;
   const uint32_t e0 = offs[0], e1 = offs[nk];
@@ -823,18 +820,12 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
   uint32_t b = bv_key_of(offs, 0, nk, lo);  // the bucket holding entry lo (non-empty)
   uint32_t nb = offs[b + 1];                // its end
   bool head = offs[b] < lo;                 // began before this lane: the piece is a carry
-  // a piece: the carry, or the bucket's sum (acc: added to the sum of the earlier segments)
-  auto emit = [&](uint32_t key, p3& P) {
-    if (head) {
+  // a piece: the carry, or the bucket's sum
+  auto emit = [&](uint32_t key, const p3& P) {
+    if (head)
       p3_store(carry, j, P);
-    } else {
-      if (acc) {
-        p3 O;
-        p3_load(O, segT, key);
-        p3_acc(P, O);
-      }
+    else
       p3_store(segT, key, P);
-    }
   };
   p3 T;
   p3_identity(T);
@@ -874,11 +865,9 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
 }
 
 // One lane per bucket key (g, w < nw, |d| - 1): empty -> identity; a bucket whose entries run
-// past the lane that began it gets the carries of the lanes it continues into. acc (streaming
-// MSM segments after the first): the buckets hold the earlier segments' sums, and an empty one
-// keeps its sum.
+// past the lane that began it gets the carries of the lanes it continues into.
 __global__ void __launch_bounds__(256) k_bv_bucket_fix(const uint32_t* __restrict__ offs, uint32_t nk,
-                                                       uint32_t ngroups, uint32_t nw, uint32_t nlanes, uint32_t acc,
+                                                       uint32_t ngroups, uint32_t nw, uint32_t nlanes,
                                                        const uint4* __restrict__ carry, uint4* __restrict__ segT) {
   const uint32_t lin = blockIdx.x * blockDim.x + threadIdx.x;
   if (lin >= ngroups * nw * BV_NB) return;
@@ -887,12 +876,10 @@ __global__ void __launch_bounds__(256) k_bv_bucket_fix(const uint32_t* __restric
   const uint32_t e0 = offs[0], e1 = offs[nk];
   const uint32_t L = (e1 - e0 + nlanes - 1) / nlanes;
   const uint32_t lo = offs[key], hi = offs[key + 1];
-  if (lo == hi) {  // (acc: the earlier segments' sum stays)
-    if (!acc) {
-      p3 I;
-      p3_identity(I);
-      p3_store(segT, key, I);
-    }
+  if (lo == hi) {
+    p3 I;
+    p3_identity(I);
+    p3_store(segT, key, I);
     return;
   }
   const uint32_t j0 = (lo - e0) / L, j1 = (hi - 1 - e0) / L;
@@ -1500,7 +1487,6 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
   const uint32_t nk = G.count * BV_NKG;
   // bucket sums of the sorted entries of m signatures
   auto buckets = [&](uint64_t m) {
-    const uint32_t acc = 0;
     if (seg == 1 && kn.bucket_bal > 0) {
       // equal entries per lane (the carries in segV: at most one per lane): 64 per lane, but at
       // least 3 waves per SIMD (196,608 lanes) while lanes keep >= 8 entries, so a small batch or
@@ -1510,12 +1496,12 @@ hipError_t launch_verify_batch(const Knobs& kn, const uint8_t* msg, const uint8_
                                         : std::max<uint64_t>(est / 64, std::min<uint64_t>(est / 8, 196608));
       const uint32_t cap = nk / 2;
       uint32_t nl = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(256, (want + 255) / 256 * 256));
-      hipLaunchKernelGGL(k_bv_bucket_bal, dim3(nl / 256), dim3(256), 0, s, pts, offs, ents, nk, nl, acc, segV, segT);
+      hipLaunchKernelGGL(k_bv_bucket_bal, dim3(nl / 256), dim3(256), 0, s, pts, offs, ents, nk, nl, segV, segT);
       hipLaunchKernelGGL(k_bv_bucket_fix, dim3(G.count * nw * BV_NB / 256), dim3(256), 0, s, offs, nk, G.count, nw, nl,
-                         acc, segV, segT);
+                         segV, segT);
     } else {
       hipLaunchKernelGGL(k_bv_bucket, dim3(G.count * nw * (BV_NB / seg) / 256), dim3(256), 0, s, pts, offs, ents,
-                         G.count, seg, nw, acc, segV, segT);
+                         G.count, seg, nw, segV, segT);
     }
   };
   if (gate && gate->n) {

@@ -304,12 +304,7 @@ __global__ void __launch_bounds__(64) k_block_walk(const uint8_t* __restrict__ b
 #pragma unroll
   for (int k = 0; k < 8; k++) h[k] = IV[k];
   h[0] ^= 0x01010020ull;  // depth 1, fanout 1, nn = 32
-#ifndef MV_WALK_PREFETCH
-#define MV_WALK_PREFETCH 1
-#endif
-  uint32_t pf = 0;  // the prefetch below: consumed one compression later
   while (__ballot(live)) {
-    if (MV_WALK_PREFETCH) asm volatile("" ::"v"(pf));  // (its load has had a compression's time)
     // fill the row up to a whole block, P's end (its final block goes first), or the end
     while (live && w.ok && pos < 128 && w.phase != DONE) {
       if (w.phase == SIG) {
@@ -325,14 +320,6 @@ __global__ void __launch_bounds__(64) k_block_walk(const uint8_t* __restrict__ b
       }
     }
     if (live && !w.ok) live = false;  // a parse error: no digests (the verdict zeroes them)
-    // Prefetch: the next fill reads the ~150 bincode bytes after the walk's position, and its
-    // first piece would wait for their line from HBM with only three waves per SIMD to cover
-    // it; a one-byte load of the line after the current one, issued now, has the compression's
-    // time to land (its value is consumed at the next fill, so the wait falls there).
-    if (MV_WALK_PREFETCH && live && w.phase < SIG) {
-      const uint32_t at = (w.phase == STMT && w.sub == SUB_SHARE ? w.psrc : w.src) + 128;
-      pf = *reinterpret_cast<const volatile uint8_t*>(w.blk + min(at, w.len - 1));
-    }
     // this step's compression: P's final block (mfin, on a copy of the state), the last block
     // of P || sig (fin), or a full block in between
     const bool mfin = live && w.phase == SIG && !pdone && pos <= 128;

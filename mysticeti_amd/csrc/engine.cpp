@@ -498,7 +498,7 @@ mv_status enqueue_committee_verify(mv_ctx* ctx, Device& dev, const uint8_t* d_ms
 // device) receives the all-groups flag word.
 mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const uint8_t* d_sig, const uint8_t* d_pk,
                         const uint32_t* d_key_idx, uint32_t n, uint8_t* d_status, hipStream_t s,
-                        uint32_t* flag_dst, const mvk::ChunkGate* gate = nullptr) {
+                        uint32_t* flag_dst, const mvk::ChunkGate* gate = nullptr, bool caller_stream = false) {
   poll_flags(ctx, dev);
   const int slot = dev.next_slot;
   dev.next_slot = (slot + 1) % Device::kSlots;
@@ -554,7 +554,10 @@ mv_status enqueue_batch(mv_ctx* ctx, Device& dev, const uint8_t* d_msg, const ui
   // committee keys (com_a): A comes from the comb tables built at mv_set_committee (no
   // per-signature decode)
   hipEvent_t chain[2] = {};
-  const bool chained = ctx->kn.prep_chain && !(gate && gate->n);
+  // on a caller's stream only when asked (MV_PREP_CHAIN=2): the chain orders the caller's streams
+  // behind each other's preparations, which the caller may not expect (its own gates could then
+  // deadlock them)
+  const bool chained = ctx->kn.prep_chain && !(gate && gate->n) && (!caller_stream || ctx->kn.prep_chain >= 2);
   if (chained) {
     if (!dev.prep_chain) HIPCHK(ctx, hipEventCreateWithFlags(&dev.prep_chain, hipEventDisableTiming));
     chain[0] = dev.prep_chained ? dev.prep_chain : nullptr;
@@ -767,7 +770,8 @@ mv_status enqueue_blocks(mv_ctx* ctx, Device& dev, const uint8_t* d_buf, uint64_
   const bool fused = ctx->kn.verdict_fused && !batch && !(ctx->flags & MV_FLAG_NO_COMB);
   const mvk::BlockVerdictOut bv{facts, claimed, md, bd, d_status};
   if (batch) {
-    st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, nullptr);
+    st = enqueue_batch(ctx, dev, md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, sst, s, nullptr, nullptr,
+                       own == nullptr);  // own == nullptr: mv_dev_verify_blocks on the caller's stream
   } else if (split) {
     HIPCHK(ctx, mvk::launch_comb_post(md, sig, dev.committee_pk.as<uint8_t>(), kidx, n, dev.combA.p,
                                       dev.keyok.as<uint8_t>(), rbuf, sbuf, qflags, sst, s, fused ? &bv : nullptr));
@@ -1145,9 +1149,10 @@ bool committee_ready(mv_ctx* ctx) {
 // One per device, made on the first eligible request. Page-locked coherent host memory holds
 // the control words, the request ring and each slot's bincode in / outputs out (the kernel
 // reads and writes them over PCIe, as the launched online path does); device memory holds the
-// ticket and each slot's ingest scratch. The kernel runs on its own stream, created with a CU
-// mask (a queue of its own, so kernels on other streams never wait behind it; and a bounded
-// share of the chip), and exits after MV_ONLINE_IDLE_US (default 10,000) without a job.
+// ticket and each slot's ingest scratch. The kernel runs on its own stream, the engine's only
+// one of the highest priority (a queue of its own, so kernels on other streams never wait behind
+// it; its 64 workgroups bound its share of the chip), and exits after MV_ONLINE_IDLE_US (default
+// 10,000) without a job.
 constexpr uint32_t kOnSlots = mvk::ONLINE_SLOTS, kOnMax = mvk::ONLINE_MAX_BLOCKS;
 constexpr size_t kOnInCap = mvk::ONLINE_IN_CAP;        // bincode bytes per request
 constexpr size_t kOnInStride = mvk::ONLINE_IN_STRIDE;  // off[n] | len[n] | bincode | 16 zero B
@@ -1588,6 +1593,15 @@ mv_status online_verify(mv_ctx* ctx, Device& dev, const uint8_t* buf, const uint
       return false;
     }
     rc = online_ensure_running(ctx, dev, o);
+    if (rc == MV_OK && o.launched && now - t_start > std::chrono::microseconds(std::max<uint64_t>(o.idle_us, 1000))) {
+      // waiting longer than the idle limit: a launch that faulted or was aborted never marks its
+      // liveness word LEFT, so ask the runtime about its end as well (fail fast, not after 20 s)
+      const hipError_t q = hipEventQuery(o.exited);
+      if (q == hipErrorNotReady)
+        (void)hipGetLastError();
+      else if (q != hipSuccess)
+        rc = set_err(ctx, MV_E_HIP, std::string("online service: ") + hipGetErrorString(q));
+    }
     if (rc == MV_OK && now - t_start > std::chrono::seconds(20))
       rc = set_err(ctx, MV_E_HIP, "online service: request timed out");
     if (rc != MV_OK) {
@@ -1940,7 +1954,7 @@ const KnobDef kKnobs[] = {
     {"MV_COMB_QUAD", &mvk::Knobs::comb_quad, K_INT, false},
     {"MV_INGEST_LANE", &mvk::Knobs::ingest_lane, K_OFF, false},
     {"MV_VERIFY_OCC", &mvk::Knobs::verify_occ, K_INT, false},
-    {"MV_PREP_CHAIN", &mvk::Knobs::prep_chain, K_ON, false},
+    {"MV_PREP_CHAIN", &mvk::Knobs::prep_chain, K_INT, false},
     {"MV_BLK_WALK", &mvk::Knobs::blk_walk, K_ON, false},
     {"MV_BUCKET_BAL", &mvk::Knobs::bucket_bal, K_INT, false},
     {"MV_FINAL_ROWS", &mvk::Knobs::final_rows, K_ON, false},
@@ -2737,7 +2751,7 @@ mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_
   HIPCHK(ctx, hipSetDevice(dev->id));
   reap_idle(ctx, *dev);
   hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
-  return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok);
+  return enqueue_batch(ctx, *dev, d_msg, d_sig, d_pk, d_key_idx, n, d_status, s, d_batch_ok, nullptr, true);
 }
 
 mv_status mv_batch_counters(mv_ctx* ctx, uint64_t* out) {

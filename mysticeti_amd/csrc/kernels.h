@@ -56,6 +56,7 @@ struct Knobs {
   int64_t final_rows = 1;                // MV_FINAL_ROWS: k_bv_final's Horner with one DPP row per coordinate
   int64_t bucket_bal = 1;                // MV_BUCKET_BAL: equal entries per bucket-kernel lane (>1: entries per lane)
   int64_t prep_chain = 1;                // MV_PREP_CHAIN: a batch's k_bv_prep starts after the previous batch's
+                                         // (1: on the engine's streams; 2: on callers' streams too)
   int64_t blk_walk = 1;                  // MV_BLK_WALK: batch-size block calls in one pass over the bincode (k_block_walk); 0: staged pre-image
 };
 
