@@ -73,10 +73,12 @@ def pmc_traffic(kernel: str, workload: str = "c2"):
     import glob
 
     files = []
-    for pat in (f"pmc_{workload}_{kernel}.json", f"pmc_{kernel}.json"):
+    # (pmc_<W>s1_: the pass ran the workload on one stream, as tools/gpu.sh pmc:c2s1 / pmc:c4s1 do)
+    for pat in (f"pmc_{workload}_{kernel}.json", f"pmc_{workload}s1_{kernel}.json", f"pmc_{kernel}.json"):
         files += glob.glob(os.path.join(ROOT, "profiles", "**", pat), recursive=True)
     rnd = lambda p: os.path.relpath(p, os.path.join(ROOT, "profiles")).split(os.sep)[0]  # r01, r02, ...
-    for f in sorted(files, key=lambda p: (rnd(p), "final" in p, f"pmc_{workload}_" in p), reverse=True):
+    mine = lambda p: os.path.basename(p).startswith((f"pmc_{workload}_", f"pmc_{workload}s1_"))
+    for f in sorted(files, key=lambda p: (rnd(p), "final" in p, mine(p)), reverse=True):
         try:
             d = json.load(open(f))
             return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)

@@ -50,18 +50,8 @@ MV_DEV uint64_t ld64(const uint8_t* p) {
   __builtin_memcpy(&v, p, 8);
   return v;
 }
-MV_DEV uint32_t ld32(const uint8_t* p) {
-  uint32_t v;
-  __builtin_memcpy(&v, p, 4);
-  return v;
-}
 MV_DEV void st64(uint8_t* q, uint64_t v) { __builtin_memcpy(q, &v, 8); }
 MV_DEV void st_be(uint8_t* q, uint64_t v) { st64(q, __builtin_bswap64(v)); }
-// the 32 digest bytes of the BlockReference at e (authority, round, u64 length, digest)
-MV_DEV void st_dig(uint8_t* q, const uint8_t* e) {
-#pragma unroll
-  for (int m = 0; m < 4; m++) st64(q + 8 * m, ld64(e + 24 + 8 * m));
-}
 
 enum : uint32_t { HDR, INC, NST, STMT, META, SIG, DONE };
 constexpr uint32_t SUB_NONE = 0, SUB_SHARE = 1, SUB_REJ2 = 2;
@@ -99,19 +89,64 @@ struct Walk {
   MV_DEV bool fits(uint32_t at, uint32_t need) const { return at <= len && need <= len - at; }
 };
 
+// The bincode window a piece reads: WIN bytes from the element's offset, loaded before the piece
+// is decoded (one round trip per piece, whichever branch its lanes take; the fields are then
+// picked out of registers at compile-time offsets). Loads are clamped to start at most at the
+// block's end, so they never leave the 16 readable bytes past it (mv_dev_verify_blocks).
+constexpr int WIN = 80;  // the largest piece reads 76 bytes (a VoteRange)
+struct Window {
+  uint64_t x[WIN / 8];
+};
+MV_DEV void load_window(Window& wn, const uint8_t* blk, uint32_t at, uint32_t lim) {
+#pragma unroll
+  for (int j = 0; j < WIN / 16; j++) {
+    uint64_t v[2];
+    __builtin_memcpy(v, blk + min(at + 16u * j, lim), 16);  // one unaligned 16-byte load
+    wn.x[2 * j] = v[0];
+    wn.x[2 * j + 1] = v[1];
+  }
+}
+// bytes [O, O + 8) of the window, little-endian
+template <int O>
+MV_DEV uint64_t wd(const Window& wn) {
+  static_assert(O >= 0 && O + 8 <= WIN, "window field out of range");
+  if constexpr (O % 8 == 0)
+    return wn.x[O / 8];
+  else
+    return (wn.x[O / 8] >> (8 * (O % 8))) | (wn.x[O / 8 + 1] << (64 - 8 * (O % 8)));
+}
+template <int O>
+MV_DEV uint32_t wd32(const Window& wn) {
+  static_assert(O % 8 <= 4, "a 32-bit field inside one word");
+  return (uint32_t)(wn.x[O / 8] >> (8 * (O % 8)));
+}
+template <int O>
+MV_DEV uint32_t wb(const Window& wn) {
+  return (uint32_t)(wn.x[O / 8] >> (8 * (O % 8))) & 0xffu;
+}
+// the 32 digest bytes of the BlockReference at window offset O (authority, round, u64 length,
+// digest)
+template <int O>
+MV_DEV void st_dig(uint8_t* q, const Window& wn) {
+  st64(q, wd<O + 24>(wn));
+  st64(q + 8, wd<O + 32>(wn));
+  st64(q + 16, wd<O + 40>(wn));
+  st64(q + 24, wd<O + 48>(wn));
+}
+
 // Emits the next piece of the pre-image at q (<= 72 bytes; bytes past the returned length may
-// be overwritten by the next piece) and runs the checks of the element it belongs to; clears
-// w.ok on the first failure. Returns the piece's length.
+// be overwritten by the next piece) from the window wn of the element's bincode, and runs the
+// checks of the element it belongs to; clears w.ok on the first failure. Returns the piece's
+// length.
 template <int NW>
-MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
-  const uint8_t* b = w.blk;
+MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca, const Window& wn) {
   if (w.phase == HDR) {  // own reference (author, round, digest) and the include count
     if (!w.fits(0, 64)) {
       w.ok = false;
       return 0;
     }
-    const uint64_t a = ld64(b), r = ld64(b + 8), n_inc = ld64(b + 56);
-    w.ok = ld64(b + 16) == 32 && n_inc <= (uint64_t)((w.len - 64) / 56);
+    const uint64_t a = wd<0>(wn), r = wd<8>(wn), n_inc = wd<56>(wn);
+    w.ok = wd<16>(wn) == 32 && n_inc <= (uint64_t)((w.len - 64) / 56);
     st_be(q, a);
     st_be(q + 8, r);
     w.me_a = a < ca.n_auth ? (uint32_t)a : ca.n_auth;
@@ -123,23 +158,22 @@ MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
     return 16;
   }
   if (w.phase == INC) {  // includes (types.rs:349-362), threshold clock (threshold_clock.rs:12-35)
-    const uint8_t* e = b + w.src;
-    const uint64_t a = ld64(e), r = ld64(e + 8);
-    w.ok = ld64(e + 16) == 32;
+    const uint64_t a = wd<0>(wn), r = wd<8>(wn);
+    w.ok = wd<16>(wn) == 32;
     st_be(q, a);
     st_be(q + 8, r);
-    st_dig(q + 16, e);
+    st_dig<0>(q + 16, wn);
     if (w.inc_code == 0)
       w.inc_code = a >= ca.n_auth ? (uint32_t)MV_BLOCK_INCLUDE_UNKNOWN_AUTHORITY
                                   : (r >= w.me_r ? (uint32_t)MV_BLOCK_INCLUDE_ROUND : 0u);
     if (w.me_r > 0 && r == w.me_r - 1 && a < ca.n_auth) {
-      const uint32_t wd = (uint32_t)a >> 5, bit = 1u << (a & 31);
+      const uint32_t wdx = (uint32_t)a >> 5, bit = 1u << (a & 31);
       uint32_t s = 0;
 #pragma unroll
-      for (int j = 0; j < NW; j++) s |= wd == (uint32_t)j ? w.seen[j] : 0u;
+      for (int j = 0; j < NW; j++) s |= wdx == (uint32_t)j ? w.seen[j] : 0u;
       if (!(s & bit)) {
 #pragma unroll
-        for (int j = 0; j < NW; j++) w.seen[j] |= wd == (uint32_t)j ? bit : 0u;
+        for (int j = 0; j < NW; j++) w.seen[j] |= wdx == (uint32_t)j ? bit : 0u;
         w.stake += ca.stakes[a];
       }
     }
@@ -152,7 +186,7 @@ MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
       w.ok = false;
       return 0;
     }
-    const uint64_t n_st = ld64(b + w.src);
+    const uint64_t n_st = wd<0>(wn);
     w.src += 8;
     w.ok = n_st <= (uint64_t)((w.len - w.src) / 12);
     w.cnt = (uint32_t)n_st;
@@ -164,32 +198,31 @@ MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
   if (w.phase == STMT) {
     uint32_t n = 0;
     bool done = true;
-    if (w.sub == SUB_SHARE) {  // Share payload, 64 bytes at a time (checked at its header; no
-                               // read starts past the payload, which ends inside the block)
-      const uint8_t* e = b + w.psrc;
+    if (w.sub == SUB_SHARE) {  // Share payload, 64 bytes at a time (checked at its header; the
+                               // words past the payload are junk the next piece overwrites)
 #pragma unroll
       for (int j = 0; j < 8; j++)
-        if (8u * j < w.rem) st64(q + 8 * j, ld64(e + 8 * j));
+        if (8u * j < w.rem) st64(q + 8 * j, wn.x[j]);
       n = min(w.rem, 64u);
       w.rem -= n;
       w.psrc += n;
       done = w.rem == 0;
-    } else if (w.sub == SUB_REJ2) {  // Reject(Some): the second locator (checked with the first)
-      const uint8_t* e = b + w.psrc;
-      st_be(q, ld64(e));
-      st_be(q + 8, ld64(e + 8));
-      st_dig(q + 16, e);
-      st_be(q + 48, ld64(e + 56));
+    } else if (w.sub == SUB_REJ2) {  // Reject(Some): the second locator (its bytes were bounded
+                                     // with the first; its digest length is checked here)
+      w.ok = wd<16>(wn) == 32;
+      st_be(q, wd<0>(wn));
+      st_be(q + 8, wd<8>(wn));
+      st_dig<0>(q + 16, wn);
+      st_be(q + 48, wd<56>(wn));
       n = 56;
     } else {
-      const uint8_t* e = b + w.src;
-      const uint32_t tag = w.fits(w.src, 4) ? ld32(e) : 3u;
+      const uint32_t tag = w.fits(w.src, 4) ? wd32<0>(wn) : 3u;
       if (tag == 0) {  // Share(Transaction): u32 tag, u64 length, bytes -> 0, bytes
-        if (!w.fits(w.src, 12) || ld64(e + 4) > (uint64_t)(w.len - w.src - 12)) {
+        if (!w.fits(w.src, 12) || wd<4>(wn) > (uint64_t)(w.len - w.src - 12)) {
           w.ok = false;
           return 0;
         }
-        const uint32_t l = (uint32_t)ld64(e + 4);
+        const uint32_t l = (uint32_t)wd<4>(wn);
         q[0] = 0;
         w.psrc = w.src + 12;
         w.rem = l;
@@ -202,15 +235,15 @@ MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
           w.ok = false;
           return 0;
         }
-        const uint32_t vote = ld32(e + 68);
-        const uint32_t some = vote == 1 && w.fits(w.src, 73) ? (uint32_t)e[72] : 2u;
+        const uint32_t vote = wd32<68>(wn);
+        const uint32_t some = vote == 1 && w.fits(w.src, 73) ? wb<72>(wn) : 2u;
         const bool two = vote == 1 && some == 1;
-        w.ok = ld64(e + 20) == 32 && (vote == 0 || some <= 1) && (!two || (w.fits(w.src, 137) && ld64(e + 89) == 32));
+        w.ok = wd<20>(wn) == 32 && (vote == 0 || some <= 1) && (!two || w.fits(w.src, 137));
         q[0] = (uint8_t)(vote == 0 ? 1 : (two ? 3 : 2));
-        st_be(q + 1, ld64(e + 4));
-        st_be(q + 9, ld64(e + 12));
-        st_dig(q + 17, e + 4);
-        st_be(q + 49, ld64(e + 60));
+        st_be(q + 1, wd<4>(wn));
+        st_be(q + 9, wd<12>(wn));
+        st_dig<4>(q + 17, wn);
+        st_be(q + 49, wd<60>(wn));
         n = 57;
         if (two) {
           w.psrc = w.src + 73;
@@ -223,12 +256,12 @@ MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
           w.ok = false;
           return 0;
         }
-        const uint64_t s0 = ld64(e + 60), s1 = ld64(e + 68);
-        w.ok = ld64(e + 20) == 32;
+        const uint64_t s0 = wd<60>(wn), s1 = wd<68>(wn);
+        w.ok = wd<20>(wn) == 32;
         q[0] = 4;
-        st_be(q + 1, ld64(e + 4));
-        st_be(q + 9, ld64(e + 12));
-        st_dig(q + 17, e + 4);
+        st_be(q + 1, wd<4>(wn));
+        st_be(q + 9, wd<12>(wn));
+        st_dig<4>(q + 17, wn);
         st_be(q + 49, s0);
         st_be(q + 57, s1);
         if (w.vr_code == 0) w.vr_code = s1 < s0 ? 1u : (s1 - s0 >= VR_MAX ? 2u : (s1 >= VR_MAX ? 3u : 0u));
@@ -247,17 +280,16 @@ MV_DEV uint32_t piece(Walk<NW>& w, uint8_t* q, const CommitteeArgs& ca) {
   }
   // META: creation time (u128 -> big-endian high, low), epoch marker, epoch; then u64 64 and the
   // signature (97 bincode bytes in all)
-  const uint8_t* e = b + w.src;
   if (!w.fits(w.src, 97)) {
     w.ok = false;
     return 0;
   }
-  const uint32_t marker = e[16];
-  w.ok = marker <= 1 && ld64(e + 25) == 64;
-  st_be(q, ld64(e + 8));
-  st_be(q + 8, ld64(e));
+  const uint32_t marker = wb<16>(wn);
+  w.ok = marker <= 1 && wd<25>(wn) == 64;
+  st_be(q, wd<8>(wn));
+  st_be(q + 8, wd<0>(wn));
   q[16] = (uint8_t)marker;
-  st_be(q + 17, ld64(e + 17));
+  st_be(q + 17, wd<17>(wn));
   w.phase = SIG;
   return 25;
 }
@@ -287,6 +319,7 @@ __global__ void __launch_bounds__(64) k_block_walk(const uint8_t* __restrict__ b
   w.blk = buf + (i < n ? off[i] : 0);
   const uint64_t L64 = i < n ? len[i] : 0;
   w.len = L64 > 0xffffffffull ? 0xffffffffu : (uint32_t)L64;
+  const uint32_t lim = min(w.len, 0xffffff00u);  // window loads start at most here (the block's end)
   w.phase = HDR;
   w.src = w.cnt = w.k = w.rem = w.psrc = 0;
   w.sub = SUB_NONE;
@@ -315,7 +348,9 @@ __global__ void __launch_bounds__(64) k_block_walk(const uint8_t* __restrict__ b
         w.phase = DONE;
         pos += 64;
       } else {
-        pos += piece(w, row + pos, ca);
+        Window wn;
+        load_window(wn, w.blk, w.phase == STMT && w.sub != SUB_NONE ? w.psrc : w.src, lim);
+        pos += piece(w, row + pos, ca, wn);
         if (w.phase == SIG && w.ok) plen = (uint32_t)(128 * blocks) + pos;  // P ends here
       }
     }
