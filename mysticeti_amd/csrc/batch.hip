@@ -616,9 +616,14 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort(const unsigned long long*
 }
 
 // The same sort with its output staged in LDS (MV_FINE_LDS): a partition of <= FINE_LDS entries
-// is read once into registers (16 per thread), counted, scanned, placed in LDS in bucket order
+// is read once into registers (16 per thread) and counted; the count's atomic returns each
+// entry's rank in its bin, so after the scan an entry's place is its bin's start + its rank (one
+// LDS atomic per entry instead of round 5's two); the entries are placed in LDS in bucket order
 // and stored coalesced; the direct form read each entry twice and stored one scattered word per
 // entry. Larger partitions (window 15's at 2^20 signatures: ~32K) take the direct form.
+// Bank conflicts stay ~65% of the LDS cycles either way (profiles/r06/pmc_c2s1_k_fine_sort_lds_*):
+// 64 lanes' random bins (and random ranks for the placement) land on 64 banks at random, about
+// four to a bank; the kernel is 0.16 ms of the 3.2-ms step.
 constexpr uint32_t FINE_LDS = 16384;
 constexpr int FINE_FPT = FINE_LDS / FINE_NT;
 __global__ void __launch_bounds__(FINE_NT) k_fine_sort_lds(const unsigned long long* __restrict__ tmp,
@@ -635,16 +640,19 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort_lds(const unsigned long l
   const bool staged = m <= FINE_LDS;  // (uniform in the block)
   if (threadIdx.x < NF) cnt[threadIdx.x] = 0;
   __syncthreads();
-  unsigned long long v[FINE_FPT];
+  uint32_t ent[FINE_FPT], br[FINE_FPT];  // entry; bin << 16 | its rank in the bin
+  static_assert(FINE_LDS <= (1u << 16), "ranks fit 16 bits");
   if (staged) {
 #pragma unroll
     for (int k = 0; k < FINE_FPT; k++) {
       const uint32_t i = threadIdx.x + (uint32_t)k * FINE_NT;
-      v[k] = i < m ? tmp[s + i] : 0ull;
+      const unsigned long long v = i < m ? tmp[s + i] : 0ull;
+      ent[k] = (uint32_t)v;
+      br[k] = ((uint32_t)(v >> 32) & (NF - 1)) << 16;
     }
 #pragma unroll
     for (int k = 0; k < FINE_FPT; k++)
-      if (threadIdx.x + (uint32_t)k * FINE_NT < m) atomicAdd(&cnt[(uint32_t)(v[k] >> 32) & (NF - 1)], 1u);
+      if (threadIdx.x + (uint32_t)k * FINE_NT < m) br[k] |= atomicAdd(&cnt[br[k] >> 16], 1u);
   } else {
     for (uint32_t i = s + threadIdx.x; i < e; i += FINE_NT) atomicAdd(&cnt[(uint32_t)(tmp[i] >> 32) & (NF - 1)], 1u);
   }
@@ -676,12 +684,8 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort_lds(const unsigned long l
   __syncthreads();
   if (staged) {
 #pragma unroll
-    for (int k = 0; k < FINE_FPT; k++) {
-      if (threadIdx.x + (uint32_t)k * FINE_NT < m) {
-        const uint32_t r = atomicAdd(&cnt[(uint32_t)(v[k] >> 32) & (NF - 1)], 1u);
-        obuf[r] = (uint32_t)v[k];
-      }
-    }
+    for (int k = 0; k < FINE_FPT; k++)
+      if (threadIdx.x + (uint32_t)k * FINE_NT < m) obuf[cnt[br[k] >> 16] + (br[k] & 0xffffu)] = ent[k];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < m; i += FINE_NT) ents[s + i] = obuf[i];
   } else {

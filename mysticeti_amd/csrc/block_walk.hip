@@ -42,7 +42,11 @@ using b2q::ror32;
 using b2q::ror63;
 using b2q::SIGMA;
 
-constexpr uint32_t ROW = 200;  // bytes per lane: one message block + the longest piece (72 B)
+#ifndef MV_WALK_ROW
+#define MV_WALK_ROW 200  // (A/B builds may pad it to trade occupancy for L2 footprint)
+#endif
+constexpr uint32_t ROW = MV_WALK_ROW;  // bytes per lane: one message block + the longest piece (72 B)
+static_assert(ROW >= 200 && ROW % 8 == 0, "a row holds a block and the longest piece");
 constexpr uint64_t VR_MAX = 1024 * 1024;  // VoteRange::verify MAX_LEN (types.rs:448)
 
 MV_DEV uint64_t ld64(const uint8_t* p) {

@@ -185,7 +185,8 @@ struct Device {
   // host-buffer batch verifies: two compute streams and double-buffered device inputs, so
   // the (pageable) H2D of one chunk runs beside the previous chunk's verification
   hipStream_t pstream[2] = {nullptr, nullptr};
-  // (three input buffer sets: the streamed pinned path's batches rotate over them)
+  // (three input buffer sets: the streamed pinned path's batches rotate over them; four measured
+  // the same for two concurrent callers, profiles/r06/e2e_two_callers.txt)
   static constexpr int kPinBufs = 3;
   DevBuf pin_msg[kPinBufs], pin_sig[kPinBufs], pin_pk[kPinBufs], pin_st[kPinBufs];
   hipEvent_t pin_free[kPinBufs] = {};

@@ -20,9 +20,13 @@
 #   abc4:V[:ARGS]    the same on config 4
 #   env:K=V          export K=V for the tasks that follow (SUF=x: later bench outputs are named <task>x.json)
 #   e2e[:ENV=V,..]   tools/e2e_probe.py (pinned end-to-end signatures) under these settings
+#   h2d              tools/h2d_probe.py: pinned H2D rates (whole arrays, chunks, two streams)
+#   e2etrace         tools/e2e_probe.py with two callers (MV_PROBE_TWO) under kernel + memory-copy trace
 #   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c4, c4s1, c5, wal}
 #   pmc:W[:KERNELS]  separate --pmc passes (one counter group per run) of W in {c2s1, c4s1, wal} and
 #                    tools/pmc_summary.py for each kernel (comma-separated)
+#   pmcg:W:K:C1,C2.. ONE --pmc pass of W with the counters C1,C2,.. (one block's limits), per kernel K
+#   avail            rocprofv3 --list-avail (the TCC_/TCP_ counter names in the output)
 #   teardown         tools/teardown_probe.py plain, then under rocprofv3 hip + kernel + memory-copy
 #                    trace (/proc maps at exit); run it LAST in a call (it may end in a teardown fault)
 set -o pipefail
@@ -128,6 +132,12 @@ for T in "$@"; do
     e2e)  # e2e[:ENV=V,ENV=V]: the pinned end-to-end probe under these environment settings
       (export ${arg//,/ }; timeout -k 10 300 python tools/e2e_probe.py) >> "$OUT/e2e.log" 2>&1 || { echo "e2e FAILED"; tail -5 "$OUT/e2e.log"; exit 1; }
       tail -1 "$OUT/e2e.log" ;;
+    h2d)  # tools/h2d_probe.py: pinned H2D rates in the streamed path's copy shapes
+      run 300 "$OUT/h2d.log" python tools/h2d_probe.py
+      grep "^h2d" "$OUT/h2d.log" ;;
+    e2etrace)  # the pinned probe with two callers, under a kernel + memory-copy trace (timeline)
+      (export MV_PROBE_TWO=1; run 300 "$OUT/e2etrace.log" rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/e2etrace" -o run -- python tools/e2e_probe.py) || exit 1
+      grep -E "two callers|e2e pinned" "$OUT/e2etrace.log" ;;
     trace)
       cmd=${W[$arg]}
       [ -n "$cmd" ] || { echo "unknown workload $arg"; exit 1; }
@@ -153,6 +163,28 @@ for T in "$@"; do
         python3 tools/pmc_summary.py "$OUT/pmc_$wl" "$k" --json "$OUT/pmc_${wl}_$k.json" > "$OUT/pmc_${wl}_$k.txt" || true
         grep -E "valu_issue|WAIT_INST|clock|fetch_GB|write_GB|kernel_avg|LDS_BANK" "$OUT/pmc_${wl}_$k.txt" | sed "s/^/$k /"
       done ;;
+    pmcg)  # pmcg:W:KERNELS:C1,C2,..: ONE extra --pmc pass with these counters (within one block's
+           # limits: at most 4 TCC_, 8 SQ_ ...), summarised per kernel
+      wl=${arg%%:*}
+      rest=${arg#*:}
+      ks=${rest%%:*}
+      ctrs=${rest#*:}
+      cmd=${W[$wl]}
+      [ -n "$cmd" ] || { echo "unknown workload $wl"; exit 1; }
+      [ "$wl" = c4s1 ] && export MV_BLK_PIPE=0
+      g=$OUT/pmcg_$wl${SUF:-}
+      mkdir -p "$g"
+      [ -d "$g/trace1" ] || run 400 "$g/trace.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$g/trace1" -o run -- $cmd
+      n=$(ls -d "$g"/pmc* 2>/dev/null | wc -l)
+      run 200 "$g/pmc$n.log" timeout -s KILL 190 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d "$g/pmc$n" -o run -- $cmd
+      for k in ${ks//,/ }; do
+        python3 tools/pmc_summary.py "$g" "$k" > "$OUT/pmcg_${wl}${SUF:-}_$k.txt" || true
+        sed "s/^/$k /" "$OUT/pmcg_${wl}${SUF:-}_$k.txt"
+      done ;;
+    avail)
+      run 120 "$OUT/avail.txt" rocprofv3 --list-avail
+      grep -oE "(TCC|TCP)_[A-Z0-9_]+" "$OUT/avail.txt" | sort -u | tr '\n' ' ' > "$OUT/avail_tcc.txt" || true
+      cut -c1-4000 "$OUT/avail_tcc.txt" ;;
     teardown)
       run 300 "$OUT/teardown_plain.log" python tools/teardown_probe.py "$OUT/maps_plain.txt"
       echo "plain: ok"
