@@ -95,6 +95,46 @@ def corpus_host(lo: int, n: int):
     return seed, msg
 
 
+def openssl_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, n: int, threads: int):
+    """BASELINE.md 2's secondary CPU speed reference: OpenSSL libcrypto Ed25519 EVP_DigestVerify
+    (bench_native/openssl_ed25519.c, built here against the system libcrypto) on the first n
+    config-2 signatures, one core and `threads` cores. Strict RFC 8032 semantics, not ZIP-215:
+    a speed reference on valid signatures only. None when libcrypto or its headers are absent."""
+    import ctypes
+
+    src = os.path.join(ROOT, "bench_native", "openssl_ed25519.c")
+    so = os.path.join(ROOT, "bench_native", "build", "libmv_openssl.so")
+    try:
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            os.makedirs(os.path.dirname(so), exist_ok=True)
+            subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-pthread", "-o", so, src, "-lcrypto"], check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        lib = ctypes.CDLL(so)
+    except (OSError, subprocess.CalledProcessError):
+        return None
+    vp = ctypes.c_void_p
+    lib.mvb_openssl_verify.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+    lib.mvb_openssl_verify.restype = ctypes.c_int
+    res = {}
+    for t, m in ((1, min(n, 1 << 16)), (threads, n)):
+        p = np.ascontiguousarray(pk[:m]); s = np.ascontiguousarray(sig[:m]); g = np.ascontiguousarray(msg[:m])
+        st = np.ones(m, dtype=np.uint8)
+        t0 = time.perf_counter()
+        rc = lib.mvb_openssl_verify(vp(p.ctypes.data), vp(s.ctypes.data), vp(g.ctypes.data), m, vp(st.ctypes.data), t)
+        dt = time.perf_counter() - t0
+        if rc != 0:
+            return None
+        res[t] = (m / dt, m, dt, int((st == 0).sum()))
+    return {"value": round(res[threads][0], 1), "unit": "sigs/s", "cores": threads,
+            "single_core_value": round(res[1][0], 1),
+            "accepted": res[threads][3], "of": res[threads][1],
+            "sample": f"{res[threads][1]} config-2 signatures on {threads} threads ({res[threads][2]:.1f} s); "
+                      f"single core: {res[1][1]} ({res[1][2]:.1f} s)",
+            "note": "OpenSSL libcrypto Ed25519 EVP_DigestVerify (BASELINE.md 2 secondary reference): strict "
+                    "RFC 8032, cofactorless -- a speed reference on valid signatures, not the reference's "
+                    "ZIP-215 semantics; the key is decoded per signature (distinct keys)"}
+
+
 def cpu_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, sample: int):
     """The oracle's C restatement (-O3 -march=native, built on this host) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -119,6 +159,7 @@ def cpu_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, sample: int):
         dt = time.perf_counter() - t0
         assert (st == 0).all(), "oracle rejected a valid corpus signature"
         res[t] = (n * passes / dt, n * passes, dt)
+    ossl = openssl_baseline(pk, sig, msg, min(sample, 1 << 18), threads)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -132,7 +173,7 @@ def cpu_baseline(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, sample: int):
         "sample": f"{res[threads][1]} verifies of config-2 signatures on {threads} threads ({res[threads][2]:.1f} s); "
                   f"single core: {res[1][1]} verifies ({res[1][2]:.1f} s)",
         "single_core_value": round(res[1][0], 1), "host_cpu": model, "nproc": os.cpu_count(),
-        "cores_source": share_src,
+        "cores_source": share_src, "openssl": ossl,
         "impl": "oracle/ed25519.c: dalek u64-backend structure (5x51 limbs, Straus wNAF-5/8), gcc -O3 -march=native",
     }
 
@@ -173,7 +214,8 @@ def summary_of(out: dict) -> dict:
          "c4_traffic_over_bincode": g(out, "config4", "roofline", "traffic_over_bincode"),
          "c4_host_fed_blocks_per_s": g(out, "config4", "host_fed", "value"),
          "wal_GBps": g(out, "wal", "value"), "cpu_sigs_per_s": g(out, "cpu_baseline", "value"),
-         "cpu_cores": g(out, "cpu_baseline", "cores")}
+         "cpu_cores": g(out, "cpu_baseline", "cores"),
+         "cpu_openssl_sigs_per_s": g(out, "cpu_baseline", "openssl", "value")}
     shapes = g(out, "config5", "shapes") or {}
     for k, v in shapes.items():
         s[f"c5_{k}_64blk_p50_us"] = g(v, "gpu", "p50_us")
