@@ -41,8 +41,12 @@ constexpr int kGuardBatches = 64;  // batches cut into sub-batch equations after
 // whole batch is re-verified after a wasted MSM): a guarded batch that failed in at least half
 // of its groups sends the next kSingleRun batches straight to the single path. Each of those
 // counts its rejected signatures; while a batch holds at least kDenseRejects of them the run is
-// renewed, otherwise the equation is tried again (guarded).
-constexpr int kSingleRun = 8;
+// renewed, otherwise the equation is tried again (guarded). The run is longer than the batches a
+// caller can have in flight (kFlagRing): a renewal is seen only when a single-path batch
+// completes, and a run that ran out before then sent a batch back to a doomed equation (config
+// 3 with three streams: 2 of 10 batches). Recovery does not wait for the run: the first clean
+// single-path batch to complete ends it.
+constexpr int kSingleRun = 32;
 constexpr uint32_t kDenseRejects = 4;
 constexpr uint32_t kSingleMark = 0x80000000u;  // flag_groups entry of a single-path batch
 constexpr int kBlockStages = 4;
