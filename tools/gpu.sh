@@ -22,7 +22,7 @@
 #   e2e[:ENV=V,..]   tools/e2e_probe.py (pinned end-to-end signatures) under these settings
 #   h2d              tools/h2d_probe.py: pinned H2D rates (whole arrays, chunks, two streams)
 #   e2etrace         tools/e2e_probe.py with two callers (MV_PROBE_TWO) under kernel + memory-copy trace
-#   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c4, c4s1, c5, wal}
+#   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c2single, c4, c4s1, c5, wal}
 #   pmc:W[:KERNELS]  separate --pmc passes (one counter group per run) of W in {c2s1, c4s1, wal} and
 #                    tools/pmc_summary.py for each kernel (comma-separated)
 #   pmcg:W:K:C1,C2.. ONE --pmc pass of W with the counters C1,C2,.. (one block's limits), per kernel K
@@ -40,6 +40,7 @@ C2ONLY="--cpu-sample 0 --no-e2e --sustain-repeats 0 --no-adversarial --no-config
 declare -A W=(
   [c2]="python bench.py --steps 5 --warmup 1 $C2ONLY"
   [c2s1]="python bench.py --steps 5 --warmup 1 --streams 1 $C2ONLY"
+  [c2single]="python bench.py --steps 5 --warmup 1 --streams 1 --path single $C2ONLY"
   [c4]="python bench.py --workload config4 --steps 6 --warmup 4 --cpu-sample 0 --host-fed-blocks 0 --batch 1048576"
   [c4s1]="python bench.py --workload config4 --steps 3 --warmup 1 --cpu-sample 0 --streams 1 --host-fed-blocks 0 --batch 1048576"
   [c5]="python bench.py --workload config5 --cpu-sample 0 --batches 1000 --conc-seconds 0.3"
