@@ -479,15 +479,12 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     from bench import pmc_traffic
 
     # the dominant kernel: by default the one-pass walk (block_walk.hip, the "parse" stage: parse,
-    # checks and both digests); MV_BLK_WALK=1: the walk hash after the check-only ingest;
-    # MV_BLK_WALK=0: the staged form's hash (k_b2_lane, or k_b2_quad with MV_B2_LANE=0)
-    walk = os.environ.get("MV_BLK_WALK", "2")
-    if walk not in ("0", "1"):
-        kname, hash_ms = "k_block_walk", stage_ms.get("parse")
-    elif walk == "1":
-        kname = "k_b2_walk"
-    else:
+    # checks and both digests); MV_BLK_WALK=0: the staged form's hash (k_b2_lane, or k_b2_quad
+    # with MV_B2_LANE=0)
+    if os.environ.get("MV_BLK_WALK", "1").startswith("0"):
         kname = "k_b2_quad" if os.environ.get("MV_B2_LANE") == "0" else "k_b2_lane"
+    else:
+        kname, hash_ms = "k_block_walk", stage_ms.get("parse")
     traffic, traffic_src = pmc_traffic(kname, "c4")
     if hash_ms:
         ach = n * comp_exec * W_BLAKE2B_OPS / (hash_ms * 1e-3)
