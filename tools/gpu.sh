@@ -20,6 +20,7 @@
 #   abc4:V[:ARGS]    the same on config 4
 #   env:K=V          export K=V for the tasks that follow (SUF=x: later bench outputs are named <task>x.json)
 #   e2e[:ENV=V,..]   tools/e2e_probe.py (pinned end-to-end signatures) under these settings
+#   benchtrace       the driver's bench command under rocprofv3 --kernel-trace --stats
 #   h2d              tools/h2d_probe.py: pinned H2D rates (whole arrays, chunks, two streams)
 #   e2etrace         tools/e2e_probe.py with two callers (MV_PROBE_TWO) under kernel + memory-copy trace
 #   trace:W          rocprofv3 --kernel-trace --stats of workload W in {c2, c2s1, c2single, c4, c4s1, c5, wal}
@@ -133,6 +134,10 @@ for T in "$@"; do
     e2e)  # e2e[:ENV=V,ENV=V]: the pinned end-to-end probe under these environment settings
       (export ${arg//,/ }; timeout -k 10 300 python tools/e2e_probe.py) >> "$OUT/e2e.log" 2>&1 || { echo "e2e FAILED"; tail -5 "$OUT/e2e.log"; exit 1; }
       tail -1 "$OUT/e2e.log" ;;
+    benchtrace)  # the driver's bench command under rocprofv3 --kernel-trace --stats (the roofline's source)
+      run 900 "$OUT/benchtrace.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/benchtrace" -o run -- python bench.py --gpus 1 --steps 20 --warmup 5
+      grep -E '^\{' "$OUT/benchtrace.log" | tail -1 | cut -c1-200
+      python3 tools/trace_top.py "$OUT/benchtrace" ;;
     h2d)  # tools/h2d_probe.py: pinned H2D rates in the streamed path's copy shapes
       run 300 "$OUT/h2d.log" python tools/h2d_probe.py
       grep "^h2d" "$OUT/h2d.log" ;;
