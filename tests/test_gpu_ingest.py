@@ -136,6 +136,38 @@ def test_statement_kinds_and_ragged_lengths(engine, host_engine):
     assert len({int(s) for s in st}) >= 3
 
 
+def test_every_statement_and_metadata_byte_flipped(engine, host_engine):
+    """One block holding every statement kind -- a Share, Vote Accept, Reject(None),
+    Reject(Some(locator)) and a VoteRange -- with bit 0 and bit 7 of every byte from the statement
+    count to the end flipped, one variant each: tags, vote options, the Some marker, both
+    locators' digest lengths, the share length, the epoch marker and the signature length all
+    change under some flip. Every form's verdict equals the host codec's, and the oracle's on
+    every third variant (types.rs:315-376, data.rs:43-52)."""
+    pks, stakes = small_committee()
+    seeds = [B.authority_seed(a) for a in range(7)]
+    prev = [B.genesis(a) for a in range(7)]
+    inc = [prev[2].reference()] + [prev[x].reference() for x in range(7) if x != 2]  # own first, a quorum
+    loc = B.Locator(prev[3].reference(), 4)
+    sts = [("share", bytes(range(5))), ("accept", loc), ("reject", loc, None), ("reject", loc, loc),
+           ("range", prev[4].reference(), 1, 3)]
+    blk = B.new_with_signer(2, 1, inc, sts, 1, False, 0, seeds[2], O.sign).bincode()
+    lo = 64 + 56 * len(inc)  # the statement count follows the header and the includes
+    out = [blk]
+    for i in range(lo, len(blk)):
+        for bit in (0, 7):
+            b = bytearray(blk)
+            b[i] ^= 1 << bit
+            out.append(bytes(b))
+    st, md, bd = agree(engine, host_engine, out, pks, stakes, 0)
+    assert int(st[0]) == 0
+    for i in range(0, len(out), 3):
+        ost, omd, obd = O.block_verify(out[i], pks, stakes, 0)
+        assert int(st[i]) == ost, i
+        if ost != O.BLOCK_PARSE_ERROR:
+            assert md[i].tobytes() == omd and bd[i].tobytes() == obd, i
+    assert (st == M.BLOCK_PARSE_ERROR).sum() > 20
+
+
 def test_batch_path_through_device_ingest(engine, host_engine, golden):
     """>= MV_BATCH_MIN blocks: device parse feeds the batch equation; blocks rejected before
     the signature check stay out of it (no fallback without a bad signature)."""
