@@ -213,7 +213,10 @@ mv_status mv_dev_ed25519_verify(mv_ctx* ctx, int device, const uint8_t* d_msg, c
  * passing combination with probability <= 2^-127).
  * `d_pk` rows are indexed by item, or by `d_key_idx` (device array) when it is non-NULL; every
  * d_key_idx[i] must then be a row of d_pk (the library cannot bound-check device arrays).
- * Enqueues only; `d_batch_ok` (optional, device, 4 bytes) receives 1 if the combination held. */
+ * Enqueues only; `d_batch_ok` (optional, device, 4 bytes) receives 1 if the combination held
+ * (0 also when dense failures sent the call straight to per-signature verification, see
+ * mv_batch_routes). The call makes `stream` wait only for the engine scratch slot it reuses;
+ * MV_PREP_CHAIN=2 (mv_set_option) also orders its preparation after the previous call's. */
 mv_status mv_dev_ed25519_verify_batch(mv_ctx* ctx, int device, const uint8_t* d_msg, const uint8_t* d_sig,
                                       const uint8_t* d_pk, const uint32_t* d_key_idx, uint32_t n,
                                       uint8_t* d_status, uint32_t* d_batch_ok, void* stream);
