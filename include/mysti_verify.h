@@ -27,6 +27,8 @@
  *                          (wal.rs:226-346): the entry walk and crc check of the WAL replay in
  *                          BlockStore::open (block_store.rs:66)
  *   mv_wal_layout          WalWriter::writev position arithmetic (wal.rs:150-188), host only
+ *   mv_frame_blocks        the block byte strings of received NetworkMessage frames
+ *                          (Network::handle_read_stream, network.rs:400-447), host only
  *
  * Conventions
  *   - The caller owns every buffer passed in and out; they must stay valid for the call.
@@ -199,6 +201,20 @@ mv_status mv_wal_verify(mv_ctx* ctx, const uint8_t* wal, uint64_t size, uint64_t
  * the writer position after them. */
 uint64_t mv_wal_layout(const uint64_t* payload_len, uint64_t n, uint32_t map_bits, uint64_t start,
                        uint64_t* pos /* n */);
+
+/* Host-only helper: the Data<StatementBlock> byte strings inside received network frames
+ * (Network::handle_read_stream, network.rs:400-447: a u32 big-endian size, then
+ * bincode(NetworkMessage), network.rs:36-46; size 0 is a ping followed by 8 bytes). Lists the
+ * blocks of every Blocks / RequestBlocksResponse message in buf[0, len) (u32 tag 1 or 3, u64
+ * count, then u64 length + bytes per block, data.rs:67-96) as offsets into buf and lengths, in
+ * stream order, for mv_verify_blocks on the same buffer (no copy of the bytes); the other
+ * messages and pings are skipped unparsed. Stops before an incomplete trailing frame, and
+ * *consumed (optional) = the bytes of the complete frames. Returns the number of blocks found
+ * (the first `cap` written; cap 0 only counts), or -1 where the reference drops the connection:
+ * a size above MAX_SIZE = 16 MiB (network.rs:216-221), a message tag above 4, or a block count
+ * or length that runs past its frame (a bincode error, network.rs:454-457). */
+int64_t mv_frame_blocks(const uint8_t* buf, uint64_t len, uint64_t* off, uint64_t* blen, uint64_t cap,
+                        uint64_t* consumed);
 
 /* ---- device-resident variants (inputs already in HBM of `device`) ----
  * Pointers are device pointers, 16-byte aligned; `stream` is a hipStream_t (NULL = the

@@ -48,6 +48,7 @@ EXPORTS = [
     "mv_dev_ed25519_sign", "mv_selftest", "mv_block_preimage", "mv_dev_ed25519_verify_batch", "mv_batch_stats",
     "mv_set_stage_timing", "mv_stage_times", "mv_dev_verify_blocks", "mv_batch_counters", "mv_batch_routes", "mv_set_batch_groups",
     "mv_queue_stats", "mv_shard_plan", "mv_crc32", "mv_wal_verify", "mv_wal_layout", "mv_dev_wal_verify",
+    "mv_frame_blocks",
     "mv_dev_crc32", "mv_host_alloc", "mv_host_free", "mv_online_stats", "mv_set_option", "mv_get_option",
 ]
 WAL_OK, WAL_CRC_MISMATCH, WAL_NONZERO_CRC_LEN0, WAL_BAD_LENGTH = range(4)
@@ -111,6 +112,8 @@ def load_library(path: str = LIB_PATH):
     lib.mv_wal_verify.argtypes = [vp, vp, u64, u64, u32, vp, vp, vp, vp, u64, vp]
     lib.mv_wal_layout.argtypes = [vp, u64, u32, u64, vp]
     lib.mv_wal_layout.restype = u64
+    lib.mv_frame_blocks.argtypes = [vp, u64, vp, vp, u64, vp]
+    lib.mv_frame_blocks.restype = ctypes.c_int64
     lib.mv_dev_wal_verify.argtypes = [vp, ctypes.c_int, vp, u64, u64, u32, vp, vp, vp, vp, u64, vp, vp]
     lib.mv_dev_crc32.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp]
     lib.mv_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
@@ -282,6 +285,16 @@ class Engine:
         self._check(self.lib.mv_verify_blocks(self.ctx, _p(buf), _p(offs), _p(lens), n, _p(st), _p(md), _p(bd)),
                     "mv_verify_blocks")
         return st, md, bd
+
+    def verify_frames(self, buf):
+        """Blocks of received NetworkMessage frames (network.rs:400-447) verified in place:
+        mv_frame_blocks lists them, mv_verify_blocks checks them on the same buffer. Returns
+        (status, msg_digest, block_digest, consumed bytes of complete frames)."""
+        buf = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf,
+                                   dtype=np.uint8)
+        offs, lens, consumed = frame_blocks(buf)
+        st, md, bd = self.verify_blocks_packed(buf, offs, lens)
+        return st, md, bd, consumed
 
     # ---- device-resident (torch tensors on the device) ----
     def dev_verify(self, device: int, d_msg, d_sig, d_pk, d_status, stream_handle: int = 0):
@@ -481,6 +494,23 @@ def wal_layout(payload_lens, map_bits: int = WAL_MAP_BITS, start: int = 0):
     pos = np.zeros(max(pl.size, 1), dtype=np.uint64)
     end = lib.mv_wal_layout(_p(pl) if pl.size else None, pl.size, map_bits, start, _p(pos))
     return pos[:pl.size], int(end)
+
+
+def frame_blocks(buf) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Host-only: (offsets, lengths) of the Data<StatementBlock> byte strings inside received
+    NetworkMessage frames (mv_frame_blocks, network.rs:400-447), and the bytes of the complete
+    frames. Raises MvError where the reference would drop the connection."""
+    lib = load_library()
+    b = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf,
+                             dtype=np.uint8)
+    consumed = ctypes.c_uint64(0)
+    n = lib.mv_frame_blocks(_p(b) if b.size else None, b.size, None, None, 0, ctypes.byref(consumed))
+    if n < 0:
+        raise MvError("mv_frame_blocks: a malformed frame stream (the reference drops the connection)")
+    offs = np.zeros(max(n, 1), dtype=np.uint64)
+    lens = np.zeros(max(n, 1), dtype=np.uint64)
+    lib.mv_frame_blocks(_p(b) if b.size else None, b.size, _p(offs), _p(lens), n, ctypes.byref(consumed))
+    return offs[:n], lens[:n], int(consumed.value)
 
 
 def version() -> str:

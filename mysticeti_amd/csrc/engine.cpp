@@ -2997,6 +2997,53 @@ uint64_t mv_wal_layout(const uint64_t* payload_len, uint64_t n, uint32_t map_bit
   return p;
 }
 
+int64_t mv_frame_blocks(const uint8_t* buf, uint64_t len, uint64_t* off, uint64_t* blen, uint64_t cap,
+                        uint64_t* consumed) {
+  constexpr uint64_t kMaxSize = 16ull << 20;  // Network::MAX_SIZE (network.rs:216)
+  constexpr uint64_t kPingRest = 8;           // PING_SIZE 12 - the size word (network.rs:425, 563)
+  auto le = [&](uint64_t p, int bytes) {
+    uint64_t v = 0;
+    for (int k = 0; k < bytes; k++) v |= (uint64_t)buf[p + k] << (8 * k);
+    return v;
+  };
+  if (consumed) *consumed = 0;
+  if (len && !buf) return -1;
+  if (cap && (!off || !blen)) return -1;
+  uint64_t p = 0, found = 0;
+  while (len - p >= 4) {
+    const uint64_t size = ((uint64_t)buf[p] << 24) | ((uint64_t)buf[p + 1] << 16) | ((uint64_t)buf[p + 2] << 8) | buf[p + 3];
+    if (size > kMaxSize) return -1;
+    const uint64_t body = p + 4, need = size ? size : kPingRest;
+    if (len - body < need) break;  // an incomplete frame: wait for more bytes
+    const uint64_t end = body + need;
+    if (size) {
+      if (size < 4) return -1;  // no room for the message tag
+      const uint64_t tag = le(body, 4);
+      if (tag > 4) return -1;
+      if (tag == 1 || tag == 3) {  // Blocks / RequestBlocksResponse: Vec<Data<StatementBlock>>
+        if (end - body < 12) return -1;
+        const uint64_t count = le(body + 4, 8);
+        uint64_t q = body + 12;
+        for (uint64_t k = 0; k < count; k++) {
+          if (end - q < 8) return -1;
+          const uint64_t l = le(q, 8);
+          q += 8;
+          if (l > end - q) return -1;
+          if (found < cap) {
+            off[found] = q;
+            blen[found] = l;
+          }
+          found++;
+          q += l;
+        }
+      }
+    }
+    p = end;
+    if (consumed) *consumed = p;
+  }
+  return (int64_t)found;
+}
+
 mv_status mv_crc32(mv_ctx* ctx, const uint8_t* buf, const uint64_t* off, const uint64_t* len, uint32_t n,
                    uint32_t* out) {
   if (!ctx || (n && (!buf || !off || !len || !out))) return set_err(ctx, MV_E_INVALID_ARG, "bad crc32 args");

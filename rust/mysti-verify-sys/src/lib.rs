@@ -81,6 +81,8 @@ extern "C" {
                          pos: *mut u64, tag: *mut u32, len: *mut u32, status: *mut u8, cap: u64,
                          count: *mut u64) -> i32;
     pub fn mv_wal_layout(payload_len: *const u64, n: u64, map_bits: u32, start: u64, pos: *mut u64) -> u64;
+    pub fn mv_frame_blocks(buf: *const u8, len: u64, off: *mut u64, blen: *mut u64, cap: u64,
+                           consumed: *mut u64) -> i64;
     pub fn mv_dev_ed25519_verify(ctx: *mut mv_ctx, device: i32, d_msg: *const u8, d_sig: *const u8,
                                  d_pk: *const u8, n: u32, d_status: *mut u8, stream: *mut c_void) -> i32;
     pub fn mv_dev_ed25519_verify_batch(ctx: *mut mv_ctx, device: i32, d_msg: *const u8, d_sig: *const u8,

@@ -313,3 +313,36 @@ def test_two_pinned_callers_at_once(engine):
         for b in bufs:
             engine.host_free(b)
     assert int(want[0][77]) != 0 and (np.delete(want[0], 77) == 0).all()
+
+
+def test_frames_verified_in_place_equal_the_blocks(engine, golden):
+    """Received NetworkMessage frames (network.rs:400-447) verified in place: mv_frame_blocks
+    lists the Blocks / RequestBlocksResponse messages' blocks, mv_verify_blocks checks them on the
+    frame buffer. Statuses and digests equal verify_blocks on the same blocks, a tampered block
+    included, with pings and other messages between the frames, at a small and a batch-size
+    count (the online service and the batch path)."""
+    import struct
+
+    import mysticeti_amd as M
+
+    g = golden("blocks_config1.json")
+    pks, stakes, epoch = committee_arrays(g["committee"])
+    engine.set_committee(pks, stakes, epoch)
+    bins = [b.bincode() for b in B.gen_config1(O.sign)]
+    bins[5] = bins[5][:-3] + bytes([bins[5][-3] ^ 1]) + bins[5][-2:]  # a signature byte
+
+    def frame(tag, blks):
+        body = struct.pack("<IQ", tag, len(blks)) + b"".join(struct.pack("<Q", len(b)) + b for b in blks)
+        return struct.pack(">I", len(body)) + body
+
+    for blocks in (bins[:40], bins):
+        stream = b""
+        for k in range(0, len(blocks), 37):
+            stream += frame(1 if k % 2 == 0 else 3, blocks[k:k + 37])
+            stream += struct.pack(">I", 0) + bytes(8)  # a ping
+            stream += struct.pack(">I", 12) + struct.pack("<IQ", 0, k)  # SubscribeOwnFrom
+        st, md, bd, consumed = engine.verify_frames(stream)
+        assert consumed == len(stream)
+        want_st, want_md, want_bd = engine.verify_blocks(blocks)
+        assert (st == want_st).all() and (md == want_md).all() and (bd == want_bd).all()
+        assert int(st[5]) != 0 and (np.delete(st, 5) == 0).all()
