@@ -85,6 +85,26 @@ impl GpuVerifier {
     }
 }
 
+/// The blocks of received network frames (network.rs:400-447: u32 BE size + bincode
+/// NetworkMessage) as (offsets, lengths) into `buf`, and the bytes of the complete frames: a
+/// receiver that reads frames into one buffer passes it and these arrays to mv_verify_blocks
+/// without deserializing. An error where Network::handle_read_stream drops the connection.
+pub fn frame_blocks(buf: &[u8]) -> eyre::Result<(Vec<u64>, Vec<u64>, usize)> {
+    let mut consumed = 0u64;
+    let n = unsafe {
+        sys::mv_frame_blocks(buf.as_ptr(), buf.len() as u64, std::ptr::null_mut(), std::ptr::null_mut(), 0,
+                             &mut consumed)
+    };
+    ensure!(n >= 0, "malformed frame stream");
+    let mut off = vec![0u64; n as usize];
+    let mut len = vec![0u64; n as usize];
+    unsafe {
+        sys::mv_frame_blocks(buf.as_ptr(), buf.len() as u64, off.as_mut_ptr(), len.as_mut_ptr(), n as u64,
+                             &mut consumed)
+    };
+    Ok((off, len, consumed as usize))
+}
+
 /// The error StatementBlock::verify returns for the check the engine reports as failing.
 fn verdict_to_result(block: &StatementBlock, status: u8, digest: &[u8], committee: &Committee) -> eyre::Result<()> {
     let round = block.round();
