@@ -298,6 +298,9 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # the CPU baselines run on rank 0 of a one-GPU run only: the N > 1 lines of a scaling run
+    # report the GPUs alone (and finish sooner); config 5's GPU-vs-CPU latency leg keeps its CPU side
+    cpu_legs = args.cpu_sample > 0 and world == 1
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     # one GPU per rank; a rehearsal with more ranks than GPUs (e.g. 2 ranks on a 1-GPU box) shares
@@ -582,7 +585,7 @@ def main():
         cfg4 = bench_blocks.config4_measure(eng, torch, local_rank, world, dist, n=args.config4_batch,
                                             steps=max(3, min(args.steps, 100)), warmup=max(4, min(args.warmup, 8)),
                                             nstreams=nstreams,
-                                            cpu=args.cpu_sample > 0, host_blocks=args.host_fed_blocks)
+                                            cpu=cpu_legs, host_blocks=args.host_fed_blocks)
         ok = ok and cfg4["correct"]
 
     rss_mark("config4")
@@ -593,7 +596,7 @@ def main():
         import bench_wal
 
         walr = bench_wal.wal_measure(eng, torch, local_rank, world, dist, n=args.wal_entries,
-                                     steps=max(3, min(args.steps // 4, 50)), warmup=1, cpu=args.cpu_sample > 0)
+                                     steps=max(3, min(args.steps // 4, 50)), warmup=1, cpu=cpu_legs)
         ok = ok and walr["correct"]
 
     rss_mark("wal")
@@ -614,7 +617,7 @@ def main():
     rss_mark("config5")
     progress("config5 done")
     cpu = None
-    if rank == 0 and args.cpu_sample > 0:
+    if rank == 0 and cpu_legs:
         cpu = cpu_baseline(d_pk.cpu().numpy(), d_sig.cpu().numpy(), msg_h, min(args.cpu_sample, n))
         rss_mark("cpu_baseline")
     # per-rank peak host RSS and HBM in use (all ranks; the line must hold at 8 ranks per node)

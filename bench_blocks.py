@@ -454,7 +454,7 @@ def config4_measure(eng, torch, local_rank, world, dist, n, steps, warmup, nstre
     comp_alg = -(-pre_len // 128) + -(-(pre_len + 64) // 128)
     hash_ms = stage_ms.get("hash")
     cpu_res = None
-    if cpu and int(os.environ.get("RANK", "0")) == 0:  # the CPU baseline: rank 0 at any N
+    if cpu and int(os.environ.get("RANK", "0")) == 0:  # the CPU baseline: rank 0 (bench.py asks at N = 1 only)
         lib = _oracle_native()
         comm = _Committee(lib, pks, stakes)
         threads, share_src = _cpu_threads()
