@@ -9,8 +9,8 @@
 // How: the lane walks its block's bincode front to back (bincode 1.3.3 defaults, data.rs:43-52;
 // types.rs:93-114 StatementBlock) and emits the signed pre-image (crypto.rs:85-128 with the
 // CryptoHash encodings of crypto.rs:150-170, types.rs:661-691, 751-755) piece by piece into its
-// own LDS row (blake2b_lane.hip's k_b2_walk pieces: one element, or 64 bytes of a Share, per
-// piece), hashing each 128-byte block as soon as it is complete. The checks of
+// own LDS row (one piece per element, or per 64 bytes of a Share's payload, each read from one
+// 80-byte window), hashing each 128-byte block as soon as it is complete. The checks of
 // StatementBlock::verify that depend on the bincode (types.rs:333-362 includes, 440-460
 // VoteRange, threshold_clock.rs:12-35) run on the same walk. The two digests share their
 // common prefix as in k_b2_lane (Plan<true>), but the schedule is found on the way: the block
