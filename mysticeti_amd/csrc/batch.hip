@@ -709,6 +709,9 @@ __global__ void __launch_bounds__(FINE_NT) k_fine_sort_lds(const unsigned long l
 #ifndef MV_BUCKET_OCC
 #define MV_BUCKET_OCC 3
 #endif
+#ifndef MV_BUCKET_PF2
+#define MV_BUCKET_PF2 1  // k_bv_bucket_bal: unconditional point prefetch (0: the old branch, A/B)
+#endif
 __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket(const uint4* __restrict__ pts, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ ents, uint32_t ngroups, uint32_t seg,
                                                    uint32_t nw, uint4* __restrict__ segV, uint4* __restrict__ segT) {
@@ -835,6 +838,9 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
   p3_identity(T);
   uint4 q[7];
   uint32_t ent = ents[lo];
+#if MV_BUCKET_PF2
+  uint32_t ent_n = ents[min(lo + 1, hi - 1)];  // the entry after the one in flight
+#endif
   {
     const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
 #pragma unroll
@@ -844,12 +850,25 @@ __global__ void __launch_bounds__(256, MV_BUCKET_OCC) k_bv_bucket_bal(const uint
     precomp pc;
     quads_to_precomp(pc, q);
     const bool neg = ent & 1u;
+#if MV_BUCKET_PF2
+    // next point in flight during this add, loaded unconditionally (the last lap reloads entry
+    // hi - 1): a load under a branch made the compiler copy the quads into the loop's registers
+    // inside the branch, waiting on the loads at once; and the entry index one lap further ahead
+    ent = ent_n;
+    ent_n = ents[min(x + 2, hi - 1)];
+    {
+      const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
+#pragma unroll
+      for (int i = 0; i < 7; i++) q[i] = p[i];
+    }
+#else
     if (x + 1 < hi) {  // next point in flight during this add
       ent = ents[x + 1];
       const uint4* p = pts + (size_t)(ent >> 1) * PT_QUADS;
 #pragma unroll
       for (int i = 0; i < 7; i++) q[i] = p[i];
     }
+#endif
     precomp_cneg(pc, neg);
     p1p1 t;
     p3_add_precomp(t, T, pc);

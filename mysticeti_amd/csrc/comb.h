@@ -24,7 +24,8 @@ MV_DEV void ct_load(uint4 (&q)[7], const uint4* row, int digit) {
 }
 
 // acc = sum over rows i in [r0, r1) of C[i][digit i of sd] (signed radix-256 digits);
-// each entry is loaded one addition ahead
+// each entry is loaded one addition ahead, unconditionally (the last lap reloads row r1 - 1): a
+// load under a branch has the compiler copy the quads inside the branch, waiting on them at once
 MV_DEV void ct_sum(p3& acc, const uint4* tab, const uint32_t sd[8], int r0, int r1) {
   p3_identity(acc);
   uint4 q[7];
@@ -35,10 +36,9 @@ MV_DEV void ct_sum(p3& acc, const uint4* tab, const uint32_t sd[8], int r0, int 
     precomp pc;
     quads_to_precomp(pc, q);
     const bool neg = dg < 0;
-    if (i + 1 < r1) {
-      dg = digit256(sd, i + 1);
-      ct_load(q, tab + (size_t)(i + 1) * CT_ROW, dg);
-    }
+    const int in = i + 1 < r1 ? i + 1 : r1 - 1;
+    dg = digit256(sd, in);
+    ct_load(q, tab + (size_t)in * CT_ROW, dg);
     precomp_cneg(pc, neg);
     p1p1 t;
     p3_add_precomp(t, acc, pc);

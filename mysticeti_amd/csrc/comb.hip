@@ -283,23 +283,24 @@ MV_DEV void q_entry_fix(fe& op, int digit) {
   if (c == 2) fe_set(op, 2);
 }
 // sum over rows [r0, r1) of the comb entries of the signed radix-256 digits sd, coordinate form;
-// the entries of the next two rows are in flight during an addition
+// the entries of the next two rows are in flight during an addition (loaded unconditionally, rows
+// past r1 - 1 clamped to it: loads under a branch are waited on inside it, see ct_sum)
 MV_DEV void q_ct_sum(fe& v, const uint4* tab, const uint32_t sd[8], int r0, int r1) {
   qp_identity(v);
   fe op0, op1;
-  int d0 = digit256(sd, r0), d1 = r0 + 1 < r1 ? digit256(sd, r0 + 1) : 0;
+  const int r01 = r0 + 1 < r1 ? r0 + 1 : r1 - 1;
+  int d0 = digit256(sd, r0), d1 = digit256(sd, r01);
   q_entry(op0, tab + (size_t)r0 * CT_ROW, d0);
-  if (r0 + 1 < r1) q_entry(op1, tab + (size_t)(r0 + 1) * CT_ROW, d1);
+  q_entry(op1, tab + (size_t)r01 * CT_ROW, d1);
 #pragma unroll 1
   for (int i = r0; i < r1; i++) {
     fe cur = op0;
     const int dcur = d0;
     op0 = op1;
     d0 = d1;
-    if (i + 2 < r1) {
-      d1 = digit256(sd, i + 2);
-      q_entry(op1, tab + (size_t)(i + 2) * CT_ROW, d1);
-    }
+    const int in = i + 2 < r1 ? i + 2 : r1 - 1;
+    d1 = digit256(sd, in);
+    q_entry(op1, tab + (size_t)in * CT_ROW, d1);
     q_entry_fix(cur, dcur);
     qp_madd(v, cur);
   }
