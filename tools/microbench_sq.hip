@@ -15,8 +15,8 @@
 // floor) and (b) on the full chip, 8 waves per SIMD (throughput: issue slots per squaring =
 // device cycles / 2 per SIMD over the wave-squarings it ran, at the clock the kernel saw, from
 // s_memtime). Result (profiles/r06/microbench_sq.jsonl): fe32 costs 1.8x fe29 on the full chip
-// (373 against 203 slots) and 2.7x on a lone wave's chain, so the 9 x 29 form stays (fe25: see
-// the same file). The chains start from the same values; their results are compared mod p
+// (373 against 203 slots) and 2.7x on a lone wave's chain, fe25 1.24x (252 slots) and 1.2x, so
+// the 9 x 29 form stays. The chains start from the same values; their results are compared mod p
 // (canonical encodings).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I mysticeti_amd/csrc tools/microbench_sq.hip -o tools/microbench_sq
 #include <hip/hip_runtime.h>
